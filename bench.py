@@ -1,0 +1,212 @@
+#!/usr/bin/env python3
+"""Benchmark: Mrays/s (primary + secondary) of the path-tracing hot path on MI355X.
+
+Workload (BASELINE.json configs[1]): scenes/spot.xml — spot (5,856 triangles)
+on a floor quad under a quad light, 1920x1080, 64 samples per pixel per GPU, maxDepth 3.
+A step = one 64-spp-per-GPU frame: every rank traces its disjoint sample partition into an FP64
+accumulator, then (N > 1) one RCCL sum-reduce of that [3][w*h] buffer to rank 0. Per-GPU work is
+fixed as N grows ("scaling": "weak"): the N-GPU job renders 64*N spp of the same frame.
+
+Rays counted = primary + extension (closest-hit queries actually traced) + shadow rays, read
+from the kernel's own counters. Inputs (scene, BVH) are resident in HBM before timing starts.
+
+Extra objects on the JSON line:
+  roofline      the trace kernel's algorithmic bytes per launch / its HIP-event duration vs HBM
+                8 TB/s; bytes per ray from the kernel's traversal counters
+  cpu_baseline  the CPU oracle (FP64 restatement of the reference algorithm) timed on this host
+                on a bounded random sample of the same workload's paths (rank 0, N = 1 only)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+SPOT_SCENE = os.path.join(ROOT, "scenes", "spot.xml")
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--spp", type=int, default=64, help="samples per pixel per GPU per step")
+    ap.add_argument("--scene", default=SPOT_SCENE)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-stats", action="store_true", help="skip the traversal-counter pass")
+    return ap.parse_args()
+
+
+def relaunch_distributed(args):
+    """`python bench.py --gpus N` without torchrun: start torchrun as a child (before any GPU
+    use in this process) and exit with its status."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def cpu_baseline(arrays, spp, seed, budget_s):
+    """Oracle (port) on random (pixel, sample) paths of the same workload, time-boxed."""
+    import numpy as np
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import pyoracle
+    pyoracle.build()
+    nthreads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    o = pyoracle.OracleScene(arrays)
+    rng = np.random.default_rng(7)
+    rays = paths = 0.0
+    t_total = 0.0
+    batch = 20000
+    while t_total < budget_s:
+        px = rng.integers(0, arrays.width, batch)
+        py = rng.integers(0, arrays.height, batch)
+        sm = rng.integers(0, spp, batch)
+        _, st = o.paths(px, py, sm, seed, nthreads=nthreads)
+        rays += st[0] + st[1] + st[2]
+        paths += st[3]
+        t_total += st[7]
+    o.close()
+    return {"value": round(rays / t_total / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+            "sample": f"{int(paths)} random (pixel, sample) paths of the same 1920x1080x{spp} workload "
+                      f"({int(rays)} rays, {t_total:.1f} s), oracle/mfx_oracle.c strict FP64 restatement, "
+                      f"OpenMP {nthreads} threads"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(relaunch_distributed(args))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import numpy as np
+    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS
+    from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
+    from mafrixraytracing_amd.scene_io import load_scene_file
+
+    dist = torch = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group(backend="nccl")  # RCCL over xGMI
+
+    arrays = load_scene_file(args.scene)
+    W, H = arrays.width, arrays.height
+    npix = W * H
+    spp_step = args.spp * world
+    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, part_index=rank, part_count=world)
+    acc = None
+    if world > 1:
+        acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
+        ctx.accum_attach(acc.data_ptr(), acc.numel() * 8)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+            torch.cuda.synchronize()
+        ctx.sync()
+
+    def step(k):
+        ctx.accum_clear()
+        ctx.trace_accumulate(spp_step, k * spp_step)
+        ctx.sync()
+        if world > 1:
+            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
+            torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    t0 = time.perf_counter()
+    rays = 0.0
+    kms = []
+    for k in range(args.steps):
+        step(args.warmup + k)
+        c = ctx.ray_counts()
+        rays += c[0] + c[1] + c[2]
+        kms.append(ctx.last_trace_ms())
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        r = torch.tensor([rays], dtype=torch.float64, device=f"cuda:{local}")
+        dist.all_reduce(r, op=dist.ReduceOp.SUM)
+        rays_all = float(r.item())
+    else:
+        rays_all = rays
+    rays_per_launch = rays / args.steps
+    kernel_ms = float(np.mean(kms))
+
+    result = None
+    if rank == 0:
+        # traversal counters (separate, untimed pass at 1 spp of the same frame)
+        bray = None
+        stats = None
+        if not args.no_stats:
+            with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS) as sc:
+                sc.trace_accumulate(1, 10 ** 6)
+                s = sc.ray_counts()
+            r = s[0] + s[1] + s[2]
+            stats = {"node_visits_per_ray": s[4] / r, "cluster_visits_per_ray": s[5] / r,
+                     "prim_tests_per_ray": s[6] / r, "rays_per_path": r / s[0]}
+            # 64 B per internal-node fetch, 64 B per reference-leaf (cluster) record,
+            # 84 B per primitive test (80 B FP64 slot + 4 B info), 64 B ray record in + out
+            bray = 64.0 * stats["node_visits_per_ray"] + 64.0 * stats["cluster_visits_per_ray"] + \
+                84.0 * stats["prim_tests_per_ray"] + 64.0
+        roofline = None
+        if bray is not None:
+            achieved = rays_per_launch * bray / (kernel_ms / 1e3) / 1e9
+            traffic = None
+            tf = os.path.join(ROOT, "profiles", "traffic_spot_1080p.json")
+            if os.path.exists(tf) and world == 1:
+                with open(tf) as f:
+                    traffic = json.load(f).get("hbm_bytes_per_launch")
+            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                        "kernel": "trace_kernel", "kernel_ms": round(kernel_ms, 3),
+                        "bytes_per_ray": round(bray, 1), "rays_per_launch": int(rays_per_launch),
+                        "counters": {k: round(v, 3) for k, v in stats.items()}}
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
+        value = rays_all / elapsed / 1e6
+        result = {
+            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic",
+            "config": {"workload": f"C2 spot ({len(arrays.prims) - 1} tris) + floor/light stage, {W}x{H}, "
+                                   f"{args.spp} spp per GPU per step",
+                       "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
+                       "spp_per_gpu": args.spp, "global_spp_per_step": spp_step, "max_depth": 3,
+                       "parallelism": f"sample-partition x{world}" + (" + RCCL reduce" if world > 1 else "")},
+            "roofline": roofline, "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

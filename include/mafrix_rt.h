@@ -1,0 +1,190 @@
+/*
+ * mafrix_rt.h — C ABI of the MI355X (gfx950) path-tracing hot path.
+ *
+ * This is the drop-in boundary for NAIVEddd/MafrixRaytracing's F# EngineCore hot path:
+ * the F# `Scene` constructor and `Scene.Render` (EngineCore/Scene/Scene.fs:298-333) bind these
+ * entry points through P/Invoke instead of running `PixelIntegrator`
+ * (EngineCore/Core/Integrator/Integrators.fs:143-172) on the .NET thread pool.
+ *
+ * Conventions
+ *  - extern "C", cdecl, plain pointers and sizes, no C++ or torch types.
+ *  - Every struct is blittable (sequential layout, natural alignment) so .NET can pin it.
+ *  - Return value: 0 on success, a negative MFX_E_* code on failure; mfx_last_error()
+ *    gives a thread-local message. Nothing ever falls back to a CPU path.
+ *  - One mfx_ctx is driven by one host thread at a time (the reference calls Sample from its
+ *    single render thread, Film.fs:32, and fans out internally, Integrators.fs:164).
+ *  - All calls are synchronous: when a call returns, its output buffer is complete.
+ *
+ * Numerics contract: every decision the reference makes in FP64
+ * (camera ray, AABB slab test, Möller–Trumbore, sphere roots, rejection-sampled hemisphere,
+ * light sample point, shadow distance) is made in FP64 with the reference's operation order
+ * and no FMA contraction, so GPU paths follow the CPU oracle's paths bit for bit; the
+ * BVH traversal that *finds* candidate leaves runs in FP32 with conservatively widened boxes.
+ */
+#ifndef MAFRIX_RT_H
+#define MAFRIX_RT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MFX_ABI_VERSION 1
+
+/* error codes */
+#define MFX_OK 0
+#define MFX_E_INVALID (-1)   /* bad argument / malformed scene */
+#define MFX_E_DEVICE (-2)    /* HIP runtime error, no device, kernel fault */
+#define MFX_E_NOMEM (-3)     /* host or device allocation failed */
+#define MFX_E_STATE (-4)     /* call out of order (e.g. render before create) */
+
+/* Primitive kinds: the three IHitable structs the reference's Bvh holds (BvhNode.fs:24). */
+#define MFX_PRIM_TRIANGLE 0  /* Triangle(v0,v1,v2,mat)        Core/Shape/Trangle.fs:107-119 */
+#define MFX_PRIM_RECT 1      /* Rect(v0,v1,v2,v3,mat) = two triangles (v0,v1,v2),(v0,v2,v3)  Rect.fs:11-20 */
+#define MFX_PRIM_SPHERE 2    /* Sphere(center,radius,mat)     Core/Shape/Sphere.fs:9-16 */
+
+/* One primitive of the scene, in the order of Scene state.shapes (Scene.fs:168-177, 301).
+ * The order matters: it is the index space Bvh.Build sorts (BvhNode.fs:25).
+ *  TRIANGLE: p[0..2] = v0,v1,v2
+ *  RECT:     p[0..3] = v0,v1,v2,v3 (the four OBJ face vertices, ObjModelLoader.fs:84-89)
+ *  SPHERE:   p[0] = center, p[1][0] = radius                                              */
+typedef struct mfx_prim {
+    int32_t kind;
+    int32_t material; /* index into mfx_scene_desc.albedo (MaterialManager order, IMaterial.fs:20-35) */
+    double p[4][3];
+} mfx_prim; /* 104 bytes */
+
+/* NewAreaLight(p0,p1,p2,p3,normal,intensity) (Core/Lights/Light.fs:31-40), as built by
+ * Scene.fs:193 from a Rect: (trig1.v0, trig1.v1, trig1.v2, trig2.v2, trig1.normal, I). */
+typedef struct mfx_quad_light {
+    double p[4][3];
+    double normal[3];
+    double intensity[3];
+} mfx_quad_light;
+
+/* PinholeCamera(pos, dir, fov, aspectRatio) (Core/Camera.fs:122-133). */
+typedef struct mfx_pinhole {
+    double position[3];
+    double direction[3];
+    double fov;    /* degrees, as in Scene.xml; effective horizontal FOV is fov/2 (Camera.fs:125) */
+    double aspect; /* aspectratio attribute; NOT derived from the film size (Scene.fs:61-72) */
+} mfx_pinhole;
+
+/* The scene a `Scene` is constructed from (Scene.fs:298-313). Deep-copied by mfx_create. */
+typedef struct mfx_scene_desc {
+    const mfx_prim* prims;
+    int64_t nprims;
+    const double* albedo; /* [nmat][3] Lambert albedo per MaterialManager slot (Material.fs:29-37);
+                             Metal -> its albedo (Material.fs:68), SpecularTransmission -> 0 (:121) */
+    int32_t nmat;
+    int32_t width;     /* Film width  (Scene.fs:201-211) */
+    int32_t height;    /* Film height */
+    int32_t max_depth; /* PathIntegrator maxDepth; the reference hard-codes 3 (Scene.fs:304) */
+    mfx_quad_light light;
+    mfx_pinhole camera;
+} mfx_scene_desc;
+
+/* Context options. */
+typedef struct mfx_options {
+    uint64_t seed;      /* counter-RNG seed; the reference uses unseeded System.Random */
+    int32_t device;     /* HIP device ordinal for this context */
+    int32_t flags;      /* MFX_F_* */
+    int32_t part_index; /* this context renders sample partition part_index of part_count */
+    int32_t part_count; /* (multi-GPU: one context per rank; partitions are disjoint sample sets) */
+} mfx_options;
+
+#define MFX_F_NONE 0
+#define MFX_F_COUNT_STATS 1 /* count traversal node/leaf/prim visits (slower; for the roofline model) */
+
+typedef struct mfx_ctx mfx_ctx;
+
+/* ---- lifetime ------------------------------------------------------------------------- */
+
+/* Replaces `new Scene(state)` (Scene.fs:298-313): builds the reference's heap BVH leaf grouping
+ * (BvhNode.fs:24-61), the GPU traversal BVH over it, uploads everything to HBM.            */
+int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out);
+void mfx_destroy(mfx_ctx* ctx);
+
+/* ---- the reference's render API --------------------------------------------------------- */
+
+/* == IPixelIntegrator.Sample(spp) (IIntegrator.fs:35-40, Integrators.fs:161-172):
+ * renders spp fresh samples per pixel and writes their mean as Color[w,h], x-major:
+ * frame[(i*h + j)*4 + {0,1,2,3}] = r,g,b,1.0 for column i, row j (row 0 = top).
+ * Successive calls draw successive global sample indices (the reference's RNG keeps
+ * running between calls).                                                                  */
+int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
+
+/* == Film.GetFrame(integrator, spp) + Scene.PostProcessAndToScreenBuffer
+ * (Film.fs:18-34, Scene.fs:315-333): adds spp samples per pixel to the film, then writes the
+ * progressive mean through ACES -> sqrt -> int(255.99 c) as RGBA8, y-major:
+ * rgba[(y*w + x)*4 + {0,1,2,3}]. `Scene.Render(delta, buffer)` is this call with spp = 1.
+ * rgba may be NULL (accumulate only).                                                      */
+int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
+
+/* == Film.Reset (Film.fs:26-30): zero the film accumulator and its frame count. */
+int mfx_reset(mfx_ctx* ctx);
+
+/* Film mean (target texture, Film.fs:23) as x-major RGBA doubles. */
+int mfx_film_mean(mfx_ctx* ctx, double* frame_xmajor_rgba);
+
+/* ---- lower-level entry points (multi-GPU composition, benchmarking) -------------------- */
+
+/* Adds, for global samples [sample_base, sample_base + spp) of this context's partition,
+ * the per-pixel radiance sums into the context's device accumulator (FP64, 3 planes of w*h,
+ * plane-major, x-major pixels). Does not synchronise; mfx_sync() does.                      */
+int mfx_trace_accumulate(mfx_ctx* ctx, int32_t spp, int64_t sample_base);
+int mfx_accum_clear(mfx_ctx* ctx);
+/* Device pointer + byte size of the FP64 accumulator (for an RCCL reduce across ranks).    */
+int mfx_accum_device_ptr(mfx_ctx* ctx, void** dptr, int64_t* nbytes);
+/* Use caller-owned device memory (>= the size above, on this context's device) as the
+ * accumulator — e.g. a buffer an RCCL reduce then works on in place; NULL restores the
+ * context's own buffer. The caller keeps it alive until detached or mfx_destroy.            */
+int mfx_accum_attach(mfx_ctx* ctx, void* dptr, int64_t nbytes);
+/* Copy accumulator / inv_count to host as x-major RGBA doubles (alpha = 1).                */
+int mfx_accum_read_mean(mfx_ctx* ctx, double inv_count, double* frame_xmajor_rgba);
+int mfx_sync(mfx_ctx* ctx);
+/* The HIP stream (hipStream_t) the context launches on, for event timing by the caller.   */
+int mfx_stream(mfx_ctx* ctx, void** stream);
+
+/* Device time (ms) of the last trace kernel launch, from HIP events recorded around it on the
+ * context's stream (waits for that launch to finish).                                       */
+int mfx_last_trace_ms(mfx_ctx* ctx, double* ms);
+
+/* Ray counters of the last mfx_trace_accumulate / mfx_sample call:
+ * out[0] = primary, out[1] = extension (closest-hit queries actually traced, excluding the
+ * reference's discarded depth -1 query), out[2] = shadow, out[3] = paths,
+ * out[4] = internal-node visits, out[5] = cluster (reference leaf) visits, out[6] = prim tests
+ * (out[4..6] only with MFX_F_COUNT_STATS).                                                 */
+int mfx_ray_counts(mfx_ctx* ctx, double out[8]);
+
+/* ---- query entry points (parity tests of the BVH/intersection layer) ----------------- */
+
+/* Closest hit, == Bvh.Hit(ray, tmin, tmax) (BvhNode.fs:62-83) for n rays given as
+ * rays[k*6 + 0..2] = origin, [3..5] = unit direction. Outputs t (0 when no hit), prim index
+ * (-1 when no hit; index into the mfx_prim array), and the hit normal.                      */
+int mfx_closest_hit(mfx_ctx* ctx, int64_t n, const double* rays, double tmin, double tmax,
+                    double* t_out, int32_t* prim_out, double* normal_out);
+/* Shadow query, == Bvh.Hit(...).hit with per-ray tmax: occluded[k] = 1/0.                  */
+int mfx_any_hit(mfx_ctx* ctx, int64_t n, const double* rays, double tmin, const double* tmax,
+                int32_t* occluded_out);
+
+/* Reference heap-BVH leaf grouping used for the exact leaf semantics (BvhNode.fs:24-61):
+ * indices[nprims] after Subdivide; leaf_first/leaf_count per reference leaf in heap order.  */
+int mfx_ref_leaves(mfx_ctx* ctx, int32_t* indices_out, int32_t* leaf_first_out,
+                   int32_t* leaf_count_out, int32_t* nleaves_out);
+
+/* Device FP64 self-test: computes a/b, sqrt(a) on the GPU for n pairs (bit-exactness check
+ * of the device math the numerics contract relies on).                                      */
+int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* b,
+                      double* div_out, double* sqrt_out);
+
+/* ---- misc -------------------------------------------------------------------------------- */
+const char* mfx_last_error(void);
+int mfx_abi_version(void);
+int mfx_device_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MAFRIX_RT_H */

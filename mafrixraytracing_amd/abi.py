@@ -1,0 +1,170 @@
+"""ctypes mirror of include/mafrix_rt.h and the loader for libmafrix_rt.so.
+
+This is the Python stand-in for the F# P/Invoke declarations a maintainer adds to
+EngineCore/Library.fs: the same structs, the same entry points.
+The library is the HIP build for gfx950; there is no CPU fallback — loading fails loudly
+if the shared object is missing.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+import numpy as np
+
+MFX_PRIM_TRIANGLE = 0
+MFX_PRIM_RECT = 1
+MFX_PRIM_SPHERE = 2
+
+MFX_F_NONE = 0
+MFX_F_COUNT_STATS = 1
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
+
+
+class MfxPrim(C.Structure):
+    _fields_ = [("kind", C.c_int32), ("material", C.c_int32), ("p", (C.c_double * 3) * 4)]
+
+
+class MfxQuadLight(C.Structure):
+    _fields_ = [("p", (C.c_double * 3) * 4), ("normal", C.c_double * 3), ("intensity", C.c_double * 3)]
+
+
+class MfxPinhole(C.Structure):
+    _fields_ = [("position", C.c_double * 3), ("direction", C.c_double * 3),
+                ("fov", C.c_double), ("aspect", C.c_double)]
+
+
+class MfxSceneDesc(C.Structure):
+    _fields_ = [("prims", C.POINTER(MfxPrim)), ("nprims", C.c_int64),
+                ("albedo", C.POINTER(C.c_double)), ("nmat", C.c_int32),
+                ("width", C.c_int32), ("height", C.c_int32), ("max_depth", C.c_int32),
+                ("light", MfxQuadLight), ("camera", MfxPinhole)]
+
+
+class MfxOptions(C.Structure):
+    _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("flags", C.c_int32),
+                ("part_index", C.c_int32), ("part_count", C.c_int32)]
+
+
+assert C.sizeof(MfxPrim) == 104
+
+# numpy structured dtype with the same layout as mfx_prim (for building big prim arrays fast)
+PRIM_DTYPE = np.dtype([("kind", "<i4"), ("material", "<i4"), ("p", "<f8", (4, 3))], align=True)
+assert PRIM_DTYPE.itemsize == 104
+
+
+class SceneArrays:
+    """Owns the numpy buffers an MfxSceneDesc points into (keeps them alive)."""
+
+    def __init__(self, prims: np.ndarray, albedo: np.ndarray, light: dict, camera: dict,
+                 width: int, height: int, max_depth: int = 3):
+        self.prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+        self.albedo = np.ascontiguousarray(albedo, dtype=np.float64).reshape(-1, 3)
+        self.light = light
+        self.camera = camera
+        self.width = int(width)
+        self.height = int(height)
+        self.max_depth = int(max_depth)
+
+    def desc(self) -> MfxSceneDesc:
+        d = MfxSceneDesc()
+        d.prims = self.prims.ctypes.data_as(C.POINTER(MfxPrim))
+        d.nprims = len(self.prims)
+        d.albedo = self.albedo.ctypes.data_as(C.POINTER(C.c_double))
+        d.nmat = len(self.albedo)
+        d.width, d.height, d.max_depth = self.width, self.height, self.max_depth
+        for k in range(4):
+            for c in range(3):
+                d.light.p[k][c] = float(self.light["p"][k][c])
+        for c in range(3):
+            d.light.normal[c] = float(self.light["normal"][c])
+            d.light.intensity[c] = float(self.light["intensity"][c])
+            d.camera.position[c] = float(self.camera["position"][c])
+            d.camera.direction[c] = float(self.camera["direction"][c])
+        d.camera.fov = float(self.camera["fov"])
+        d.camera.aspect = float(self.camera["aspect"])
+        return d
+
+    def with_film(self, width: int, height: int) -> "SceneArrays":
+        return SceneArrays(self.prims, self.albedo, self.light, self.camera, width, height, self.max_depth)
+
+
+_P = C.POINTER
+_dp = _P(C.c_double)
+_ip = _P(C.c_int32)
+
+
+def _bind(lib):
+    sig = {
+        "mfx_create": (C.c_int, [_P(MfxSceneDesc), _P(MfxOptions), _P(C.c_void_p)]),
+        "mfx_destroy": (None, [C.c_void_p]),
+        "mfx_sample": (C.c_int, [C.c_void_p, C.c_int32, _dp]),
+        "mfx_render_rgba8": (C.c_int, [C.c_void_p, C.c_int32, _P(C.c_uint8)]),
+        "mfx_reset": (C.c_int, [C.c_void_p]),
+        "mfx_film_mean": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_trace_accumulate": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
+        "mfx_accum_clear": (C.c_int, [C.c_void_p]),
+        "mfx_accum_device_ptr": (C.c_int, [C.c_void_p, _P(C.c_void_p), _P(C.c_int64)]),
+        "mfx_accum_read_mean": (C.c_int, [C.c_void_p, C.c_double, _dp]),
+        "mfx_accum_attach": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
+        "mfx_sync": (C.c_int, [C.c_void_p]),
+        "mfx_stream": (C.c_int, [C.c_void_p, _P(C.c_void_p)]),
+        "mfx_ray_counts": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_last_trace_ms": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_closest_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, C.c_double, _dp, _ip, _dp]),
+        "mfx_any_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, _dp, _ip]),
+        "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
+        "mfx_fp64_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _dp, _dp]),
+        "mfx_last_error": (C.c_char_p, []),
+        "mfx_abi_version": (C.c_int, []),
+        "mfx_device_count": (C.c_int, []),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+EXPORTED_SYMBOLS = [
+    "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_reset", "mfx_film_mean",
+    "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
+    "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
+    "mfx_fp64_selftest", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+]
+
+_lib = None
+
+
+def load_library(path: str | None = None):
+    """Load libmafrix_rt.so (the HIP build). Raises if it is missing — no fallback exists."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(f"mafrix_rt native library not built: {p} (run __graft_entry__.build())")
+    lib = _bind(C.CDLL(p, mode=C.RTLD_GLOBAL))
+    if path is None:
+        _lib = lib
+    return lib
+
+
+class MfxError(RuntimeError):
+    pass
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = load_library().mfx_last_error()
+        raise MfxError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+
+
+def dptr(a: np.ndarray):
+    return a.ctypes.data_as(_dp)
+
+
+def iptr(a: np.ndarray):
+    return a.ctypes.data_as(_ip)

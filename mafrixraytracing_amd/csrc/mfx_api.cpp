@@ -1,0 +1,411 @@
+// mfx_api.cpp — the extern "C" boundary (include/mafrix_rt.h).
+//
+// One mfx_ctx = one `Scene` on one GPU: the scene images live in HBM from mfx_create until
+// mfx_destroy; every render call is a single persistent-kernel launch plus a small film/post
+// kernel, all on the context's own HIP stream. No call falls back to a CPU path.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/mafrix_rt.h"
+#include "mfx_device.h"
+#include "mfx_scene.h"
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHECK(expr)                                                                               \
+    do {                                                                                             \
+        hipError_t _e = (expr);                                                                      \
+        if (_e != hipSuccess) return fail(MFX_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+    } while (0)
+
+template <typename T>
+hipError_t upload(T** dptr, const std::vector<T>& v) {
+    size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
+    hipError_t e = hipMalloc((void**)dptr, bytes);
+    if (e != hipSuccess) return e;
+    if (!v.empty()) e = hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+    return e;
+}
+}  // namespace
+
+struct mfx_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    MfxHostScene host;
+    MfxNode* d_nodes = nullptr;
+    MfxCluster* d_clusters = nullptr;
+    int32_t* d_pinfo = nullptr;
+    MfxSlot* d_slots = nullptr;
+    MfxShade* d_shade = nullptr;
+    double* d_albedo = nullptr;
+    double* d_accum = nullptr;   // [3][npix] (the active accumulator)
+    double* d_accum_own = nullptr;
+    double* d_film = nullptr;    // [3][npix]
+    double* d_frame = nullptr;   // [npix][4] staging for x-major outputs
+    uint8_t* d_rgba = nullptr;   // [npix][4]
+    unsigned long long* d_work = nullptr;
+    unsigned long long* d_counters = nullptr;  // [8]
+    uint64_t seed = 0;
+    int flags = 0;
+    int part_index = 0, part_count = 1;
+    int64_t next_sample = 0;
+    double frame_count = 0.0;
+    int grid = 0;
+    int stack_size = 1;
+    int64_t npix = 0;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr;
+    bool ev_valid = false;
+};
+
+static void free_ctx(mfx_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    void* bufs[] = {c->d_nodes, c->d_clusters, c->d_pinfo, c->d_slots, c->d_shade, c->d_albedo, c->d_accum_own,
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters};
+    for (void* b : bufs)
+        if (b) (void)hipFree(b);
+    if (c->ev0) (void)hipEventDestroy(c->ev0);
+    if (c->ev1) (void)hipEventDestroy(c->ev1);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+}
+
+extern "C" {
+
+const char* mfx_last_error(void) { return g_err.c_str(); }
+int mfx_abi_version(void) { return MFX_ABI_VERSION; }
+
+int mfx_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out) {
+    if (!scene || !opt || !out) return fail(MFX_E_INVALID, "mfx_create: null argument");
+    *out = nullptr;
+    if (opt->part_count < 1 || opt->part_index < 0 || opt->part_index >= opt->part_count)
+        return fail(MFX_E_INVALID, "mfx_create: bad sample partition");
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    if (opt->device < 0 || opt->device >= ndev) return fail(MFX_E_DEVICE, "mfx_create: no such HIP device");
+    mfx_ctx* c = new mfx_ctx();
+    std::string err;
+    if (!mfx_build_scene(scene, c->host, err)) {
+        delete c;
+        return fail(MFX_E_INVALID, "mfx_create: " + err);
+    }
+    c->device = opt->device;
+    c->seed = opt->seed;
+    c->flags = opt->flags;
+    c->part_index = opt->part_index;
+    c->part_count = opt->part_count;
+    c->npix = (int64_t)c->host.width * c->host.height;
+    c->stack_size = std::max(1, c->host.bvh_depth + 1);
+    if (c->stack_size > 96) {
+        free_ctx(c);
+        return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
+    }
+#define CK(expr)                                                                               \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess) {                                                                \
+            std::string m = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
+            free_ctx(c);                                                                       \
+            return fail(_e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE, m);            \
+        }                                                                                      \
+    } while (0)
+    CK(hipSetDevice(c->device));
+    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    CK(hipEventCreate(&c->ev0));
+    CK(hipEventCreate(&c->ev1));
+    CK(upload(&c->d_nodes, c->host.nodes));
+    CK(upload(&c->d_clusters, c->host.clusters));
+    CK(upload(&c->d_pinfo, c->host.pinfo));
+    CK(upload(&c->d_slots, c->host.slots));
+    CK(upload(&c->d_shade, c->host.shade));
+    CK(upload(&c->d_albedo, c->host.albedo));
+    const size_t plane = sizeof(double) * (size_t)c->npix;
+    CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
+    c->d_accum = c->d_accum_own;
+    CK(hipMalloc((void**)&c->d_film, 3 * plane));
+    CK(hipMalloc((void**)&c->d_frame, 4 * plane));
+    CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
+    CK(hipMalloc((void**)&c->d_work, 64));
+    CK(hipMalloc((void**)&c->d_counters, 8 * sizeof(unsigned long long)));
+    CK(hipMemset(c->d_accum, 0, 3 * plane));
+    CK(hipMemset(c->d_film, 0, 3 * plane));
+    CK(hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)));
+    hipDeviceProp_t prop;
+    CK(hipGetDeviceProperties(&prop, c->device));
+    int bpc = 0;
+    CK(mfx_trace_occupancy(c->stack_size, &bpc));
+    bpc = std::max(1, std::min(bpc, 8));
+    c->grid = prop.multiProcessorCount * bpc;
+#undef CK
+    *out = c;
+    return MFX_OK;
+}
+
+void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
+
+int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
+    HIPCHECK(hipSetDevice(c->device));
+    const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
+    HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
+    HIPCHECK(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    if (ns == 0) return MFX_OK;
+    TraceParams P;
+    std::memset(&P, 0, sizeof(P));
+    P.nodes = c->d_nodes;
+    P.clusters = c->d_clusters;
+    P.pinfo = c->d_pinfo;
+    P.slots = c->d_slots;
+    P.shade = c->d_shade;
+    P.albedo = c->d_albedo;
+    P.accum = c->d_accum;
+    P.work_counter = c->d_work;
+    P.counters = c->d_counters;
+    P.light = c->host.light;
+    P.cam = c->host.camera;
+    P.seed = c->seed;
+    P.sample_base = sample_base;
+    P.nsamples = ns;
+    P.part_index = c->part_index;
+    P.part_count = c->part_count;
+    P.width = c->host.width;
+    P.height = c->host.height;
+    P.max_depth = c->host.max_depth;
+    P.root_is_leaf = c->host.root_is_leaf;
+    P.stack_size = c->stack_size;
+    P.chunk = 256;
+    HIPCHECK(hipEventRecord(c->ev0, c->stream));
+    HIPCHECK(mfx_launch_trace(P, (c->flags & MFX_F_COUNT_STATS) != 0, c->grid, c->stream));
+    HIPCHECK(hipEventRecord(c->ev1, c->stream));
+    c->ev_valid = true;
+    return MFX_OK;
+}
+
+int mfx_last_trace_ms(mfx_ctx* c, double* ms) {
+    if (!c || !ms) return fail(MFX_E_INVALID, "null argument");
+    if (!c->ev_valid) return fail(MFX_E_STATE, "no trace launch recorded yet");
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipEventSynchronize(c->ev1));
+    float f = 0.f;
+    HIPCHECK(hipEventElapsedTime(&f, c->ev0, c->ev1));
+    *ms = (double)f;
+    return MFX_OK;
+}
+
+int mfx_accum_clear(mfx_ctx* c) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipMemsetAsync(c->d_accum, 0, 3 * sizeof(double) * (size_t)c->npix, c->stream));
+    return MFX_OK;
+}
+
+int mfx_accum_device_ptr(mfx_ctx* c, void** dptr, int64_t* nbytes) {
+    if (!c || !dptr || !nbytes) return fail(MFX_E_INVALID, "null argument");
+    *dptr = c->d_accum;
+    *nbytes = 3 * (int64_t)sizeof(double) * c->npix;
+    return MFX_OK;
+}
+
+int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    if (!dptr) {
+        c->d_accum = c->d_accum_own;
+        return MFX_OK;
+    }
+    if (nbytes < 3 * (int64_t)sizeof(double) * c->npix) return fail(MFX_E_INVALID, "attached accumulator too small");
+    c->d_accum = (double*)dptr;
+    return MFX_OK;
+}
+
+int mfx_accum_read_mean(mfx_ctx* c, double inv_count, double* frame) {
+    if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(c->device));
+    // texture[i,j] <- color / float n (Integrators.fs:171): divide by n = 1 / inv_count
+    HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, 1.0 / inv_count, c->d_frame, c->stream));
+    HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    return MFX_OK;
+}
+
+int mfx_sync(mfx_ctx* c) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    return MFX_OK;
+}
+
+int mfx_stream(mfx_ctx* c, void** stream) {
+    if (!c || !stream) return fail(MFX_E_INVALID, "null argument");
+    *stream = (void*)c->stream;
+    return MFX_OK;
+}
+
+int mfx_ray_counts(mfx_ctx* c, double out[8]) {
+    if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(c->device));
+    unsigned long long h[8];
+    HIPCHECK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (int k = 0; k < 8; ++k) out[k] = (double)h[k];
+    out[3] = out[0];  // paths == primary rays
+    return MFX_OK;
+}
+
+int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
+    if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
+    if (c->part_count != 1)
+        return fail(MFX_E_STATE, "mfx_sample needs the whole sample set (part_count == 1); "
+                                 "partitioned contexts compose with mfx_trace_accumulate + a reduce");
+    int rc = mfx_accum_clear(c);
+    if (rc) return rc;
+    rc = mfx_trace_accumulate(c, spp, c->next_sample);
+    if (rc) return rc;
+    c->next_sample += spp;
+    return mfx_accum_read_mean(c, 1.0 / (double)spp, frame);
+}
+
+int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
+    if (!c) return fail(MFX_E_INVALID, "null context");
+    if (c->part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
+    int rc = mfx_accum_clear(c);
+    if (rc) return rc;
+    rc = mfx_trace_accumulate(c, spp, c->next_sample);
+    if (rc) return rc;
+    c->next_sample += spp;
+    c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
+    HIPCHECK(mfx_launch_film_post(c->d_accum, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
+                                  rgba ? c->d_rgba : nullptr, c->stream));
+    if (rgba)
+        HIPCHECK(hipMemcpyAsync(rgba, c->d_rgba, 4 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    return MFX_OK;
+}
+
+int mfx_reset(mfx_ctx* c) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(hipMemsetAsync(c->d_film, 0, 3 * sizeof(double) * (size_t)c->npix, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    c->frame_count = 0.0;
+    return MFX_OK;
+}
+
+int mfx_film_mean(mfx_ctx* c, double* frame) {
+    if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(mfx_launch_film_mean(c->d_film, c->npix, c->frame_count, c->d_frame, c->stream));
+    HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    return MFX_OK;
+}
+
+static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, double tmax, const double* tmax_arr,
+                     double* t_out, int32_t* prim_out, double* normal_out, int32_t* occ_out, bool shadow) {
+    if (!c || !rays || n < 0) return fail(MFX_E_INVALID, "bad query arguments");
+    if (n == 0) return MFX_OK;
+    HIPCHECK(hipSetDevice(c->device));
+    double *d_rays = nullptr, *d_tmax = nullptr, *d_t = nullptr, *d_n = nullptr;
+    int32_t *d_p = nullptr, *d_o = nullptr;
+    hipError_t e = hipMalloc((void**)&d_rays, sizeof(double) * 6 * n);
+    if (e == hipSuccess) e = hipMemcpy(d_rays, rays, sizeof(double) * 6 * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && shadow) e = hipMalloc((void**)&d_tmax, sizeof(double) * n);
+    if (e == hipSuccess && shadow) e = hipMemcpy(d_tmax, tmax_arr, sizeof(double) * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess && shadow) e = hipMalloc((void**)&d_o, sizeof(int32_t) * n);
+    if (e == hipSuccess && !shadow) e = hipMalloc((void**)&d_t, sizeof(double) * n);
+    if (e == hipSuccess && !shadow) e = hipMalloc((void**)&d_p, sizeof(int32_t) * n);
+    if (e == hipSuccess && !shadow) e = hipMalloc((void**)&d_n, sizeof(double) * 3 * n);
+    if (e == hipSuccess) {
+        QueryParams Q;
+        std::memset(&Q, 0, sizeof(Q));
+        Q.nodes = c->d_nodes;
+        Q.clusters = c->d_clusters;
+        Q.pinfo = c->d_pinfo;
+        Q.slots = c->d_slots;
+        Q.shade = c->d_shade;
+        Q.rays = d_rays;
+        Q.tmax_per_ray = d_tmax;
+        Q.t_out = d_t;
+        Q.prim_out = d_p;
+        Q.normal_out = d_n;
+        Q.occ_out = d_o;
+        Q.n = n;
+        Q.tmin = tmin;
+        Q.tmax = tmax;
+        Q.root_is_leaf = c->host.root_is_leaf;
+        Q.stack_size = c->stack_size;
+        e = mfx_launch_query(Q, shadow, c->stream);
+    }
+    if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+    if (e == hipSuccess && shadow) e = hipMemcpy(occ_out, d_o, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow) e = hipMemcpy(t_out, d_t, sizeof(double) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow) e = hipMemcpy(prim_out, d_p, sizeof(int32_t) * n, hipMemcpyDeviceToHost);
+    if (e == hipSuccess && !shadow && normal_out)
+        e = hipMemcpy(normal_out, d_n, sizeof(double) * 3 * n, hipMemcpyDeviceToHost);
+    for (void* b : {(void*)d_rays, (void*)d_tmax, (void*)d_t, (void*)d_n, (void*)d_p, (void*)d_o})
+        if (b) (void)hipFree(b);
+    if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("query: ") + hipGetErrorString(e));
+    return MFX_OK;
+}
+
+int mfx_closest_hit(mfx_ctx* c, int64_t n, const double* rays, double tmin, double tmax, double* t_out,
+                    int32_t* prim_out, double* normal_out) {
+    if (!t_out || !prim_out) return fail(MFX_E_INVALID, "null output");
+    return run_query(c, n, rays, tmin, tmax, nullptr, t_out, prim_out, normal_out, nullptr, false);
+}
+
+int mfx_any_hit(mfx_ctx* c, int64_t n, const double* rays, double tmin, const double* tmax, int32_t* occluded_out) {
+    if (!tmax || !occluded_out) return fail(MFX_E_INVALID, "null argument");
+    return run_query(c, n, rays, tmin, 0.0, tmax, nullptr, nullptr, nullptr, occluded_out, true);
+}
+
+int mfx_ref_leaves(mfx_ctx* c, int32_t* indices_out, int32_t* leaf_first_out, int32_t* leaf_count_out,
+                   int32_t* nleaves_out) {
+    if (!c || !indices_out || !leaf_first_out || !leaf_count_out || !nleaves_out)
+        return fail(MFX_E_INVALID, "null argument");
+    std::copy(c->host.ref_indices.begin(), c->host.ref_indices.end(), indices_out);
+    std::copy(c->host.leaf_first.begin(), c->host.leaf_first.end(), leaf_first_out);
+    std::copy(c->host.leaf_count.begin(), c->host.leaf_count.end(), leaf_count_out);
+    *nleaves_out = (int32_t)c->host.leaf_first.size();
+    return MFX_OK;
+}
+
+int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* b, double* div_out, double* sqrt_out) {
+    if (n <= 0 || !a || !b || !div_out || !sqrt_out) return fail(MFX_E_INVALID, "bad selftest arguments");
+    HIPCHECK(hipSetDevice(device));
+    double *da = nullptr, *db = nullptr, *dd = nullptr, *ds = nullptr;
+    const size_t bytes = sizeof(double) * n;
+    hipError_t e = hipMalloc((void**)&da, bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&db, bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&dd, bytes);
+    if (e == hipSuccess) e = hipMalloc((void**)&ds, bytes);
+    if (e == hipSuccess) e = hipMemcpy(da, a, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = hipMemcpy(db, b, bytes, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mfx_launch_fp64_selftest(da, db, n, dd, ds, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(div_out, dd, bytes, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(sqrt_out, ds, bytes, hipMemcpyDeviceToHost);
+    for (void* p : {(void*)da, (void*)db, (void*)dd, (void*)ds})
+        if (p) (void)hipFree(p);
+    if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("fp64 selftest: ") + hipGetErrorString(e));
+    return MFX_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,60 @@
+// mfx_device.h — kernel parameter blocks and host-side launcher declarations.
+#ifndef MFX_DEVICE_H
+#define MFX_DEVICE_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "mfx_layout.h"
+
+struct TraceParams {
+    const MfxNode* nodes;
+    const MfxCluster* clusters;
+    const int32_t* pinfo;
+    const MfxSlot* slots;
+    const MfxShade* shade;
+    const double* albedo;
+    double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
+    unsigned long long* work_counter;
+    unsigned long long* counters;    // [8] ray / traversal counters
+    MfxLight light;
+    MfxCamera cam;
+    uint64_t seed;
+    int64_t sample_base;             // first global sample index of this call
+    int64_t nsamples;                // samples this context renders per pixel in this call
+    int32_t part_index, part_count;  // global sample = sample_base + part_index + s * part_count
+    int32_t width, height, max_depth;
+    int32_t root_is_leaf;
+    int32_t stack_size;              // LDS traversal stack entries per lane
+    int32_t chunk;                   // path indices a wave takes per atomic
+};
+
+struct QueryParams {
+    const MfxNode* nodes;
+    const MfxCluster* clusters;
+    const int32_t* pinfo;
+    const MfxSlot* slots;
+    const MfxShade* shade;
+    const double* rays;
+    const double* tmax_per_ray;
+    double* t_out;
+    int32_t* prim_out;
+    double* normal_out;
+    int32_t* occ_out;
+    int64_t n;
+    double tmin, tmax;
+    int32_t root_is_leaf;
+    int32_t stack_size;
+};
+
+hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st);
+hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu);
+hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st);
+hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st);
+hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h, double spp, double frame_count,
+                                int add, uint8_t* rgba, hipStream_t st);
+hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_count, double* out, hipStream_t st);
+hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo,
+                                    hipStream_t st);
+
+#endif

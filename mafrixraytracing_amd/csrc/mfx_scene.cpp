@@ -1,0 +1,495 @@
+// mfx_scene.cpp — host-side preparation of a scene for the gfx950 kernels.
+//
+// 1. Primitive records in FP64, with exactly the reference constructors' arithmetic
+//    (Triangle: Trangle.fs:107-119, Rect: Rect.fs:11-20, Sphere: Sphere.fs:9-16).
+// 2. The reference's heap BVH (BvhNode.fs:24-61) is built only for its LEAF GROUPING: which
+//    2-3 primitives share a leaf decides the shadow-ray result when every primitive of a leaf
+//    is hit beyond tMax (Triangle.Hit ignores tMax, Trangle.fs:148; the leaf minBy, :76-80).
+//    Its median split sorts with F#'s Array.sortInPlaceBy = .NET 6 introsort, restated here so
+//    ties fall the same way.
+// 3. A binned-SAH BVH2 over those leaves ("clusters") is what the GPU traverses, in FP32
+//    with conservatively widened boxes; the exact FP64 leaf test happens at each cluster.
+#include "mfx_scene.h"
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+
+namespace {
+
+struct D3 {
+    double x, y, z;
+};
+inline D3 d3(const double* p) { return {p[0], p[1], p[2]}; }
+inline D3 sub(D3 a, D3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+inline D3 add(D3 a, D3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+inline D3 scale(D3 v, double a) { return {v.x * a, v.y * a, v.z * a}; }
+inline D3 cross(D3 a, D3 v) { return {a.y * v.z - a.z * v.y, a.z * v.x - a.x * v.z, a.x * v.y - a.y * v.x}; }
+inline double len(D3 v) { return std::sqrt(v.x * v.x + v.y * v.y + v.z * v.z); }
+inline D3 normalize(D3 v) {
+    double l = len(v);
+    if (l == 0.0) return {0, 0, 0};
+    return {v.x / l, v.y / l, v.z / l};
+}
+inline double comp(D3 v, int i) { return i == 0 ? v.x : (i == 1 ? v.y : v.z); }
+inline double mn(double a, double b) { return a < b ? a : b; }
+inline double mx(double a, double b) { return a > b ? a : b; }
+inline void put(double* dst, D3 v) { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; }
+
+struct Box {
+    D3 lo, hi;
+};
+inline Box box2(D3 p, D3 q) {  // Bound(p1, p2), Aggregate.fs:9-11
+    return {{mn(p.x, q.x), mn(p.y, q.y), mn(p.z, q.z)}, {mx(p.x, q.x), mx(p.y, q.y), mx(p.z, q.z)}};
+}
+inline Box join(Box a, Box b) {  // Bound.Union, Aggregate.fs:58-61
+    return box2({mn(a.lo.x, b.lo.x), mn(a.lo.y, b.lo.y), mn(a.lo.z, b.lo.z)},
+                {mx(a.hi.x, b.hi.x), mx(a.hi.y, b.hi.y), mx(a.hi.z, b.hi.z)});
+}
+inline Box join_pt(Box a, D3 p) {
+    return box2({mn(a.lo.x, p.x), mn(a.lo.y, p.y), mn(a.lo.z, p.z)}, {mx(a.hi.x, p.x), mx(a.hi.y, p.y), mx(a.hi.z, p.z)});
+}
+inline Box tri_box(D3 a, D3 b, D3 c) { return join_pt(box2(a, b), c); }  // Trangle.fs:113
+
+// ---- .NET 6 GenericArraySortHelper<double,int>.IntroSort (tie behaviour of Array.Sort) ------
+struct NetSort {
+    double* k;
+    int32_t* v;
+    void swap(int i, int j) {
+        std::swap(k[i], k[j]);
+        std::swap(v[i], v[j]);
+    }
+    void swap_if_greater(int i, int j) {
+        if (k[i] > k[j]) swap(i, j);
+    }
+    void insertion(int n) {
+        for (int i = 0; i < n - 1; ++i) {
+            double t = k[i + 1];
+            int32_t tv = v[i + 1];
+            int j = i;
+            for (; j >= 0 && t < k[j]; --j) {
+                k[j + 1] = k[j];
+                v[j + 1] = v[j];
+            }
+            k[j + 1] = t;
+            v[j + 1] = tv;
+        }
+    }
+    void down_heap(int i, int n) {
+        double d = k[i - 1];
+        int32_t dv = v[i - 1];
+        while (i <= n >> 1) {
+            int c = 2 * i;
+            if (c < n && k[c - 1] < k[c]) ++c;
+            if (!(d < k[c - 1])) break;
+            k[i - 1] = k[c - 1];
+            v[i - 1] = v[c - 1];
+            i = c;
+        }
+        k[i - 1] = d;
+        v[i - 1] = dv;
+    }
+    void heap(int n) {
+        for (int i = n >> 1; i >= 1; --i) down_heap(i, n);
+        for (int i = n; i > 1; --i) {
+            swap(0, i - 1);
+            down_heap(1, i - 1);
+        }
+    }
+    int partition(int n) {
+        const int hi = n - 1, mid = hi >> 1;
+        swap_if_greater(0, mid);
+        swap_if_greater(0, hi);
+        swap_if_greater(mid, hi);
+        const double pivot = k[mid];
+        swap(mid, hi - 1);
+        int l = 0, r = hi - 1;
+        while (l < r) {
+            while (pivot > k[++l]) {
+            }
+            while (pivot < k[--r]) {
+            }
+            if (l >= r) break;
+            swap(l, r);
+        }
+        if (l != hi - 1) swap(l, hi - 1);
+        return l;
+    }
+    static void intro(double* kk, int32_t* vv, int n, int depth) {
+        while (n > 1) {
+            NetSort s{kk, vv};
+            if (n <= 16) {
+                if (n == 2) {
+                    s.swap_if_greater(0, 1);
+                } else if (n == 3) {
+                    s.swap_if_greater(0, 1);
+                    s.swap_if_greater(0, 2);
+                    s.swap_if_greater(1, 2);
+                } else {
+                    s.insertion(n);
+                }
+                return;
+            }
+            if (depth == 0) {
+                s.heap(n);
+                return;
+            }
+            --depth;
+            int p = s.partition(n);
+            intro(kk + p + 1, vv + p + 1, n - p - 1, depth);
+            n = p;
+        }
+    }
+    static void sort(double* kk, int32_t* vv, int n) {
+        if (n < 2) return;
+        int lg = 0;
+        for (unsigned x = (unsigned)n; x >>= 1;) ++lg;
+        intro(kk, vv, n, 2 * (lg + 1));
+    }
+};
+
+// ---- reference heap BVH: leaf grouping only ------------------------------------------------
+struct RefBvh {
+    const std::vector<Box>& pb;
+    std::vector<int32_t>& idx;
+    std::vector<int32_t>& lf;
+    std::vector<int32_t>& lc;
+    std::vector<double> keys;
+    std::vector<int32_t> tmp;
+
+    Box bound(int first, int count) const {  // InitNode, BvhNode.fs:32-37
+        Box b = pb[idx[first]];
+        for (int k = 1; k < count; ++k) b = join(b, pb[idx[first + k]]);
+        return b;
+    }
+    // Subdivide (BvhNode.fs:42-61), visiting leaves left to right
+    void subdivide(int first, int count, Box b) {
+        if (count <= 3) {
+            lf.push_back(first);
+            lc.push_back(count);
+            return;
+        }
+        D3 d = sub(b.hi, b.lo);  // MaximumExtent, Aggregate.fs:29-36
+        int axis = (d.x > d.y && d.x > d.z) ? 0 : (d.y > d.z ? 1 : 2);
+        for (int k = 0; k < count; ++k) {
+            int p = idx[first + k];
+            const Box& q = pb[p];
+            D3 c = add(q.lo, scale(sub(q.hi, q.lo), 0.5));
+            keys[k] = comp(c, axis);
+            tmp[k] = p;
+        }
+        NetSort::sort(keys.data(), tmp.data(), count);
+        std::memcpy(&idx[first], tmp.data(), sizeof(int32_t) * count);
+        int left = count / 2;
+        Box bl = bound(first, left), br = bound(first + left, count - left);
+        subdivide(first, left, bl);
+        subdivide(first + left, count - left, br);
+    }
+};
+
+// ---- binned SAH BVH2 over clusters ---------------------------------------------------------
+struct FBox {
+    float lo[3], hi[3];
+    void grow(const FBox& b) {
+        for (int i = 0; i < 3; ++i) {
+            lo[i] = std::min(lo[i], b.lo[i]);
+            hi[i] = std::max(hi[i], b.hi[i]);
+        }
+    }
+    float area() const {
+        float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (dx < 0 || dy < 0 || dz < 0) return 0.f;
+        return 2.f * (dx * dy + dx * dz + dy * dz);
+    }
+    static FBox empty() {
+        FBox b;
+        for (int i = 0; i < 3; ++i) {
+            b.lo[i] = FLT_MAX;
+            b.hi[i] = -FLT_MAX;
+        }
+        return b;
+    }
+};
+
+struct SahBuilder {
+    std::vector<FBox> cb;      // cluster boxes (conservative FP32)
+    std::vector<float> cent;   // centroids [3*n]
+    std::vector<int32_t> ids;  // permutation being partitioned
+    std::vector<MfxNode>& nodes;
+    int max_depth = 0;
+    static constexpr int NB = 32;
+
+    explicit SahBuilder(std::vector<MfxNode>& n) : nodes(n) {}
+
+    // returns child reference; fills `out` with the subtree box
+    int build(int b, int e, int depth, FBox& out) {
+        max_depth = std::max(max_depth, depth);
+        if (e - b == 1) {
+            out = cb[ids[b]];
+            return ~ids[b];
+        }
+        FBox cbox = FBox::empty();
+        for (int i = b; i < e; ++i) {
+            FBox p;
+            for (int a = 0; a < 3; ++a) p.lo[a] = p.hi[a] = cent[3 * ids[i] + a];
+            cbox.grow(p);
+        }
+        int best_axis = -1, best_split = 0;
+        float best_cost = FLT_MAX;
+        for (int a = 0; a < 3; ++a) {
+            float ext = cbox.hi[a] - cbox.lo[a];
+            if (!(ext > 0.f)) continue;
+            FBox bb[NB];
+            int cnt[NB] = {0};
+            for (int k = 0; k < NB; ++k) bb[k] = FBox::empty();
+            for (int i = b; i < e; ++i) {
+                int k = (int)((cent[3 * ids[i] + a] - cbox.lo[a]) / ext * NB);
+                k = std::min(NB - 1, std::max(0, k));
+                cnt[k]++;
+                bb[k].grow(cb[ids[i]]);
+            }
+            float ra[NB];
+            int rc[NB];
+            FBox acc = FBox::empty();
+            int c = 0;
+            for (int k = NB - 1; k > 0; --k) {
+                acc.grow(bb[k]);
+                c += cnt[k];
+                ra[k] = acc.area();
+                rc[k] = c;
+            }
+            acc = FBox::empty();
+            c = 0;
+            for (int k = 0; k < NB - 1; ++k) {
+                acc.grow(bb[k]);
+                c += cnt[k];
+                if (c == 0 || rc[k + 1] == 0) continue;
+                float cost = acc.area() * c + ra[k + 1] * rc[k + 1];
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_split = k;
+                }
+            }
+        }
+        int mid;
+        if (best_axis < 0) {
+            mid = (b + e) / 2;  // all centroids coincide: split by position
+        } else {
+            const float lo = cbox.lo[best_axis], ext = cbox.hi[best_axis] - cbox.lo[best_axis];
+            auto it = std::partition(ids.begin() + b, ids.begin() + e, [&](int id) {
+                int k = (int)((cent[3 * id + best_axis] - lo) / ext * NB);
+                k = std::min(NB - 1, std::max(0, k));
+                return k <= best_split;
+            });
+            mid = (int)(it - ids.begin());
+            if (mid == b || mid == e) mid = (b + e) / 2;
+        }
+        int self = (int)nodes.size();
+        nodes.push_back(MfxNode{});
+        FBox lb, rb;
+        int l = build(b, mid, depth + 1, lb);
+        int r = build(mid, e, depth + 1, rb);
+        MfxNode& n = nodes[self];
+        n.c0lox = lb.lo[0]; n.c0hix = lb.hi[0]; n.c0loy = lb.lo[1]; n.c0hiy = lb.hi[1];
+        n.c1lox = rb.lo[0]; n.c1hix = rb.hi[0]; n.c1loy = rb.lo[1]; n.c1hiy = rb.hi[1];
+        n.c0loz = lb.lo[2]; n.c0hiz = lb.hi[2]; n.c1loz = rb.lo[2]; n.c1hiz = rb.hi[2];
+        n.child0 = l;
+        n.child1 = r;
+        n.pad0 = n.pad1 = 0;
+        out = lb;
+        out.grow(rb);
+        return self;
+    }
+};
+
+inline float round_down(double x) {
+    float f = (float)x;
+    if ((double)f > x) f = std::nextafter(f, -FLT_MAX);
+    return f;
+}
+inline float round_up(double x) {
+    float f = (float)x;
+    if ((double)f < x) f = std::nextafter(f, FLT_MAX);
+    return f;
+}
+
+}  // namespace
+
+bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err) {
+    if (!d || !d->prims || d->nprims < 1) {
+        err = "scene has no primitives (Bvh.Build on an empty array throws, BvhNode.fs:26)";
+        return false;
+    }
+    if (d->nprims > (1 << 28)) {
+        err = "too many primitives";
+        return false;
+    }
+    if (d->width < 1 || d->height < 1 || d->nmat < 1 || !d->albedo) {
+        err = "invalid film size or empty material table";
+        return false;
+    }
+    const int n = (int)d->nprims;
+    s.width = d->width;
+    s.height = d->height;
+    s.max_depth = d->max_depth;
+    s.albedo.assign(d->albedo, d->albedo + 3 * (size_t)d->nmat);
+
+    // ---- primitives: FP64 bounds + slot records -------------------------------------------
+    std::vector<Box> pb(n);
+    std::vector<int32_t> slot_of(n);
+    s.slots.clear();
+    s.shade.clear();
+    auto add_tri = [&](D3 v0, D3 v1, D3 v2, int mat, int prim, int kind) {
+        MfxSlot t{};
+        D3 e1 = sub(v1, v0), e2 = sub(v2, v0);
+        put(t.a, v0);
+        put(t.b, e1);
+        put(t.c, e2);
+        s.slots.push_back(t);
+        MfxShade sh{};
+        D3 a = cross(e1, e2);
+        double al = len(a);
+        put(sh.n, D3{a.x / al, a.y / al, a.z / al});  // Trangle.fs:110-111
+        sh.material = mat;
+        sh.prim_kind = (prim << 2) | kind;
+        s.shade.push_back(sh);
+    };
+    for (int i = 0; i < n; ++i) {
+        const mfx_prim& p = d->prims[i];
+        if (p.material < 0 || p.material >= d->nmat) {
+            err = "primitive " + std::to_string(i) + " has material index out of range";
+            return false;
+        }
+        slot_of[i] = (int)s.slots.size();
+        if (p.kind == MFX_PRIM_TRIANGLE) {
+            D3 v0 = d3(p.p[0]), v1 = d3(p.p[1]), v2 = d3(p.p[2]);
+            pb[i] = tri_box(v0, v1, v2);
+            add_tri(v0, v1, v2, p.material, i, MFX_KIND_TRI);
+        } else if (p.kind == MFX_PRIM_RECT) {
+            D3 v0 = d3(p.p[0]), v1 = d3(p.p[1]), v2 = d3(p.p[2]), v3 = d3(p.p[3]);
+            pb[i] = join(tri_box(v0, v1, v2), tri_box(v0, v2, v3));  // Rect.fs:18
+            add_tri(v0, v1, v2, p.material, i, MFX_KIND_RECT);
+            add_tri(v0, v2, v3, p.material, i, MFX_KIND_RECT);
+        } else if (p.kind == MFX_PRIM_SPHERE) {
+            D3 c = d3(p.p[0]);
+            double r = p.p[1][0];
+            D3 v{r, r, r};
+            pb[i] = box2(sub(c, v), add(c, v));  // Sphere.fs:14-15
+            MfxSlot t{};
+            put(t.a, c);
+            t.b[0] = r;
+            s.slots.push_back(t);
+            MfxShade sh{};
+            sh.material = p.material;
+            sh.prim_kind = (i << 2) | MFX_KIND_SPHERE;
+            s.shade.push_back(sh);
+        } else {
+            err = "primitive " + std::to_string(i) + " has an unknown kind";
+            return false;
+        }
+    }
+
+    // ---- reference leaf grouping -----------------------------------------------------------
+    s.ref_indices.resize(n);
+    for (int i = 0; i < n; ++i) s.ref_indices[i] = i;
+    s.leaf_first.clear();
+    s.leaf_count.clear();
+    {
+        RefBvh rb{pb, s.ref_indices, s.leaf_first, s.leaf_count, std::vector<double>(n), std::vector<int32_t>(n)};
+        Box root = rb.bound(0, n);
+        rb.subdivide(0, n, root);
+    }
+    s.pinfo.resize(n);
+    for (int k = 0; k < n; ++k) {
+        int p = s.ref_indices[k];
+        s.pinfo[k] = d->prims[p].kind | (slot_of[p] << 2);
+    }
+    const int nc = (int)s.leaf_first.size();
+    s.clusters.resize(nc);
+    for (int c = 0; c < nc; ++c) {
+        MfxCluster& cl = s.clusters[c];
+        Box b = pb[s.ref_indices[s.leaf_first[c]]];
+        for (int k = 1; k < s.leaf_count[c]; ++k) b = join(b, pb[s.ref_indices[s.leaf_first[c] + k]]);
+        put(cl.lo, b.lo);
+        put(cl.hi, b.hi);
+        cl.first = s.leaf_first[c];
+        cl.count = s.leaf_count[c];
+    }
+
+    // ---- camera (Camera.fs:96-133) and light (Light.fs:31-40) -------------------------------
+    {
+        const mfx_pinhole& c = d->camera;
+        D3 fwd = normalize(d3(c.direction));
+        D3 up0 = normalize(D3{0, 1, 0});
+        D3 hori0 = cross(fwd, normalize(up0));
+        D3 vert0 = cross(hori0, fwd);
+        double hori = std::tan(0.5 * c.fov * 3.141592653589793 / 360.);
+        double vert = hori / c.aspect;
+        D3 up = scale(vert0, vert), right = scale(hori0, hori);
+        D3 pos = d3(c.position);
+        D3 tl = add(sub(add(pos, scale(fwd, 0.5)), scale(right, 0.5)), scale(up, 0.5));
+        put(s.camera.position, pos);
+        put(s.camera.topleft, tl);
+        put(s.camera.right, right);
+        put(s.camera.down, D3{-up.x, -up.y, -up.z});
+    }
+    {
+        const mfx_quad_light& L = d->light;
+        D3 q[4] = {d3(L.p[0]), d3(L.p[1]), d3(L.p[2]), d3(L.p[3])};
+        D3 tv[2][3] = {{q[0], q[1], q[2]}, {q[0], q[2], q[3]}};
+        double area = 0;
+        for (int t = 0; t < 2; ++t) {
+            D3 e1 = sub(tv[t][1], tv[t][0]), e2 = sub(tv[t][2], tv[t][0]);
+            put(s.light.v0[t], tv[t][0]);
+            put(s.light.e1[t], e1);
+            put(s.light.e2[t], e2);
+            double al = len(cross(e1, e2));
+            double ta = al * 0.5;  // Trangle.fs:114
+            area = (t == 0) ? ta : area + ta;
+        }
+        s.light.area = area;
+        s.light.pdf = 1. / area;
+        put(s.light.normal, d3(L.normal));
+        put(s.light.color, d3(L.intensity));
+    }
+
+    // ---- conservative FP32 cluster boxes + SAH BVH2 ----------------------------------------
+    double R = 0, T = 0;
+    {
+        Box all = pb[0];
+        for (int i = 1; i < n; ++i) all = join(all, pb[i]);
+        for (double v : {all.lo.x, all.lo.y, all.lo.z, all.hi.x, all.hi.y, all.hi.z}) R = std::max(R, std::fabs(v));
+        for (int a = 0; a < 3; ++a) R = std::max(R, std::fabs(d->camera.position[a]));
+        T = len(sub(all.hi, all.lo)) + len(sub(d3(d->camera.position), scale(add(all.lo, all.hi), 0.5)));
+        for (int k = 0; k < 4; ++k)
+            for (int a = 0; a < 3; ++a) R = std::max(R, std::fabs(d->light.p[k][a]));
+    }
+    s.eps = (float)std::ldexp(R + T, -19);
+    s.nodes.clear();
+    SahBuilder sb(s.nodes);
+    sb.cb.resize(nc);
+    sb.cent.resize(3 * (size_t)nc);
+    sb.ids.resize(nc);
+    for (int c = 0; c < nc; ++c) {
+        FBox f;
+        for (int a = 0; a < 3; ++a) {
+            f.lo[a] = round_down(s.clusters[c].lo[a] - (double)s.eps);
+            f.hi[a] = round_up(s.clusters[c].hi[a] + (double)s.eps);
+            sb.cent[3 * c + a] = 0.5f * (f.lo[a] + f.hi[a]);
+        }
+        sb.cb[c] = f;
+        sb.ids[c] = c;
+    }
+    if (nc == 1) {
+        s.root_is_leaf = 1;
+        s.bvh_depth = 0;
+    } else {
+        FBox rootbox;
+        sb.build(0, nc, 0, rootbox);
+        s.root_is_leaf = 0;
+        s.bvh_depth = sb.max_depth;
+    }
+    return true;
+}

@@ -1,0 +1,33 @@
+// mfx_scene.h — host-side scene preparation (runs once per `Scene`, Scene.fs:298-313).
+#ifndef MFX_SCENE_H
+#define MFX_SCENE_H
+
+#include <string>
+#include <vector>
+
+#include "../../include/mafrix_rt.h"
+#include "mfx_layout.h"
+
+struct MfxHostScene {
+    // reference heap-BVH leaf grouping (BvhNode.fs:24-61)
+    std::vector<int32_t> ref_indices;                  // `indices` after Subdivide
+    std::vector<int32_t> leaf_first, leaf_count;       // leaves in heap (DFS) order
+    // device images
+    std::vector<MfxNode> nodes;
+    std::vector<MfxCluster> clusters;
+    std::vector<int32_t> pinfo;
+    std::vector<MfxSlot> slots;
+    std::vector<MfxShade> shade;
+    std::vector<double> albedo;  // [nmat][3]
+    MfxLight light;
+    MfxCamera camera;
+    int32_t width = 0, height = 0, max_depth = 3;
+    int32_t root_is_leaf = 0;  // 1 => a single cluster, no internal nodes
+    int32_t bvh_depth = 0;     // longest root-to-leaf path in nodes[] (traversal stack bound)
+    float eps = 0.f;           // conservative box widening
+};
+
+// Builds everything from the C-ABI scene description; returns false with `err` set on bad input.
+bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err);
+
+#endif

@@ -1,0 +1,195 @@
+"""Host-side mirror of the reference's render API over the C ABI.
+
+`Scene`, `NativePixelIntegrator` and `Film` keep the names and argument meaning of
+EngineCore/Scene/Scene.fs:291-333, Core/Integrator/Integrators.fs:143-172 and
+Core/Film.fs:13-34; all work happens in libmafrix_rt.so on the GPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from .abi import (MFX_F_NONE, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
+
+DEFAULT_SEED = 0x4D414652
+
+
+class NativeContext:
+    """One mfx_ctx: a scene resident in HBM on one GPU."""
+
+    def __init__(self, arrays: SceneArrays, seed: int = DEFAULT_SEED, device: int = 0, flags: int = MFX_F_NONE,
+                 part_index: int = 0, part_count: int = 1):
+        self.lib = load_library()
+        self.arrays = arrays
+        self.w, self.h = arrays.width, arrays.height
+        self._desc = arrays.desc()
+        opt = MfxOptions(seed=seed, device=device, flags=flags, part_index=part_index, part_count=part_count)
+        h = C.c_void_p()
+        check(self.lib.mfx_create(C.byref(self._desc), C.byref(opt), C.byref(h)), "mfx_create")
+        self._h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mfx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- reference API -------------------------------------------------------------------
+    def sample(self, spp: int) -> np.ndarray:
+        frame = np.empty((self.w * self.h, 4), dtype=np.float64)
+        check(self.lib.mfx_sample(self._h, spp, dptr(frame)), "mfx_sample")
+        return frame
+
+    def render_rgba8(self, spp: int = 1, want_pixels: bool = True) -> np.ndarray | None:
+        if not want_pixels:
+            check(self.lib.mfx_render_rgba8(self._h, spp, None), "mfx_render_rgba8")
+            return None
+        out = np.empty(self.w * self.h * 4, dtype=np.uint8)
+        check(self.lib.mfx_render_rgba8(self._h, spp, out.ctypes.data_as(C.POINTER(C.c_uint8))), "mfx_render_rgba8")
+        return out
+
+    def reset(self):
+        check(self.lib.mfx_reset(self._h), "mfx_reset")
+
+    def film_mean(self) -> np.ndarray:
+        frame = np.empty((self.w * self.h, 4), dtype=np.float64)
+        check(self.lib.mfx_film_mean(self._h, dptr(frame)), "mfx_film_mean")
+        return frame
+
+    # -- lower level ---------------------------------------------------------------------
+    def trace_accumulate(self, spp: int, sample_base: int):
+        check(self.lib.mfx_trace_accumulate(self._h, spp, sample_base), "mfx_trace_accumulate")
+
+    def accum_clear(self):
+        check(self.lib.mfx_accum_clear(self._h), "mfx_accum_clear")
+
+    def accum_device_ptr(self) -> tuple[int, int]:
+        p = C.c_void_p()
+        n = C.c_int64()
+        check(self.lib.mfx_accum_device_ptr(self._h, C.byref(p), C.byref(n)), "mfx_accum_device_ptr")
+        return p.value, n.value
+
+    def accum_attach(self, dptr: int | None, nbytes: int = 0):
+        check(self.lib.mfx_accum_attach(self._h, C.c_void_p(dptr) if dptr else None, nbytes), "mfx_accum_attach")
+
+    def accum_read_mean(self, count: float) -> np.ndarray:
+        frame = np.empty((self.w * self.h, 4), dtype=np.float64)
+        check(self.lib.mfx_accum_read_mean(self._h, 1.0 / count, dptr(frame)), "mfx_accum_read_mean")
+        return frame
+
+    def sync(self):
+        check(self.lib.mfx_sync(self._h), "mfx_sync")
+
+    def stream(self) -> int:
+        s = C.c_void_p()
+        check(self.lib.mfx_stream(self._h, C.byref(s)), "mfx_stream")
+        return s.value or 0
+
+    def ray_counts(self) -> np.ndarray:
+        out = np.zeros(8)
+        check(self.lib.mfx_ray_counts(self._h, dptr(out)), "mfx_ray_counts")
+        return out
+
+    def last_trace_ms(self) -> float:
+        ms = C.c_double()
+        check(self.lib.mfx_last_trace_ms(self._h, C.byref(ms)), "mfx_last_trace_ms")
+        return ms.value
+
+    def closest_hit(self, rays: np.ndarray, tmin: float = 1e-6, tmax: float = 99999999.0):
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        n = len(rays)
+        t = np.zeros(n)
+        prim = np.zeros(n, dtype=np.int32)
+        nrm = np.zeros((n, 3))
+        check(self.lib.mfx_closest_hit(self._h, n, dptr(rays), tmin, tmax, dptr(t), iptr(prim), dptr(nrm)),
+              "mfx_closest_hit")
+        return t, prim, nrm
+
+    def any_hit(self, rays: np.ndarray, tmax: np.ndarray, tmin: float = 1e-6):
+        rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)
+        tmax = np.ascontiguousarray(tmax, dtype=np.float64)
+        occ = np.zeros(len(rays), dtype=np.int32)
+        check(self.lib.mfx_any_hit(self._h, len(rays), dptr(rays), tmin, dptr(tmax), iptr(occ)), "mfx_any_hit")
+        return occ
+
+    def ref_leaves(self):
+        n = len(self.arrays.prims)
+        idx = np.zeros(n, dtype=np.int32)
+        lf = np.zeros(n, dtype=np.int32)
+        lc = np.zeros(n, dtype=np.int32)
+        nl = C.c_int32()
+        check(self.lib.mfx_ref_leaves(self._h, iptr(idx), iptr(lf), iptr(lc), C.byref(nl)), "mfx_ref_leaves")
+        return idx, lf[:nl.value], lc[:nl.value]
+
+
+def fp64_selftest(a: np.ndarray, b: np.ndarray, device: int = 0):
+    lib = load_library()
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    b = np.ascontiguousarray(b, dtype=np.float64)
+    dv = np.zeros_like(a)
+    sq = np.zeros_like(a)
+    check(lib.mfx_fp64_selftest(device, len(a), dptr(a), dptr(b), dptr(dv), dptr(sq)), "mfx_fp64_selftest")
+    return dv, sq
+
+
+# ---- the reference's object model -----------------------------------------------------------
+class Film:
+    """Film (Film.fs:13-34): progressive accumulation; here the accumulator lives on the GPU."""
+
+    def __init__(self, ctx: NativeContext):
+        self._ctx = ctx
+        self.Size = (ctx.w, ctx.h)
+
+    def Reset(self):
+        self._ctx.reset()
+
+    def GetFrame(self, integrator: "NativePixelIntegrator", samples: int) -> np.ndarray:
+        self._ctx.render_rgba8(samples, want_pixels=False)
+        return self._ctx.film_mean()
+
+
+class NativePixelIntegrator:
+    """IPixelIntegrator (IIntegrator.fs:35-40) backed by the GPU: Sample(n) -> Color[w,h] x-major."""
+
+    def __init__(self, ctx: NativeContext):
+        self._ctx = ctx
+
+    def Sample(self, n: int) -> np.ndarray:
+        return self._ctx.sample(n)
+
+
+class Scene:
+    """Scene (Scene.fs:291-333) with the path-tracing hot path on the GPU."""
+
+    def __init__(self, state, seed: int = DEFAULT_SEED, device: int = 0, max_depth: int = 3):
+        arrays = state.arrays(max_depth=max_depth) if hasattr(state, "arrays") else state
+        self._ctx = NativeContext(arrays, seed=seed, device=device)
+        self.width, self.height = arrays.width, arrays.height
+        self.film = Film(self._ctx)
+        self.pixelIntegrator = NativePixelIntegrator(self._ctx)
+
+    @property
+    def ScreenSize(self):
+        return (self.width, self.height)
+
+    def Render(self, delta: float, buffer) -> None:
+        """Scene.Render(delta, buffer) (Scene.fs:331-333): one 1-spp frame into the film, then
+        ACES -> sqrt -> RGBA8 into `buffer` (byte[w*h*4], y-major)."""
+        out = self._ctx.render_rgba8(1)
+        mv = memoryview(buffer).cast("B")
+        mv[:] = out.tobytes()
+
+    def close(self):
+        self._ctx.close()
