@@ -174,6 +174,12 @@ int mfx_any_hit(mfx_ctx* ctx, int64_t n, const double* rays, double tmin, const 
 int mfx_ref_leaves(mfx_ctx* ctx, int32_t* indices_out, int32_t* leaf_first_out,
                    int32_t* leaf_count_out, int32_t* nleaves_out);
 
+/* Host-only (no device needed): the same leaf grouping computed straight from a scene
+ * description, plus the traversal BVH's shape: info[0] = clusters, info[1] = internal nodes,
+ * info[2] = depth. Any output pointer may be NULL.                                          */
+int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t* leaf_first_out,
+                     int32_t* leaf_count_out, int32_t* nleaves_out, int32_t info_out[4]);
+
 /* Device FP64 self-test: computes a/b, sqrt(a) on the GPU for n pairs (bit-exactness check
  * of the device math the numerics contract relies on).                                      */
 int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* b,

@@ -117,6 +117,7 @@ def _bind(lib):
         "mfx_any_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, _dp, _ip]),
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
         "mfx_fp64_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _dp, _dp]),
+        "mfx_build_leaves": (C.c_int, [_P(MfxSceneDesc), _ip, _ip, _ip, _ip, _ip]),
         "mfx_last_error": (C.c_char_p, []),
         "mfx_abi_version": (C.c_int, []),
         "mfx_device_count": (C.c_int, []),
@@ -132,7 +133,7 @@ EXPORTED_SYMBOLS = [
     "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_reset", "mfx_film_mean",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
-    "mfx_fp64_selftest", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+    "mfx_fp64_selftest", "mfx_build_leaves", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 
 _lib = None
@@ -168,3 +169,19 @@ def dptr(a: np.ndarray):
 
 def iptr(a: np.ndarray):
     return a.ctypes.data_as(_ip)
+
+
+def build_leaves(arrays: SceneArrays):
+    """Host-only: reference leaf grouping + traversal-BVH shape of a scene (no GPU needed)."""
+    lib = load_library()
+    d = arrays.desc()
+    n = len(arrays.prims)
+    idx = np.zeros(n, dtype=np.int32)
+    lf = np.zeros(n, dtype=np.int32)
+    lc = np.zeros(n, dtype=np.int32)
+    nl = np.zeros(1, dtype=np.int32)
+    info = np.zeros(4, dtype=np.int32)
+    check(lib.mfx_build_leaves(C.byref(d), iptr(idx), iptr(lf), iptr(lc), iptr(nl), iptr(info)), "mfx_build_leaves")
+    k = int(nl[0])
+    return idx, lf[:k], lc[:k], {"clusters": int(info[0]), "nodes": int(info[1]), "depth": int(info[2]),
+                                 "root_is_leaf": int(info[3])}

@@ -387,6 +387,24 @@ int mfx_ref_leaves(mfx_ctx* c, int32_t* indices_out, int32_t* leaf_first_out, in
     return MFX_OK;
 }
 
+int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t* leaf_first_out,
+                     int32_t* leaf_count_out, int32_t* nleaves_out, int32_t info_out[4]) {
+    MfxHostScene s;
+    std::string err;
+    if (!mfx_build_scene(scene, s, err)) return fail(MFX_E_INVALID, "mfx_build_leaves: " + err);
+    if (indices_out) std::copy(s.ref_indices.begin(), s.ref_indices.end(), indices_out);
+    if (leaf_first_out) std::copy(s.leaf_first.begin(), s.leaf_first.end(), leaf_first_out);
+    if (leaf_count_out) std::copy(s.leaf_count.begin(), s.leaf_count.end(), leaf_count_out);
+    if (nleaves_out) *nleaves_out = (int32_t)s.leaf_first.size();
+    if (info_out) {
+        info_out[0] = (int32_t)s.clusters.size();
+        info_out[1] = (int32_t)s.nodes.size();
+        info_out[2] = s.bvh_depth;
+        info_out[3] = s.root_is_leaf;
+    }
+    return MFX_OK;
+}
+
 int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* b, double* div_out, double* sqrt_out) {
     if (n <= 0 || !a || !b || !div_out || !sqrt_out) return fail(MFX_E_INVALID, "bad selftest arguments");
     HIPCHECK(hipSetDevice(device));

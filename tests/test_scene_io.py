@@ -1,0 +1,107 @@
+"""Scene XML v0.1 / OBJ / MTL loading with the reference's semantics (Scene.fs:26-271,
+ObjModelLoader.fs:18-340, Obj_Mtl.fs:50-217). CPU only."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SCENES, scene
+from mafrixraytracing_amd.scene_io import InitSceneState, MaterialManager, SceneError, load_obj
+
+
+def test_cornell_scene_structure():
+    a = scene("cornell")
+    assert (a.width, a.height) == (300, 300)  # Scene.xml:67-70
+    assert len(a.prims) == 15 and set(a.prims["kind"].tolist()) == {1}  # every face is a quad -> Rect
+    assert a.albedo.tolist() == [[0.725, 0.71, 0.68], [0.14, 0.45, 0.091], [0.63, 0.065, 0.05]]
+    # XML shape order (floor, ceiling, backWall, rightWall, leftWall, shortBox x5, tallBox x5)
+    assert a.prims["material"].tolist() == [0, 0, 0, 1, 2] + [0] * 10
+    assert list(a.light["normal"]) == [0.0, -1.0, 0.0]
+    assert a.camera["fov"] == 120 and a.camera["aspect"] == 1.0
+
+
+def test_mtl_materials_come_first():
+    """cube.mtl's Ka=0 is added while the model loads, so XML materials start at slot 1."""
+    a = scene("cube_cornell")
+    assert a.albedo[0].tolist() == [0.0, 0.0, 0.0]
+    assert a.albedo[1].tolist() == [0.725, 0.71, 0.68]
+    kinds = a.prims["kind"].tolist()
+    assert kinds.count(0) == 12 and kinds.count(1) == 5
+
+
+def test_manager_is_process_global():
+    """MaterialManager.GetManager() is a singleton that keeps growing (IMaterial.fs:20-35)."""
+    MaterialManager.reset_default()
+    text = open(os.path.join(SCENES, "two_spheres_plane.xml")).read()
+    s1 = InitSceneState(text, base_dir=SCENES)
+    s2 = InitSceneState(text, base_dir=SCENES)
+    assert len(s1.manager.materials) == 6 and s2.manager is s1.manager
+    MaterialManager.reset_default()
+
+
+def _write(tmp_path, name, text):
+    p = tmp_path / name
+    p.write_text(text)
+    return str(p)
+
+
+XML = """<Scene version="0.1">
+  <Camera type="pinhole"><Point name="position" value="0,0,5"/><Vector name="direction" value="0,0,-1"/></Camera>
+  <Models><Model type="obj" name="m"><string name="filename" value="m.obj"/></Model></Models>
+  <Materials><Material type="lambert"><color name="albedo" value="0.5, 0.5,0.5"/></Material></Materials>
+  <Shapes><Shape type="shapelist"><string name="obj_ref" value="m.{group}"/><int name="material" value="0"/></Shape></Shapes>
+  <Light type="area"><string name="shape_ref" value="m.{light}"/><color name="intensity" value="1,1,1"/></Light>
+</Scene>"""
+
+OBJ = """# test
+v 0 0 0
+v 1 0 0
+v 1 1 0
+v 0 1 0
+vt 0 0
+vn 0 0 1
+g tri
+f -4 -3 -2
+g quad
+f 1/1/1 2/1/1 3/1/1 4/1/1
+g lamp
+f 1 4 3 2
+"""
+
+
+def test_defaults_negative_indices_and_extensions(tmp_path):
+    _write(tmp_path, "m.obj", OBJ)
+    st = InitSceneState(XML.format(group="tri", light="lamp"), base_dir=str(tmp_path), manager=MaterialManager())
+    assert (st.width, st.height) == (800, 800)  # Film defaults (Scene.fs:203-204)
+    assert st.camera["fov"] == 60.0 and st.camera["aspect"] == 1.333
+    assert len(st.prims) == 1 and st.prims[0].pts == ((0.0, 0, 0), (1.0, 0, 0), (1.0, 1, 0))
+    # light quad (1,4,3,2) -> normal of (v0,v1,v2) = (0,0,-1)
+    assert st.light["normal"] == (0.0, 0.0, -1.0)
+
+
+def test_errors_where_the_reference_asserts(tmp_path):
+    _write(tmp_path, "m.obj", OBJ)
+    with pytest.raises(SceneError):  # Map.find on a missing group
+        InitSceneState(XML.format(group="nope", light="lamp"), base_dir=str(tmp_path), manager=MaterialManager())
+    with pytest.raises(SceneError):  # light's first primitive is a triangle, not a Rect
+        InitSceneState(XML.format(group="tri", light="tri"), base_dir=str(tmp_path), manager=MaterialManager())
+    with pytest.raises(SceneError):
+        InitSceneState(XML.replace('version="0.1"', 'version="0.2"').format(group="tri", light="lamp"),
+                       base_dir=str(tmp_path), manager=MaterialManager())
+    _write(tmp_path, "bad.obj", "v 0 0 0\nv 1 0 0\nv 1 1 0\nv 0 1 0\nv 2 2 2\nf 1 2 3 4 5\n")
+    with pytest.raises(SceneError):  # 5-vertex face (ObjModelLoader.fs:90-92)
+        load_obj(str(tmp_path / "bad.obj"), MaterialManager())
+
+
+def test_converted_meshes_keep_counts():
+    for name, tris in [("spot", 5856), ("renault", 36996), ("spot16", 5856 * 16)]:
+        a = scene(name)
+        assert (a.prims["kind"] == 0).sum() == tris
+    assert scene("cube_cornell").prims["kind"].tolist().count(0) == 12
+
+
+def test_sphere_extension():
+    a = scene("two_spheres_plane")
+    sph = a.prims[a.prims["kind"] == 2]
+    assert len(sph) == 2 and sph["p"][:, 1, 0].tolist() == [0.5, 0.5]
+    assert np.allclose(sph["p"][:, 0, :], [[-0.6, 0.5, -1.0], [0.6, 0.5, -1.0]])
