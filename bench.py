@@ -165,8 +165,9 @@ def main():
                 sc.trace_accumulate(1, 10 ** 6)
                 s = sc.ray_counts()
             r = s[0] + s[1] + s[2]
-            stats = {"node_visits_per_ray": s[4] / r, "cluster_visits_per_ray": s[5] / r,
-                     "prim_tests_per_ray": s[6] / r, "rays_per_path": r / s[0]}
+            # closest-hit traversal counters in s[4..6], shadow in s[7..9]
+            stats = {"node_visits_per_ray": (s[4] + s[7]) / r, "cluster_visits_per_ray": (s[5] + s[8]) / r,
+                     "prim_tests_per_ray": (s[6] + s[9]) / r, "rays_per_path": r / s[0]}
             # 64 B per internal-node fetch, 64 B per reference-leaf (cluster) record,
             # 84 B per primitive test (80 B FP64 slot + 4 B info), 64 B ray record in + out
             bray = 64.0 * stats["node_visits_per_ray"] + 64.0 * stats["cluster_visits_per_ray"] + \

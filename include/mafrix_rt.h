@@ -96,6 +96,7 @@ typedef struct mfx_options {
 
 #define MFX_F_NONE 0
 #define MFX_F_COUNT_STATS 1 /* count traversal node/leaf/prim visits (slower; for the roofline model) */
+#define MFX_F_MEGAKERNEL 2  /* one persistent megakernel instead of the wavefront pipeline */
 
 typedef struct mfx_ctx mfx_ctx;
 
@@ -147,16 +148,22 @@ int mfx_sync(mfx_ctx* ctx);
 /* The HIP stream (hipStream_t) the context launches on, for event timing by the caller.   */
 int mfx_stream(mfx_ctx* ctx, void** stream);
 
-/* Device time (ms) of the last trace kernel launch, from HIP events recorded around it on the
- * context's stream (waits for that launch to finish).                                       */
+/* Device time (ms) of the last mfx_trace_accumulate, from HIP events recorded on the
+ * context's stream around its kernels (waits for them to finish).                           */
 int mfx_last_trace_ms(mfx_ctx* ctx, double* ms);
+
+/* Per-stage device time of the last mfx_trace_accumulate (wavefront pipeline), summed over its
+ * iterations from HIP events around each kernel: out[0] = whole call, out[1] = logic,
+ * out[2] = extension traversal, out[3] = shade, out[4] = shadow traversal, out[5] = iterations
+ * (kernel launches per stage). Megakernel: out[0] = out[2] = its single launch.              */
+int mfx_trace_timing(mfx_ctx* ctx, double out[8]);
 
 /* Ray counters of the last mfx_trace_accumulate / mfx_sample call:
  * out[0] = primary, out[1] = extension (closest-hit queries actually traced, excluding the
- * reference's discarded depth -1 query), out[2] = shadow, out[3] = paths,
- * out[4] = internal-node visits, out[5] = cluster (reference leaf) visits, out[6] = prim tests
- * (out[4..6] only with MFX_F_COUNT_STATS).                                                 */
-int mfx_ray_counts(mfx_ctx* ctx, double out[8]);
+ * reference's discarded depth -1 query), out[2] = shadow, out[3] = paths; with
+ * MFX_F_COUNT_STATS: out[4..6] = internal-node visits, cluster (reference leaf) visits and
+ * primitive tests of the closest-hit queries, out[7..9] the same for the shadow queries.     */
+int mfx_ray_counts(mfx_ctx* ctx, double out[16]);
 
 /* ---- query entry points (parity tests of the BVH/intersection layer) ----------------- */
 

@@ -18,6 +18,7 @@ MFX_PRIM_SPHERE = 2
 
 MFX_F_NONE = 0
 MFX_F_COUNT_STATS = 1
+MFX_F_MEGAKERNEL = 2
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -113,6 +114,7 @@ def _bind(lib):
         "mfx_stream": (C.c_int, [C.c_void_p, _P(C.c_void_p)]),
         "mfx_ray_counts": (C.c_int, [C.c_void_p, _dp]),
         "mfx_last_trace_ms": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_trace_timing": (C.c_int, [C.c_void_p, _dp]),
         "mfx_closest_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, C.c_double, _dp, _ip, _dp]),
         "mfx_any_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, _dp, _ip]),
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
@@ -132,7 +134,7 @@ def _bind(lib):
 EXPORTED_SYMBOLS = [
     "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_reset", "mfx_film_mean",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
-    "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
+    "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
     "mfx_fp64_selftest", "mfx_build_leaves", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -14,6 +15,7 @@
 #include "../../include/mafrix_rt.h"
 #include "mfx_device.h"
 #include "mfx_scene.h"
+#include "mfx_wavefront.h"
 
 namespace {
 thread_local std::string g_err;
@@ -44,11 +46,11 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
-    MfxCluster* d_clusters = nullptr;
-    int32_t* d_pinfo = nullptr;
-    MfxSlot* d_slots = nullptr;
+    uint8_t* d_blob = nullptr;
     MfxShade* d_shade = nullptr;
     double* d_albedo = nullptr;
+    MfxLight* d_light = nullptr;
+    MfxCamera* d_cam = nullptr;
     double* d_accum = nullptr;   // [3][npix] (the active accumulator)
     double* d_accum_own = nullptr;
     double* d_film = nullptr;    // [3][npix]
@@ -66,15 +68,30 @@ struct mfx_ctx {
     int64_t npix = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
+    // wavefront pipeline
+    WfParams wf{};
+    void* wf_mem = nullptr;
+    int32_t wf_pool = 0;
+    int64_t wf_pool_max = 1 << 23;
+    unsigned long long* d_wfctl = nullptr;
+    void* h_pin = nullptr;
+    hipEvent_t wf_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    double stage_ms[4] = {0, 0, 0, 0};
+    int iterations = 0;
+    bool mega_last = false;
+    int wf_ext_grid = 0, wf_shd_grid = 0;
 };
 
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    void* bufs[] = {c->d_nodes, c->d_clusters, c->d_pinfo, c->d_slots, c->d_shade, c->d_albedo, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters};
+    void* bufs[] = {c->d_nodes, c->d_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    if (c->h_pin) (void)hipHostFree(c->h_pin);
+    for (hipEvent_t e : c->wf_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -131,11 +148,11 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
-    CK(upload(&c->d_clusters, c->host.clusters));
-    CK(upload(&c->d_pinfo, c->host.pinfo));
-    CK(upload(&c->d_slots, c->host.slots));
+    CK(upload(&c->d_blob, c->host.blob));
     CK(upload(&c->d_shade, c->host.shade));
     CK(upload(&c->d_albedo, c->host.albedo));
+    CK(upload(&c->d_light, std::vector<MfxLight>{c->host.light}));
+    CK(upload(&c->d_cam, std::vector<MfxCamera>{c->host.camera}));
     const size_t plane = sizeof(double) * (size_t)c->npix;
     CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
     c->d_accum = c->d_accum_own;
@@ -143,16 +160,24 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_frame, 4 * plane));
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
-    CK(hipMalloc((void**)&c->d_counters, 8 * sizeof(unsigned long long)));
+    CK(hipMalloc((void**)&c->d_counters, 16 * WF_SHARDS * sizeof(unsigned long long)));
+    CK(hipMalloc((void**)&c->d_wfctl, WF_NCTL * sizeof(unsigned long long)));
+    CK(hipHostMalloc(&c->h_pin, 64, hipHostMallocDefault));
+    for (hipEvent_t& e : c->wf_ev) CK(hipEventCreate(&e));
+    if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(256, atoll(pm));
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
-    CK(hipMemset(c->d_counters, 0, 8 * sizeof(unsigned long long)));
+    CK(hipMemset(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long)));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, c->device));
     int bpc = 0;
     CK(mfx_trace_occupancy(c->stack_size, &bpc));
     bpc = std::max(1, std::min(bpc, 8));
     c->grid = prop.multiProcessorCount * bpc;
+    int ebpc = 0, sbpc = 0;
+    CK(mfx_wf_occupancy(c->stack_size, &ebpc, &sbpc));
+    c->wf_ext_grid = prop.multiProcessorCount * std::max(1, std::min(ebpc, 8));
+    c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
 #undef CK
     *out = c;
     return MFX_OK;
@@ -160,27 +185,132 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
 
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
+// Allocate (or grow) the wavefront path-slot pool (SoA).
+static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
+    if (pool <= c->wf_pool) return MFX_OK;
+    if (c->wf_mem) (void)hipFree(c->wf_mem);
+    c->wf_mem = nullptr;
+    c->wf_pool = 0;
+    const size_t P = (size_t)pool;
+    const size_t bytes = P * (WF_DOUBLES_PER_SLOT * 8 + WF_WORDS_PER_SLOT * 4) + 64 * 256;
+    hipError_t e = hipMalloc(&c->wf_mem, bytes);
+    if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
+                                     std::string("wavefront pool: ") + hipGetErrorString(e));
+    char* p = (char*)c->wf_mem;
+    auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
+    double** dbl[WF_DOUBLES_PER_SLOT - 1] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz,
+                                             &c->wf.tx, &c->wf.ty, &c->wf.tz, &c->wf.lx, &c->wf.ly, &c->wf.lz,
+                                             &c->wf.sdx, &c->wf.sdy, &c->wf.sdz, &c->wf.stmax, &c->wf.scx,
+                                             &c->wf.scy, &c->wf.scz, &c->wf.hit_t};
+    for (double** d : dbl) *d = (double*)take(P * 8);
+    c->wf.key = (uint64_t*)take(P * 8);
+    c->wf.hit_slot = (int32_t*)take(P * 4);
+    c->wf.rn = (uint32_t*)take(P * 4);
+    c->wf.depth = (int32_t*)take(P * 4);
+    c->wf.pixel = (int32_t*)take(P * 4);
+    c->wf.state = (int32_t*)take(P * 4);
+    c->wf_pool = pool;
+    return MFX_OK;
+}
+
+static void fill_scene_params(mfx_ctx* c, WfParams& P) {
+    P.nodes = c->d_nodes;
+    P.blob = c->d_blob;
+    P.shade = c->d_shade;
+    P.albedo = c->d_albedo;
+    P.light = c->d_light;
+    P.cam = c->d_cam;
+    P.accum = c->d_accum;
+}
+
+// The wavefront pipeline: logic -> extend -> shade -> shadow per iteration. Once every path
+// index of the call has been handed out (the host reads the 8 shard counters after each
+// iteration), max_depth more iterations finish the last paths and a final logic pass retires them.
+static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
+    const int W = c->host.width, H = c->host.height;
+    const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
+    const int64_t total = per_sample * ns;
+    const int64_t pool64 = std::min<int64_t>(total, c->wf_pool_max);
+    const int32_t pool = (int32_t)((pool64 + 2047) / 2048 * 2048);
+    int rc = wf_ensure_pool(c, pool);
+    if (rc) return rc;
+    WfParams P = c->wf;
+    fill_scene_params(c, P);
+    P.ctl = c->d_wfctl;
+    P.counters = c->d_counters;
+    P.total = total;
+    P.seed = c->seed;
+    P.sample_base = sample_base;
+    P.part_index = c->part_index;
+    P.part_count = c->part_count;
+    P.pool = pool;
+    P.width = W;
+    P.height = H;
+    P.max_depth = c->host.max_depth;
+    P.root_is_leaf = c->host.root_is_leaf;
+    P.stack_size = c->stack_size;
+    P.chunk = 256;
+    HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)pool, c->stream));
+    HIPCHECK(hipMemsetAsync(c->d_wfctl, 0, WF_NCTL * sizeof(unsigned long long), c->stream));
+    const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
+    double stage_ms[4] = {0, 0, 0, 0};
+    int iters = 0, drain = -1;
+    HIPCHECK(hipEventRecord(c->ev0, c->stream));
+    for (;;) {
+        HIPCHECK(hipEventRecord(c->wf_ev[0], c->stream));
+        HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, c->wf_ev + 1));
+        HIPCHECK(hipEventRecord(c->wf_ev[4], c->stream));
+        ++iters;
+        if (drain < 0) {
+            HIPCHECK(hipMemcpyAsync(c->h_pin, c->d_wfctl + WF_CTL_PATH, WF_SHARDS * 8, hipMemcpyDeviceToHost,
+                                    c->stream));
+            HIPCHECK(hipStreamSynchronize(c->stream));
+            bool all = true;
+            const unsigned long long* ctr = (const unsigned long long*)c->h_pin;
+            for (int g = 0; g < WF_SHARDS; ++g)
+                if ((int64_t)ctr[g] < total * (g + 1) / WF_SHARDS - total * g / WF_SHARDS) all = false;
+            if (all) drain = P.max_depth;  // no path starts after this iteration
+        } else {
+            HIPCHECK(hipStreamSynchronize(c->stream));
+            --drain;
+        }
+        for (int k = 0; k < 4; ++k) {
+            float f = 0.f;
+            HIPCHECK(hipEventElapsedTime(&f, c->wf_ev[k], c->wf_ev[k + 1]));
+            stage_ms[k] += f;
+        }
+        if (drain == 0) break;
+        if (iters > 10000000) return fail(MFX_E_STATE, "wavefront pipeline did not drain");
+    }
+    HIPCHECK(mfx_wf_finish(P, c->stream));  // retire the last finished paths
+    HIPCHECK(hipEventRecord(c->ev1, c->stream));
+    c->ev_valid = true;
+    for (int k = 0; k < 4; ++k) c->stage_ms[k] = stage_ms[k];
+    c->iterations = iters;
+    return MFX_OK;
+}
+
 int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
     HIPCHECK(hipSetDevice(c->device));
     const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
     HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
-    HIPCHECK(hipMemsetAsync(c->d_counters, 0, 8 * sizeof(unsigned long long), c->stream));
+    HIPCHECK(hipMemsetAsync(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long), c->stream));
+    c->mega_last = (c->flags & MFX_F_MEGAKERNEL) != 0;
     if (ns == 0) return MFX_OK;
+    if (!c->mega_last) return wf_trace(c, ns, sample_base);
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
-    P.clusters = c->d_clusters;
-    P.pinfo = c->d_pinfo;
-    P.slots = c->d_slots;
+    P.blob = c->d_blob;
     P.shade = c->d_shade;
     P.albedo = c->d_albedo;
     P.accum = c->d_accum;
     P.work_counter = c->d_work;
     P.counters = c->d_counters;
-    P.light = c->host.light;
-    P.cam = c->host.camera;
+    P.light = c->d_light;
+    P.cam = c->d_cam;
     P.seed = c->seed;
     P.sample_base = sample_base;
     P.nsamples = ns;
@@ -196,6 +326,23 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(mfx_launch_trace(P, (c->flags & MFX_F_COUNT_STATS) != 0, c->grid, c->stream));
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
+    return MFX_OK;
+}
+
+int mfx_trace_timing(mfx_ctx* c, double out[8]) {
+    if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    double total = 0;
+    int rc = mfx_last_trace_ms(c, &total);
+    if (rc) return rc;
+    for (int k = 0; k < 8; ++k) out[k] = 0.0;
+    out[0] = total;
+    if (c->mega_last) {
+        out[2] = total;
+        out[5] = 1;
+    } else {
+        for (int k = 0; k < 4; ++k) out[1 + k] = c->stage_ms[k];
+        out[5] = c->iterations;
+    }
     return MFX_OK;
 }
 
@@ -258,13 +405,17 @@ int mfx_stream(mfx_ctx* c, void** stream) {
     return MFX_OK;
 }
 
-int mfx_ray_counts(mfx_ctx* c, double out[8]) {
+int mfx_ray_counts(mfx_ctx* c, double out[16]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
     HIPCHECK(hipSetDevice(c->device));
-    unsigned long long h[8];
+    unsigned long long h[16 * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
     HIPCHECK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    for (int k = 0; k < 8; ++k) out[k] = (double)h[k];
+    for (int k = 0; k < 16; ++k) {
+        double v = 0;
+        for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[16 * g + k];
+        out[k] = v;
+    }
     out[3] = out[0];  // paths == primary rays
     return MFX_OK;
 }
@@ -336,9 +487,7 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         QueryParams Q;
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
-        Q.clusters = c->d_clusters;
-        Q.pinfo = c->d_pinfo;
-        Q.slots = c->d_slots;
+        Q.blob = c->d_blob;
         Q.shade = c->d_shade;
         Q.rays = d_rays;
         Q.tmax_per_ray = d_tmax;
@@ -397,7 +546,7 @@ int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t*
     if (leaf_count_out) std::copy(s.leaf_count.begin(), s.leaf_count.end(), leaf_count_out);
     if (nleaves_out) *nleaves_out = (int32_t)s.leaf_first.size();
     if (info_out) {
-        info_out[0] = (int32_t)s.clusters.size();
+        info_out[0] = s.nclusters;
         info_out[1] = (int32_t)s.nodes.size();
         info_out[2] = s.bvh_depth;
         info_out[3] = s.root_is_leaf;

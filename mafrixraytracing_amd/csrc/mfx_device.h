@@ -9,16 +9,14 @@
 
 struct TraceParams {
     const MfxNode* nodes;
-    const MfxCluster* clusters;
-    const int32_t* pinfo;
-    const MfxSlot* slots;
+    const uint8_t* blob;
     const MfxShade* shade;
     const double* albedo;
     double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
     unsigned long long* work_counter;
     unsigned long long* counters;    // [8] ray / traversal counters
-    MfxLight light;
-    MfxCamera cam;
+    const MfxLight* light;           // device copies (scalar-loaded where used; keeps SGPRs free)
+    const MfxCamera* cam;
     uint64_t seed;
     int64_t sample_base;             // first global sample index of this call
     int64_t nsamples;                // samples this context renders per pixel in this call
@@ -31,9 +29,7 @@ struct TraceParams {
 
 struct QueryParams {
     const MfxNode* nodes;
-    const MfxCluster* clusters;
-    const int32_t* pinfo;
-    const MfxSlot* slots;
+    const uint8_t* blob;
     const MfxShade* shade;
     const double* rays;
     const double* tmax_per_ray;

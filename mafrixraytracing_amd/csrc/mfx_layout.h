@@ -1,19 +1,17 @@
 // mfx_layout.h — HBM data layout shared by the host builder (mfx_scene.cpp) and the gfx950
-// kernels (mfx_kernels.hip). See DESIGN.md §2 for the layout rationale.
+// kernels. See DESIGN.md §2 for the layout rationale.
 //
-//   nodes[]    BVH2 over reference leaves ("clusters"), 64 B per internal node, both child
-//              boxes stored in the parent (one node fetch = two FP32 slab tests). child >= 0 is an
-//              internal node index, child < 0 is ~cluster. Boxes are the clusters' FP64 boxes
-//              rounded outward and widened by eps (conservative: every cluster the reference's
-//              FP64 slab test accepts is reached).
-//   clusters[] one per leaf of the reference's heap BVH (BvhNode.fs:36-39, count <= 3): its exact
-//              FP64 box (InitNode, BvhNode.fs:32-37) and its prim range in the reference's
-//              `indices` order. 64 B.
-//   pinfo[]    per prim, in `indices` order: kind | slot << 2.
-//   slots[]    FP64 triangle records {v0, e1 = v1 - v0, e2 = v2 - v0} (a Rect uses two
-//              consecutive slots, Rect.fs:11-20); a Sphere slot holds {center, radius}. 80 B.
-//   shade[]    per slot: face normal (FP64, Trangle.fs:108-113), material index, original prim
-//              and kind.
+//   nodes[]  BVH2 over the reference's leaves ("clusters"), 64 B per internal node, both child
+//            boxes stored in the parent (one node fetch = two FP32 slab tests). child >= 0 is an
+//            internal node index; child < 0 is ~(16-byte offset of a leaf record in blob[]).
+//            Boxes are the clusters' FP64 boxes rounded outward and widened by eps (conservative:
+//            every cluster the reference's FP64 slab test accepts is reached).
+//   blob[]   one record per leaf of the reference's heap BVH (BvhNode.fs:36-39, count <= 3), laid
+//            out in the traversal BVH's depth-first leaf order: a 64-B MfxLeaf header (its exact
+//            FP64 box, InitNode BvhNode.fs:32-37) followed by its primitives' FP64 MfxSlot records
+//            (a Triangle takes 1 slot, a Rect 2, a Sphere 1). A leaf is fetched in one round trip.
+//   shade[]  per slot: face normal (FP64, Trangle.fs:108-113) — the centre for a sphere —,
+//            material index, original primitive index and kind.
 #ifndef MFX_LAYOUT_H
 #define MFX_LAYOUT_H
 
@@ -30,11 +28,13 @@ struct alignas(16) MfxNode {
     int32_t child0, child1, pad0, pad1;
 };
 
-struct alignas(16) MfxCluster {
+struct alignas(16) MfxLeaf {
     double lo[3];
     double hi[3];
-    int32_t first;  // position in the reference `indices` array (heap order of leaves = ascending first)
-    int32_t count;  // 1..3
+    int32_t count;       // primitives in this reference leaf, 1..3
+    int32_t kinds;       // 2 bits per primitive, in the reference's `indices` order
+    int32_t first;       // position of the leaf in `indices` (heap order of leaves = ascending first)
+    int32_t shade_base;  // shade[] index of the leaf's first slot
 };
 
 struct alignas(16) MfxSlot {
@@ -45,7 +45,7 @@ struct alignas(16) MfxSlot {
 };
 
 struct alignas(16) MfxShade {
-    double n[3];        // face normal of this triangle slot (unused for spheres)
+    double n[3];        // face normal of this triangle slot; a sphere's centre
     int32_t material;   // MaterialManager slot
     int32_t prim_kind;  // original primitive index (mfx_prim order) << 2 | MFX_KIND_*
 };

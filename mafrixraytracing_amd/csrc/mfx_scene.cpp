@@ -336,25 +336,25 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
     s.max_depth = d->max_depth;
     s.albedo.assign(d->albedo, d->albedo + 3 * (size_t)d->nmat);
 
-    // ---- primitives: FP64 bounds + slot records -------------------------------------------
+    // ---- primitives: FP64 bounds + slot records (in primitive order for now) ---------------
     std::vector<Box> pb(n);
-    std::vector<int32_t> slot_of(n);
-    s.slots.clear();
-    s.shade.clear();
+    std::vector<int32_t> slot_of(n), nslot_of(n);
+    std::vector<MfxSlot> pslots;
+    std::vector<MfxShade> pshade;
     auto add_tri = [&](D3 v0, D3 v1, D3 v2, int mat, int prim, int kind) {
         MfxSlot t{};
         D3 e1 = sub(v1, v0), e2 = sub(v2, v0);
         put(t.a, v0);
         put(t.b, e1);
         put(t.c, e2);
-        s.slots.push_back(t);
+        pslots.push_back(t);
         MfxShade sh{};
         D3 a = cross(e1, e2);
         double al = len(a);
         put(sh.n, D3{a.x / al, a.y / al, a.z / al});  // Trangle.fs:110-111
         sh.material = mat;
         sh.prim_kind = (prim << 2) | kind;
-        s.shade.push_back(sh);
+        pshade.push_back(sh);
     };
     for (int i = 0; i < n; ++i) {
         const mfx_prim& p = d->prims[i];
@@ -362,7 +362,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             err = "primitive " + std::to_string(i) + " has material index out of range";
             return false;
         }
-        slot_of[i] = (int)s.slots.size();
+        slot_of[i] = (int)pslots.size();
         if (p.kind == MFX_PRIM_TRIANGLE) {
             D3 v0 = d3(p.p[0]), v1 = d3(p.p[1]), v2 = d3(p.p[2]);
             pb[i] = tri_box(v0, v1, v2);
@@ -380,15 +380,17 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             MfxSlot t{};
             put(t.a, c);
             t.b[0] = r;
-            s.slots.push_back(t);
+            pslots.push_back(t);
             MfxShade sh{};
+            put(sh.n, c);  // the shade record of a sphere carries its centre
             sh.material = p.material;
             sh.prim_kind = (i << 2) | MFX_KIND_SPHERE;
-            s.shade.push_back(sh);
+            pshade.push_back(sh);
         } else {
             err = "primitive " + std::to_string(i) + " has an unknown kind";
             return false;
         }
+        nslot_of[i] = (int)pslots.size() - slot_of[i];
     }
 
     // ---- reference leaf grouping -----------------------------------------------------------
@@ -401,21 +403,18 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         Box root = rb.bound(0, n);
         rb.subdivide(0, n, root);
     }
-    s.pinfo.resize(n);
-    for (int k = 0; k < n; ++k) {
-        int p = s.ref_indices[k];
-        s.pinfo[k] = d->prims[p].kind | (slot_of[p] << 2);
-    }
     const int nc = (int)s.leaf_first.size();
-    s.clusters.resize(nc);
+    std::vector<MfxLeaf> leaves(nc);
     for (int c = 0; c < nc; ++c) {
-        MfxCluster& cl = s.clusters[c];
+        MfxLeaf& lf = leaves[c];
         Box b = pb[s.ref_indices[s.leaf_first[c]]];
         for (int k = 1; k < s.leaf_count[c]; ++k) b = join(b, pb[s.ref_indices[s.leaf_first[c] + k]]);
-        put(cl.lo, b.lo);
-        put(cl.hi, b.hi);
-        cl.first = s.leaf_first[c];
-        cl.count = s.leaf_count[c];
+        put(lf.lo, b.lo);
+        put(lf.hi, b.hi);
+        lf.first = s.leaf_first[c];
+        lf.count = s.leaf_count[c];
+        lf.kinds = 0;
+        for (int k = 0; k < lf.count; ++k) lf.kinds |= d->prims[s.ref_indices[lf.first + k]].kind << (2 * k);
     }
 
     // ---- camera (Camera.fs:96-133) and light (Light.fs:31-40) -------------------------------
@@ -475,8 +474,8 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
     for (int c = 0; c < nc; ++c) {
         FBox f;
         for (int a = 0; a < 3; ++a) {
-            f.lo[a] = round_down(s.clusters[c].lo[a] - (double)s.eps);
-            f.hi[a] = round_up(s.clusters[c].hi[a] + (double)s.eps);
+            f.lo[a] = round_down(leaves[c].lo[a] - (double)s.eps);
+            f.hi[a] = round_up(leaves[c].hi[a] + (double)s.eps);
             sb.cent[3 * c + a] = 0.5f * (f.lo[a] + f.hi[a]);
         }
         sb.cb[c] = f;
@@ -491,5 +490,48 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         s.root_is_leaf = 0;
         s.bvh_depth = sb.max_depth;
     }
+
+    // ---- leaf blob in depth-first leaf order; child refs become ~(16-byte offset) ----------
+    std::vector<int> order;
+    order.reserve(nc);
+    if (nc == 1) {
+        order.push_back(0);
+    } else {
+        std::vector<int> st{0};  // depth-first, child0 before child1
+        while (!st.empty()) {
+            const int ref = st.back();
+            st.pop_back();
+            if (ref < 0) {
+                order.push_back(~ref);
+            } else {
+                st.push_back(s.nodes[ref].child1);
+                st.push_back(s.nodes[ref].child0);
+            }
+        }
+    }
+    std::vector<int32_t> offset16(nc);
+    s.blob.clear();
+    s.shade.clear();
+    for (int c : order) {
+        MfxLeaf lf = leaves[c];
+        lf.shade_base = (int32_t)s.shade.size();
+        offset16[c] = (int32_t)(s.blob.size() / 16);
+        const uint8_t* hp = (const uint8_t*)&lf;
+        s.blob.insert(s.blob.end(), hp, hp + sizeof(MfxLeaf));
+        for (int k = 0; k < lf.count; ++k) {
+            const int p = s.ref_indices[lf.first + k];
+            for (int j = 0; j < nslot_of[p]; ++j) {
+                const uint8_t* sp = (const uint8_t*)&pslots[slot_of[p] + j];
+                s.blob.insert(s.blob.end(), sp, sp + sizeof(MfxSlot));
+                s.shade.push_back(pshade[slot_of[p] + j]);
+            }
+        }
+    }
+    s.blob.resize(s.blob.size() + 3 * sizeof(MfxSlot), 0);  // speculative slot loads stay in bounds
+    for (MfxNode& nd : s.nodes) {
+        if (nd.child0 < 0) nd.child0 = ~offset16[~nd.child0];
+        if (nd.child1 < 0) nd.child1 = ~offset16[~nd.child1];
+    }
+    s.nclusters = nc;
     return true;
 }

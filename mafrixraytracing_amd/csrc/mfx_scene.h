@@ -14,10 +14,9 @@ struct MfxHostScene {
     std::vector<int32_t> leaf_first, leaf_count;       // leaves in heap (DFS) order
     // device images
     std::vector<MfxNode> nodes;
-    std::vector<MfxCluster> clusters;
-    std::vector<int32_t> pinfo;
-    std::vector<MfxSlot> slots;
-    std::vector<MfxShade> shade;
+    std::vector<uint8_t> blob;    // MfxLeaf headers + inline MfxSlot records, DFS leaf order
+    std::vector<MfxShade> shade;  // per slot, in blob order
+    int32_t nclusters = 0;
     std::vector<double> albedo;  // [nmat][3]
     MfxLight light;
     MfxCamera camera;

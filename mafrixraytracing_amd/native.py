@@ -98,7 +98,7 @@ class NativeContext:
         return s.value or 0
 
     def ray_counts(self) -> np.ndarray:
-        out = np.zeros(8)
+        out = np.zeros(16)
         check(self.lib.mfx_ray_counts(self._h, dptr(out)), "mfx_ray_counts")
         return out
 
@@ -106,6 +106,12 @@ class NativeContext:
         ms = C.c_double()
         check(self.lib.mfx_last_trace_ms(self._h, C.byref(ms)), "mfx_last_trace_ms")
         return ms.value
+
+    def trace_timing(self) -> dict:
+        out = np.zeros(8)
+        check(self.lib.mfx_trace_timing(self._h, dptr(out)), "mfx_trace_timing")
+        return {"total_ms": out[0], "logic_ms": out[1], "extend_ms": out[2], "shade_ms": out[3],
+                "shadow_ms": out[4], "iterations": int(out[5])}
 
     def closest_hit(self, rays: np.ndarray, tmin: float = 1e-6, tmax: float = 99999999.0):
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)

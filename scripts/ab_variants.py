@@ -1,0 +1,50 @@
+#!/usr/bin/env python3
+"""A/B timing of libmafrix_rt variants (build_variants/*.so) on the bench workload, each in its own
+process, interleaved over rounds (cdna_hip_programming.md §5.4 rule 24)."""
+import glob
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CHILD = r'''
+import sys, json, time
+sys.path.insert(0, ROOT)
+import mafrixraytracing_amd.abi as abi
+abi.load_library(LIB); abi._lib = abi.load_library(LIB)
+from mafrixraytracing_amd.native import NativeContext, DEFAULT_SEED
+from mafrixraytracing_amd.scene_io import load_scene_file
+a = load_scene_file(SCENE)
+ctx = NativeContext(a, seed=DEFAULT_SEED)
+res = []
+for k in range(STEPS + 1):
+    ctx.accum_clear(); t = time.perf_counter(); ctx.trace_accumulate(SPP, k * SPP); ctx.sync(); dt = time.perf_counter() - t
+    c = ctx.ray_counts(); ms = ctx.last_trace_ms()
+    if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms))
+print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res]}))
+'''
+
+
+def main():
+    libs = sorted(glob.glob(os.path.join(ROOT, "build_variants", "*.so")))
+    scene = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "spot.xml")
+    rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
+    spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+    out = {os.path.basename(l): [] for l in libs}
+    for r in range(rounds):
+        for l in libs:
+            code = CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(l)).replace("SCENE", repr(scene)) \
+                .replace("STEPS", "2").replace("SPP", str(spp))
+            p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+            if p.returncode != 0:
+                print(os.path.basename(l), "FAILED", p.stderr[-2000:], flush=True)
+                continue
+            d = json.loads(p.stdout.strip().splitlines()[-1])
+            out[os.path.basename(l)] += d["mrays"]
+            print(os.path.basename(l), "round", r, ["%.1f" % x for x in d["mrays"]], "ms", ["%.2f" % x for x in d["ms"]], flush=True)
+    print("SUMMARY", json.dumps({k: (max(v) if v else None) for k, v in out.items()}))
+
+
+if __name__ == "__main__":
+    main()
