@@ -63,12 +63,18 @@ typedef struct mfx_quad_light {
     double intensity[3];
 } mfx_quad_light;
 
-/* PinholeCamera(pos, dir, fov, aspectRatio) (Core/Camera.fs:122-133). */
+/* PinholeCamera(pos, dir, fov, aspectRatio) (Core/Camera.fs:122-133). With derived == 0 the
+ * library runs the constructor (CameraCoordinate + tan); with derived != 0 it takes an existing
+ * camera's fields as they are — PinholeCamera.position, .topleft, .coord.right, .coord.down —
+ * which is what the F# shim passes, so GetRay (Camera.fs:134-139) starts from identical bits. */
 typedef struct mfx_pinhole {
     double position[3];
     double direction[3];
     double fov;    /* degrees, as in Scene.xml; effective horizontal FOV is fov/2 (Camera.fs:125) */
     double aspect; /* aspectratio attribute; NOT derived from the film size (Scene.fs:61-72) */
+    double topleft[3], right[3], down[3];
+    int32_t derived;
+    int32_t reserved;
 } mfx_pinhole;
 
 /* The scene a `Scene` is constructed from (Scene.fs:298-313). Deep-copied by mfx_create. */

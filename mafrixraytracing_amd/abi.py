@@ -34,7 +34,9 @@ class MfxQuadLight(C.Structure):
 
 class MfxPinhole(C.Structure):
     _fields_ = [("position", C.c_double * 3), ("direction", C.c_double * 3),
-                ("fov", C.c_double), ("aspect", C.c_double)]
+                ("fov", C.c_double), ("aspect", C.c_double),
+                ("topleft", C.c_double * 3), ("right", C.c_double * 3), ("down", C.c_double * 3),
+                ("derived", C.c_int32), ("reserved", C.c_int32)]
 
 
 class MfxSceneDesc(C.Structure):

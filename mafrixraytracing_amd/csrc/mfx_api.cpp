@@ -72,7 +72,7 @@ struct mfx_ctx {
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
-    int64_t wf_pool_max = 1 << 23;
+    int64_t wf_pool_max = 1 << 24;
     unsigned long long* d_wfctl = nullptr;
     void* h_pin = nullptr;
     hipEvent_t wf_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};

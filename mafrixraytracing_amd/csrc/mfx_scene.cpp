@@ -433,6 +433,11 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         put(s.camera.topleft, tl);
         put(s.camera.right, right);
         put(s.camera.down, D3{-up.x, -up.y, -up.z});
+        if (c.derived) {  // an existing PinholeCamera's fields, taken as they are
+            put(s.camera.topleft, d3(c.topleft));
+            put(s.camera.right, d3(c.right));
+            put(s.camera.down, d3(c.down));
+        }
     }
     {
         const mfx_quad_light& L = d->light;

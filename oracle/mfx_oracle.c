@@ -513,6 +513,11 @@ OScene* oracle_create(const mfx_scene_desc* d) {
     s->light_normal = arr3(d->light.normal);
     s->light_color = c3(d->light.intensity[0], d->light.intensity[1], d->light.intensity[2]);
     s->cam = pinhole_make(arr3(d->camera.position), arr3(d->camera.direction), d->camera.fov, d->camera.aspect);
+    if (d->camera.derived) { /* an existing PinholeCamera's fields (Camera.fs:113-119) */
+        s->cam.topleft = arr3(d->camera.topleft);
+        s->cam.right = arr3(d->camera.right);
+        s->cam.down = arr3(d->camera.down);
+    }
     s->width = d->width;
     s->height = d->height;
     s->max_depth = d->max_depth;

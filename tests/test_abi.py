@@ -33,7 +33,7 @@ def test_struct_layouts_match_header():
     from mafrixraytracing_amd.abi import MfxOptions, MfxPinhole, MfxPrim, MfxQuadLight, MfxSceneDesc
     assert C.sizeof(MfxPrim) == 104
     assert C.sizeof(MfxQuadLight) == 18 * 8
-    assert C.sizeof(MfxPinhole) == 8 * 8
+    assert C.sizeof(MfxPinhole) == 17 * 8 + 8
     assert C.sizeof(MfxOptions) == 24
     assert C.sizeof(MfxSceneDesc) == 8 + 8 + 8 + 4 * 4 + C.sizeof(MfxQuadLight) + C.sizeof(MfxPinhole)
 
