@@ -11,8 +11,10 @@ Rays counted = primary + extension (closest-hit queries actually traced) + shado
 from the kernel's own counters. Inputs (scene, BVH) are resident in HBM before timing starts.
 
 Extra objects on the JSON line:
-  roofline      the trace kernel's algorithmic bytes per launch / its HIP-event duration vs HBM
-                8 TB/s; bytes per ray from the kernel's traversal counters
+  roofline      the dominant kernel — k_traverse<false,false>, the closest-hit traversal of the
+                wavefront pipeline — algorithmic bytes per launch / its HIP-event duration vs HBM
+                8 TB/s; bytes per ray from the kernel's traversal counters; traffic =
+                PMC HBM bytes per launch (profiles/traffic_spot_1080p.json, scripts/profile_r01.sh)
   cpu_baseline  the CPU oracle (FP64 restatement of the reference algorithm) timed on this host
                 on a bounded random sample of the same workload's paths (rank 0, N = 1 only)
 """
@@ -43,6 +45,7 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the traversal-counter pass")
+    ap.add_argument("--megakernel", action="store_true", help="persistent megakernel instead of the wavefront")
     return ap.parse_args()
 
 
@@ -95,7 +98,7 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
 
     import numpy as np
-    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS
+    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE
     from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
@@ -110,7 +113,8 @@ def main():
     W, H = arrays.width, arrays.height
     npix = W * H
     spp_step = args.spp * world
-    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, part_index=rank, part_count=world)
+    mode = MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE
+    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world)
     acc = None
     if world > 1:
         acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
@@ -135,12 +139,14 @@ def main():
     barrier()
     t0 = time.perf_counter()
     rays = 0.0
-    kms = []
+    closest_rays = 0.0
+    timings = []
     for k in range(args.steps):
         step(args.warmup + k)
         c = ctx.ray_counts()
         rays += c[0] + c[1] + c[2]
-        kms.append(ctx.last_trace_ms())
+        closest_rays += c[0] + c[1]
+        timings.append(ctx.trace_timing())
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -152,39 +158,71 @@ def main():
         rays_all = float(r.item())
     else:
         rays_all = rays
-    rays_per_launch = rays / args.steps
-    kernel_ms = float(np.mean(kms))
+    stage_ms = {k: float(np.mean([t[k] for t in timings]))
+                for k in ("total_ms", "logic_ms", "extend_ms", "shade_ms", "shadow_ms", "iterations")}
 
     result = None
     if rank == 0:
         # traversal counters (separate, untimed pass at 1 spp of the same frame)
-        bray = None
         stats = None
         if not args.no_stats:
-            with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS) as sc:
+            with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS | mode) as sc:
                 sc.trace_accumulate(1, 10 ** 6)
                 s = sc.ray_counts()
-            r = s[0] + s[1] + s[2]
+            rc, rs = s[0] + s[1], s[2]
             # closest-hit traversal counters in s[4..6], shadow in s[7..9]
-            stats = {"node_visits_per_ray": (s[4] + s[7]) / r, "cluster_visits_per_ray": (s[5] + s[8]) / r,
-                     "prim_tests_per_ray": (s[6] + s[9]) / r, "rays_per_path": r / s[0]}
-            # 64 B per internal-node fetch, 64 B per reference-leaf (cluster) record,
-            # 84 B per primitive test (80 B FP64 slot + 4 B info), 64 B ray record in + out
-            bray = 64.0 * stats["node_visits_per_ray"] + 64.0 * stats["cluster_visits_per_ray"] + \
-                84.0 * stats["prim_tests_per_ray"] + 64.0
+            stats = {"closest": {"node_visits_per_ray": s[4] / rc, "cluster_visits_per_ray": s[5] / rc,
+                                 "prim_tests_per_ray": s[6] / rc},
+                     "shadow": {"node_visits_per_ray": s[7] / rs, "cluster_visits_per_ray": s[8] / rs,
+                                "prim_tests_per_ray": s[9] / rs},
+                     "all": {"node_visits_per_ray": (s[4] + s[7]) / (rc + rs),
+                             "cluster_visits_per_ray": (s[5] + s[8]) / (rc + rs),
+                             "prim_tests_per_ray": (s[6] + s[9]) / (rc + rs)},
+                     "rays_per_path": (rc + rs) / s[0]}
+
+        def bytes_per_ray(c):
+            # SURVEY.md §8d / DESIGN.md §7: 32 B per BVH2 node visit (internal or leaf), 36 B per
+            # primitive test, 64 B ray record; priced from the frozen fixture when it has the scene
+            return 32.0 * (c["node_visits_per_ray"] + c["cluster_visits_per_ray"]) + \
+                36.0 * c["prim_tests_per_ray"] + 64.0
+
+        fixture = None
+        fx = os.path.join(ROOT, "profiles", "bray_fixture.json")
+        sname = os.path.splitext(os.path.basename(args.scene))[0]
+        if os.path.exists(fx):
+            with open(fx) as f:
+                fixture = json.load(f)["scenes"].get(sname)
+
         roofline = None
-        if bray is not None:
-            achieved = rays_per_launch * bray / (kernel_ms / 1e3) / 1e9
+        if stats is not None:
+            if args.megakernel:
+                kname, kms, krays, launches = "trace_kernel<false>", stage_ms["total_ms"], rays / args.steps, 1
+                bray = bytes_per_ray(stats["all"])
+                if fixture:
+                    fc, fs = fixture["closest"], fixture["shadow"]
+                    n_c, n_s = fixture["closest_rays"], fixture["shadow_rays"]
+                    bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
+            else:
+                kname, kms, krays = "k_traverse<false, false>", stage_ms["extend_ms"], closest_rays / args.steps
+                launches = stage_ms["iterations"]
+                bray = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
+            # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
+            achieved = krays * bray / (kms / 1e3) / 1e9
             traffic = None
             tf = os.path.join(ROOT, "profiles", "traffic_spot_1080p.json")
-            if os.path.exists(tf) and world == 1:
+            if os.path.exists(tf) and world == 1 and args.spp == 64 and args.scene == SPOT_SCENE:
                 with open(tf) as f:
-                    traffic = json.load(f).get("hbm_bytes_per_launch")
+                    traffic = json.load(f).get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch")
             roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                        "kernel": "trace_kernel", "kernel_ms": round(kernel_ms, 3),
-                        "bytes_per_ray": round(bray, 1), "rays_per_launch": int(rays_per_launch),
-                        "counters": {k: round(v, 3) for k, v in stats.items()}}
+                        "kernel": kname, "launches_per_step": launches,
+                        "avg_launch_ms": round(kms / launches, 4),
+                        "bytes_per_ray": round(bray, 1), "bytes_per_ray_source":
+                            "profiles/bray_fixture.json (frozen)" if fixture else "live counters",
+                        "rays_per_launch": round(krays / launches, 1),
+                        "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
+                        "counters": {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
+                                         else round(d, 4)) for g, d in stats.items()}}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
@@ -198,6 +236,7 @@ def main():
                                    f"{args.spp} spp per GPU per step",
                        "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
                        "spp_per_gpu": args.spp, "global_spp_per_step": spp_step, "max_depth": 3,
+                       "pipeline": "megakernel" if args.megakernel else "wavefront",
                        "parallelism": f"sample-partition x{world}" + (" + RCCL reduce" if world > 1 else "")},
             "roofline": roofline, "cpu_baseline": cpu,
         }

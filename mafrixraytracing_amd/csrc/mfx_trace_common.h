@@ -126,14 +126,27 @@ struct Stats {
 // One reference leaf: exact FP64 box test, then Array.minBy over its primitives with key
 // (hit ? t : tMax), first minimum wins (BvhNode.fs:76-80). Returns whether the leaf's result is
 // a hit; t and the shade[] index of the hit slot. The header and the slots are contiguous.
-template <bool STATS>
+//
+// The leaf's result is (box hit) && (minBy result is a hit); neither test has side effects, so
+// the primitives run first and the FP64 box test (six divisions) only when it can still change
+// the answer: the minBy result is a hit and, for closest queries, its t does not exceed the best
+// hit so far (`reject_above`; a larger t can never be accepted by the caller's tie rule). SHADOW
+// queries stop at the first primitive hit with t < tMax: its key is below every miss's key
+// (tMax), so the minBy result is a hit whatever follows. A hit beyond tMax (Triangle.Hit ignores
+// tMax, Trangle.fs:148) does not stop the scan — a later miss can still win the minBy.
+template <bool SHADOW, bool STATS>
 __device__ __forceinline__ bool cluster_hit(const SceneView& S, int off16, DV o, DV d, double tMin, double tMax,
-                                            double& t_out, int& slot_out, int& first_out, Stats& st) {
+                                            double reject_above, double& t_out, int& slot_out, int& first_out,
+                                            Stats& st) {
     const MfxLeaf* __restrict__ lf = (const MfxLeaf*)(S.blob + (size_t)off16 * 16);
     const MfxSlot* __restrict__ sl = (const MfxSlot*)(lf + 1);
-    const MfxLeaf c = *lf;
+    // only the 16-B tail (count, kinds, first, shade_base) now; the box is read (L1/L2 hit)
+    // after the primitives, when needed — keeping six doubles live costs occupancy
+    struct Meta {
+        int32_t count, kinds, first, shade_base;
+    };
+    const Meta c = *(const Meta*)((const uint8_t*)lf + offsetof(MfxLeaf, count));
     if (STATS) st.clusters++;
-    if (!aabb_hit64(c.lo, c.hi, o, d, tMin, tMax)) return false;
     bool best_hit = false;
     double best_key = 0.0, best_t = 0.0;
     int best_slot = -1;
@@ -166,19 +179,71 @@ __device__ __forceinline__ bool cluster_hit(const SceneView& S, int off16, DV o,
             best_t = t;
             best_slot = hs;
         }
+        if (SHADOW && h && t < tMax) break;
     }
-    if (best_hit) {
-        t_out = best_t;
-        slot_out = c.shade_base + best_slot;
-        first_out = c.first;
-    }
-    return best_hit;
+    if (!best_hit || best_t > reject_above) return false;
+    if (!aabb_hit64(lf->lo, lf->hi, o, d, tMin, tMax)) return false;
+    t_out = best_t;
+    slot_out = c.shade_base + best_slot;
+    first_out = c.first;
+    return true;
 }
 
 __device__ __forceinline__ float f_round_up(double x) {
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, __builtin_inff());
     return f;
+}
+
+// FP32 ray for the cluster-BVH slab tests
+struct RayF {
+    float ix, iy, iz, oix, oiy, oiz;
+};
+__device__ __forceinline__ RayF make_rayf(DV o, DV d) {
+    // tiny direction components clamped so 1/d stays finite (no 0*inf NaNs)
+    float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
+    const float tiny = 1e-20f;
+    if (fabsf(dx) < tiny) dx = copysignf(tiny, dx);
+    if (fabsf(dy) < tiny) dy = copysignf(tiny, dy);
+    if (fabsf(dz) < tiny) dz = copysignf(tiny, dz);
+    RayF r;
+    r.ix = 1.0f / dx; r.iy = 1.0f / dy; r.iz = 1.0f / dz;
+    r.oix = (float)o.x * r.ix; r.oiy = (float)o.y * r.iy; r.oiz = (float)o.z * r.iz;
+    return r;
+}
+
+#define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
+
+// One internal-node step of the cluster BVH2, branch-free: both child slab tests, then
+// near-first descent / push of the far child / pop, chosen with selects. The far child is
+// written to the stack slot unconditionally and sp only advances when both children are hit;
+// the pop candidate (top of stack) is read before the node's boxes arrive, so the LDS read
+// overlaps the HBM/L2 load. Returns the next node: >= 0 internal, < 0 a leaf (~offset), or
+// MFX_TRAV_EXIT when nothing is left.
+__device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
+                                         int* __restrict__ stack, int& sp) {
+    const int top = stack[(sp > 0 ? sp - 1 : 0) * 64];
+    const MfxNode nd = nodes[node];
+    float a0 = fmaf(nd.c0lox, r.ix, -r.oix), a1 = fmaf(nd.c0hix, r.ix, -r.oix);
+    float b0 = fmaf(nd.c0loy, r.iy, -r.oiy), b1 = fmaf(nd.c0hiy, r.iy, -r.oiy);
+    float c0 = fmaf(nd.c0loz, r.iz, -r.oiz), c1 = fmaf(nd.c0hiz, r.iz, -r.oiz);
+    const float n0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+    const float f0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+    a0 = fmaf(nd.c1lox, r.ix, -r.oix); a1 = fmaf(nd.c1hix, r.ix, -r.oix);
+    b0 = fmaf(nd.c1loy, r.iy, -r.oiy); b1 = fmaf(nd.c1hiy, r.iy, -r.oiy);
+    c0 = fmaf(nd.c1loz, r.iz, -r.oiz); c1 = fmaf(nd.c1hiz, r.iz, -r.oiz);
+    const float n1 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+    const float f1 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+    const bool h0 = n0 <= f0, h1 = n1 <= f1;
+    const bool both = h0 && h1;
+    const bool take1 = h1 && (!h0 || n1 < n0);  // child 1 is the one to descend into
+    const int near = take1 ? nd.child1 : nd.child0;
+    const int far = take1 ? nd.child0 : nd.child1;
+    stack[sp * 64] = far;  // kept only if sp advances
+    const bool any = h0 || h1;
+    const bool pop = !any && sp > 0;
+    sp += (both ? 1 : 0) - (pop ? 1 : 0);
+    return any ? near : (pop ? top : MFX_TRAV_EXIT);
 }
 
 // Bvh.Hit over the cluster BVH2. SHADOW: returns occluded (any leaf reporting a hit; the
@@ -195,59 +260,30 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
     if (S.root_is_leaf) {
         double t;
         int s, f;
-        if (cluster_hit<STATS>(S, 0, o, d, tMin, tMax, t, s, f, st)) {
+        if (cluster_hit<SHADOW, STATS>(S, 0, o, d, tMin, tMax, __builtin_inf(), t, s, f, st)) {
             t_best = t;
             slot_best = s;
             return true;
         }
         return false;
     }
-    // FP32 ray; tiny direction components clamped so 1/d stays finite (no 0*inf NaNs)
-    float dx = (float)d.x, dy = (float)d.y, dz = (float)d.z;
-    const float tiny = 1e-20f;
-    if (fabsf(dx) < tiny) dx = copysignf(tiny, dx);
-    if (fabsf(dy) < tiny) dy = copysignf(tiny, dy);
-    if (fabsf(dz) < tiny) dz = copysignf(tiny, dz);
-    const float ix = 1.0f / dx, iy = 1.0f / dy, iz = 1.0f / dz;
-    const float oix = (float)o.x * ix, oiy = (float)o.y * iy, oiz = (float)o.z * iz;
+    const RayF rf = make_rayf(o, d);
     float tlim = f_round_up(tMax);
     int sp = 0;
     int node = 0;
     while (true) {
         // ---- internal nodes ----
         while (node >= 0) {
-            const MfxNode nd = S.nodes[node];
             if (STATS) st.nodes++;
-            float a0 = fmaf(nd.c0lox, ix, -oix), a1 = fmaf(nd.c0hix, ix, -oix);
-            float b0 = fmaf(nd.c0loy, iy, -oiy), b1 = fmaf(nd.c0hiy, iy, -oiy);
-            float c0 = fmaf(nd.c0loz, iz, -oiz), c1 = fmaf(nd.c0hiz, iz, -oiz);
-            float n0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-            float f0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-            a0 = fmaf(nd.c1lox, ix, -oix); a1 = fmaf(nd.c1hix, ix, -oix);
-            b0 = fmaf(nd.c1loy, iy, -oiy); b1 = fmaf(nd.c1hiy, iy, -oiy);
-            c0 = fmaf(nd.c1loz, iz, -oiz); c1 = fmaf(nd.c1hiz, iz, -oiz);
-            float n1 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-            float f1 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-            const bool h0 = n0 <= f0, h1 = n1 <= f1;
-            if (h0 && h1) {
-                int near = nd.child0, far = nd.child1;
-                if (n1 < n0) { near = nd.child1; far = nd.child0; }
-                stack[(sp++) * 64] = far;
-                node = near;
-            } else if (h0) {
-                node = nd.child0;
-            } else if (h1) {
-                node = nd.child1;
-            } else {
-                if (sp == 0) return found;
-                node = stack[(--sp) * 64];
-            }
+            node = node_step(S.nodes, node, rf, tlim, stack, sp);
         }
+        if (node == MFX_TRAV_EXIT) return found;
         // ---- leaf: one reference leaf (cluster) ----
         {
             double t;
             int s, f;
-            if (cluster_hit<STATS>(S, ~node, o, d, tMin, tMax, t, s, f, st)) {
+            if (cluster_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, found ? t_best : __builtin_inf(), t, s, f,
+                                           st)) {
                 if (SHADOW) {
                     t_best = t;
                     slot_best = s;

@@ -21,6 +21,10 @@
 #include "mfx_trace_common.h"
 #include "mfx_wavefront.h"
 
+#ifndef MFX_TRAV_WAVES
+#define MFX_TRAV_WAVES 1  // min waves per SIMD requested from the register allocator
+#endif
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ uint64_t lanes_below() { return (1ULL << lane_id()) - 1ULL; }
 
@@ -131,7 +135,7 @@ __global__ void __launch_bounds__(1024) k_logic(WfParams P) {
 // Persistent traversal (closest hit or shadow) with per-lane dynamic fetch
 // ------------------------------------------------------------------------------------------------
 template <bool SHADOW, bool STATS>
-__global__ void __launch_bounds__(256) k_traverse(WfParams P) {
+__global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_traverse(WfParams P) {
     extern __shared__ int lds[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
@@ -146,7 +150,8 @@ __global__ void __launch_bounds__(256) k_traverse(WfParams P) {
     int s = 0;
     DV o = dv(0, 0, 0), d = dv(0, 0, 0);
     double tmax64 = 0.0, best_t = 0.0;
-    float ix = 0.f, iy = 0.f, iz = 0.f, oix = 0.f, oiy = 0.f, oiz = 0.f, tlim = 0.f;
+    RayF rf{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    float tlim = 0.f;
     int node = 0, sp = 0, best_slot = -1, best_first = -1;
     bool found = false;
     int win_next = 0, win_end = 0;   // slot window being scanned (wave-uniform)
@@ -213,13 +218,7 @@ __global__ void __launch_bounds__(256) k_traverse(WfParams P) {
                     if (P.depth[s] != P.max_depth) c_ext++;
                 }
                 c_rays++;
-                float fx = (float)d.x, fy = (float)d.y, fz = (float)d.z;
-                const float tiny = 1e-20f;
-                if (fabsf(fx) < tiny) fx = copysignf(tiny, fx);
-                if (fabsf(fy) < tiny) fy = copysignf(tiny, fy);
-                if (fabsf(fz) < tiny) fz = copysignf(tiny, fz);
-                ix = 1.0f / fx; iy = 1.0f / fy; iz = 1.0f / fz;
-                oix = (float)o.x * ix; oiy = (float)o.y * iy; oiz = (float)o.z * iz;
+                rf = make_rayf(o, d);
                 tlim = f_round_up(tmax64);
                 best_t = tmax64;
                 best_slot = -1;
@@ -234,41 +233,18 @@ __global__ void __launch_bounds__(256) k_traverse(WfParams P) {
         }
         if (!__any(active)) break;  // every chunk taken and every pending slot traced
         if (active) {
-            bool done = false;
             // ---- internal nodes until this lane reaches a leaf (while-while) ----
             while (node >= 0) {
-                const MfxNode nd = S.nodes[node];
                 if (STATS) st.nodes++;
-                float a0 = fmaf(nd.c0lox, ix, -oix), a1 = fmaf(nd.c0hix, ix, -oix);
-                float b0 = fmaf(nd.c0loy, iy, -oiy), b1 = fmaf(nd.c0hiy, iy, -oiy);
-                float c0 = fmaf(nd.c0loz, iz, -oiz), c1 = fmaf(nd.c0hiz, iz, -oiz);
-                const float n0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-                const float f0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-                a0 = fmaf(nd.c1lox, ix, -oix); a1 = fmaf(nd.c1hix, ix, -oix);
-                b0 = fmaf(nd.c1loy, iy, -oiy); b1 = fmaf(nd.c1hiy, iy, -oiy);
-                c0 = fmaf(nd.c1loz, iz, -oiz); c1 = fmaf(nd.c1hiz, iz, -oiz);
-                const float n1 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-                const float f1 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-                const bool h0 = n0 <= f0, h1 = n1 <= f1;
-                if (h0 && h1) {
-                    int near = nd.child0, far = nd.child1;
-                    if (n1 < n0) { near = nd.child1; far = nd.child0; }
-                    stack[(sp++) * 64] = far;
-                    node = near;
-                } else if (h0) {
-                    node = nd.child0;
-                } else if (h1) {
-                    node = nd.child1;
-                } else {
-                    if (sp == 0) { done = true; break; }
-                    node = stack[(--sp) * 64];
-                }
+                node = node_step(S.nodes, node, rf, tlim, stack, sp);
             }
+            bool done = node == MFX_TRAV_EXIT;
             // ---- one reference leaf (exact FP64) ----
             if (!done) {
                 double t;
                 int sl, f;
-                if (cluster_hit<STATS>(S, ~node, o, d, 1e-6, tmax64, t, sl, f, st)) {
+                if (cluster_hit<SHADOW, STATS>(S, ~node, o, d, 1e-6, tmax64, found ? best_t : __builtin_inf(), t, sl,
+                                               f, st)) {
                     if (SHADOW) {
                         found = true;
                         done = true;
