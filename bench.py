@@ -159,7 +159,8 @@ def main():
     else:
         rays_all = rays
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
-                for k in ("total_ms", "logic_ms", "extend_ms", "shade_ms", "shadow_ms", "iterations")}
+                for k in ("total_ms", "logic_ms", "extend_ms", "shade_ms", "shadow_ms", "iterations", "launches",
+                          "subpools")}
 
     result = None
     if rank == 0:
@@ -204,7 +205,7 @@ def main():
                     bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
             else:
                 kname, kms, krays = "k_traverse<false, false>", stage_ms["extend_ms"], closest_rays / args.steps
-                launches = stage_ms["iterations"]
+                launches = stage_ms["launches"]
                 bray = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
             # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
             achieved = krays * bray / (kms / 1e3) / 1e9

@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mafrix_rt.h"
@@ -41,6 +42,8 @@ hipError_t upload(T** dptr, const std::vector<T>& v) {
 }
 }  // namespace
 
+#define MFX_MAX_SUB 4
+
 struct mfx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -68,16 +71,21 @@ struct mfx_ctx {
     int64_t npix = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
-    // wavefront pipeline
+    // wavefront pipeline: the slot pool is split into nsub sub-pools, each driven on its own
+    // stream so one sub-pool's traversal tail overlaps another's logic / shade kernels
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
-    int64_t wf_pool_max = 1 << 24;
-    unsigned long long* d_wfctl = nullptr;
-    void* h_pin = nullptr;
-    hipEvent_t wf_ev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    int64_t wf_pool_max = 1 << 25;
+    int nsub = 1;
+    unsigned long long* d_wfctl = nullptr;  // [MFX_MAX_SUB][WF_NCTL]
+    unsigned long long* h_pin = nullptr;    // [MFX_MAX_SUB][WF_SHARDS] path counters read back
+    hipStream_t sub_stream[MFX_MAX_SUB] = {};
+    hipEvent_t sub_ev[MFX_MAX_SUB][4] = {};  // iteration start, extend|shadow boundary, end, counters copied
+    hipEvent_t fork_ev = nullptr;
     double stage_ms[4] = {0, 0, 0, 0};
-    int iterations = 0;
+    int iterations = 0;  // iterations of the longest sub-pool
+    int launches = 0;    // launches per stage kernel, all sub-pools
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
 };
@@ -90,8 +98,12 @@ static void free_ctx(mfx_ctx* c) {
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     if (c->h_pin) (void)hipHostFree(c->h_pin);
-    for (hipEvent_t e : c->wf_ev)
-        if (e) (void)hipEventDestroy(e);
+    for (auto& evs : c->sub_ev)
+        for (hipEvent_t e : evs)
+            if (e) (void)hipEventDestroy(e);
+    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
+    for (hipStream_t st : c->sub_stream)
+        if (st) (void)hipStreamDestroy(st);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -161,10 +173,15 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
     CK(hipMalloc((void**)&c->d_counters, 16 * WF_SHARDS * sizeof(unsigned long long)));
-    CK(hipMalloc((void**)&c->d_wfctl, WF_NCTL * sizeof(unsigned long long)));
-    CK(hipHostMalloc(&c->h_pin, 64, hipHostMallocDefault));
-    for (hipEvent_t& e : c->wf_ev) CK(hipEventCreate(&e));
-    if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(256, atoll(pm));
+    CK(hipMalloc((void**)&c->d_wfctl, MFX_MAX_SUB * WF_NCTL * sizeof(unsigned long long)));
+    CK(hipHostMalloc((void**)&c->h_pin, MFX_MAX_SUB * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
+    if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
+    if (const char* ns = getenv("MFX_SUBPOOLS")) c->nsub = std::max(1, std::min(MFX_MAX_SUB, atoi(ns)));
+    CK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
+    for (int k = 0; k < c->nsub; ++k) {
+        CK(hipStreamCreateWithFlags(&c->sub_stream[k], hipStreamNonBlocking));
+        for (hipEvent_t& e : c->sub_ev[k]) CK(hipEventCreate(&e));
+    }
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
     CK(hipMemset(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long)));
@@ -199,15 +216,13 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
     double** dbl[WF_DOUBLES_PER_SLOT - 1] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz,
-                                             &c->wf.tx, &c->wf.ty, &c->wf.tz, &c->wf.lx, &c->wf.ly, &c->wf.lz,
-                                             &c->wf.sdx, &c->wf.sdy, &c->wf.sdz, &c->wf.stmax, &c->wf.scx,
-                                             &c->wf.scy, &c->wf.scz, &c->wf.hit_t};
+                                             &c->wf.tx, &c->wf.ty, &c->wf.tz, &c->wf.lx, &c->wf.ly, &c->wf.lz};
     for (double** d : dbl) *d = (double*)take(P * 8);
     c->wf.key = (uint64_t*)take(P * 8);
-    c->wf.hit_slot = (int32_t*)take(P * 4);
     c->wf.rn = (uint32_t*)take(P * 4);
     c->wf.depth = (int32_t*)take(P * 4);
     c->wf.pixel = (int32_t*)take(P * 4);
+    c->wf.hit_slot = (int32_t*)take(P * 4);
     c->wf.state = (int32_t*)take(P * 4);
     c->wf_pool = pool;
     return MFX_OK;
@@ -223,70 +238,118 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.accum = c->d_accum;
 }
 
-// The wavefront pipeline: logic -> extend -> shade -> shadow per iteration. Once every path
-// index of the call has been handed out (the host reads the 8 shard counters after each
-// iteration), max_depth more iterations finish the last paths and a final logic pass retires them.
+// The wavefront pipeline: logic -> extend -> shade -> shadow per iteration, per sub-pool. Each
+// sub-pool owns a contiguous range of path indices, its control words and a stream; the host
+// feeds whichever sub-pool finished its last iteration (polling events), so the GPU always has
+// another sub-pool's kernels to run during a traversal kernel's tail. Once every path index of a
+// sub-pool has been handed out (its 8 shard counters, read back after each iteration),
+// max_depth more iterations finish and retire its last paths.
 static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
-    const int64_t pool64 = std::min<int64_t>(total, c->wf_pool_max);
-    const int32_t pool = (int32_t)((pool64 + 2047) / 2048 * 2048);
-    int rc = wf_ensure_pool(c, pool);
+    const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(c->nsub, total / 65536 + 1));
+    const int64_t sub_max = std::min<int64_t>((total + nsub - 1) / nsub, c->wf_pool_max / c->nsub);
+    const int32_t sub_pool = (int32_t)((sub_max + 2047) / 2048 * 2048);
+    int rc = wf_ensure_pool(c, sub_pool * nsub);
     if (rc) return rc;
-    WfParams P = c->wf;
-    fill_scene_params(c, P);
-    P.ctl = c->d_wfctl;
-    P.counters = c->d_counters;
-    P.total = total;
-    P.seed = c->seed;
-    P.sample_base = sample_base;
-    P.part_index = c->part_index;
-    P.part_count = c->part_count;
-    P.pool = pool;
-    P.width = W;
-    P.height = H;
-    P.max_depth = c->host.max_depth;
-    P.root_is_leaf = c->host.root_is_leaf;
-    P.stack_size = c->stack_size;
-    P.chunk = 256;
-    HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)pool, c->stream));
-    HIPCHECK(hipMemsetAsync(c->d_wfctl, 0, WF_NCTL * sizeof(unsigned long long), c->stream));
+    WfParams base = c->wf;
+    fill_scene_params(c, base);
+    base.counters = c->d_counters;
+    base.seed = c->seed;
+    base.sample_base = sample_base;
+    base.part_index = c->part_index;
+    base.part_count = c->part_count;
+    base.width = W;
+    base.height = H;
+    base.max_depth = c->host.max_depth;
+    base.root_is_leaf = c->host.root_is_leaf;
+    base.stack_size = c->stack_size;
+    base.chunk = 256;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
-    double stage_ms[4] = {0, 0, 0, 0};
-    int iters = 0, drain = -1;
+    struct Sub {
+        WfParams P;
+        hipStream_t st;
+        hipEvent_t* ev;
+        unsigned long long* pin;
+        int drain, iters;
+        bool done;
+    };
+    Sub sub[MFX_MAX_SUB];
     HIPCHECK(hipEventRecord(c->ev0, c->stream));
-    for (;;) {
-        HIPCHECK(hipEventRecord(c->wf_ev[0], c->stream));
-        HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, c->wf_ev + 1));
-        HIPCHECK(hipEventRecord(c->wf_ev[4], c->stream));
-        ++iters;
-        if (drain < 0) {
-            HIPCHECK(hipMemcpyAsync(c->h_pin, c->d_wfctl + WF_CTL_PATH, WF_SHARDS * 8, hipMemcpyDeviceToHost,
-                                    c->stream));
-            HIPCHECK(hipStreamSynchronize(c->stream));
-            bool all = true;
-            const unsigned long long* ctr = (const unsigned long long*)c->h_pin;
-            for (int g = 0; g < WF_SHARDS; ++g)
-                if ((int64_t)ctr[g] < total * (g + 1) / WF_SHARDS - total * g / WF_SHARDS) all = false;
-            if (all) drain = P.max_depth;  // no path starts after this iteration
-        } else {
-            HIPCHECK(hipStreamSynchronize(c->stream));
-            --drain;
-        }
-        for (int k = 0; k < 4; ++k) {
-            float f = 0.f;
-            HIPCHECK(hipEventElapsedTime(&f, c->wf_ev[k], c->wf_ev[k + 1]));
-            stage_ms[k] += f;
-        }
-        if (drain == 0) break;
-        if (iters > 10000000) return fail(MFX_E_STATE, "wavefront pipeline did not drain");
+    HIPCHECK(hipEventRecord(c->fork_ev, c->stream));
+    for (int k = 0; k < nsub; ++k) {
+        Sub& u = sub[k];
+        u.P = mfx_wf_slice(base, k * sub_pool, sub_pool);
+        u.P.ctl = c->d_wfctl + k * WF_NCTL;
+        u.P.path_base = total * k / nsub;
+        u.P.total = total * (k + 1) / nsub - u.P.path_base;
+        u.st = c->sub_stream[k];
+        u.ev = c->sub_ev[k];
+        u.pin = c->h_pin + k * WF_SHARDS;
+        u.drain = -1;
+        u.iters = 0;
+        u.done = false;
+        HIPCHECK(hipStreamWaitEvent(u.st, c->fork_ev, 0));
+        HIPCHECK(hipMemsetAsync(u.P.state, 0, sizeof(int32_t) * (size_t)sub_pool, u.st));
+        HIPCHECK(hipMemsetAsync(u.P.ctl, 0, WF_NCTL * sizeof(unsigned long long), u.st));
     }
-    HIPCHECK(mfx_wf_finish(P, c->stream));  // retire the last finished paths
+    auto enqueue = [&](Sub& u) -> int {
+        HIPCHECK(hipEventRecord(u.ev[0], u.st));
+        HIPCHECK(mfx_wf_iteration(u.P, c->wf_ext_grid, c->wf_shd_grid, stats, u.st, u.ev + 1));
+        HIPCHECK(hipEventRecord(u.ev[2], u.st));
+        if (u.drain < 0)
+            HIPCHECK(hipMemcpyAsync(u.pin, u.P.ctl + WF_CTL_PATH, WF_SHARDS * sizeof(unsigned long long),
+                                    hipMemcpyDeviceToHost, u.st));
+        HIPCHECK(hipEventRecord(u.ev[3], u.st));
+        ++u.iters;
+        return MFX_OK;
+    };
+    double stage_ms[4] = {0, 0, 0, 0};
+    int iters = 0;
+    for (int k = 0; k < nsub; ++k)
+        if ((rc = enqueue(sub[k]))) return rc;
+    int live = nsub;
+    while (live > 0) {
+        bool progressed = false;
+        for (int k = 0; k < nsub; ++k) {
+            Sub& u = sub[k];
+            if (u.done) continue;
+            const hipError_t q = hipEventQuery(u.ev[3]);
+            if (q == hipErrorNotReady) continue;
+            HIPCHECK(q);
+            progressed = true;
+            for (int s = 0; s < 2; ++s) {
+                float f = 0.f;
+                HIPCHECK(hipEventElapsedTime(&f, u.ev[s], u.ev[s + 1]));
+                stage_ms[1 + 2 * s] += f;  // [1] extend, [3] shade + shadow
+            }
+            if (u.drain < 0) {
+                bool all = true;
+                for (int g = 0; g < WF_SHARDS; ++g)
+                    if ((int64_t)u.pin[g] < u.P.total * (g + 1) / WF_SHARDS - u.P.total * g / WF_SHARDS) all = false;
+                if (all) u.drain = u.P.max_depth;  // no path of this sub-pool starts after this iteration
+            } else {
+                --u.drain;
+            }
+            if (u.drain == 0) {  // every path of this sub-pool has been retired
+                HIPCHECK(hipStreamWaitEvent(c->stream, u.ev[3], 0));
+                u.done = true;
+                --live;
+                iters = std::max(iters, u.iters);
+                continue;
+            }
+            if (u.iters > 10000000) return fail(MFX_E_STATE, "wavefront pipeline did not drain");
+            if ((rc = enqueue(u))) return rc;
+        }
+        if (!progressed) std::this_thread::yield();
+    }
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
     for (int k = 0; k < 4; ++k) c->stage_ms[k] = stage_ms[k];
     c->iterations = iters;
+    c->launches = 0;
+    for (int k = 0; k < nsub; ++k) c->launches += sub[k].iters;
     return MFX_OK;
 }
 
@@ -339,9 +402,12 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
     if (c->mega_last) {
         out[2] = total;
         out[5] = 1;
+        out[6] = 1;
     } else {
         for (int k = 0; k < 4; ++k) out[1 + k] = c->stage_ms[k];
         out[5] = c->iterations;
+        out[6] = c->launches;
+        out[7] = c->nsub;
     }
     return MFX_OK;
 }

@@ -1,11 +1,13 @@
 // mfx_wavefront.h — path-slot pool (SoA in HBM) of the wavefront pipeline.
 //
-// Each slot carries one path through a small state machine; every stage scans the pool and
-// handles the slots in its state, so no ray queue (and no hot queue-tail atomic) exists:
-//   FREE -> (logic) NEED_EXT -> (extend) EXT_DONE -> (shade) SHADOW_CONT | SHADOW_END | DONE
-//   SHADOW_CONT -> (shadow) NEED_EXT,  SHADOW_END -> (shadow) DONE,  DONE -> (logic) FREE
-// The only atomics are per-wave chunk fetches and per-block path allocations, spread over
-// WF_SHARDS counters (a returning atomic on one word saturates near 88 per microsecond).
+// Each slot carries one path through a three-state machine; each kernel scans the pool for the
+// slots in its state, so no ray queue (and no hot queue-tail atomic) exists:
+//   FREE -(extend: new camera ray)-> ...
+//   FREE | NEED_EXT -(k_extend: closest hit)-> EXT_DONE
+//   EXT_DONE -(k_shadow: shade + shadow ray)-> NEED_EXT, or FREE once the path is retired
+// The only atomics are per-wave chunk fetches and path allocations, spread over WF_SHARDS
+// counters (a returning atomic on one word saturates near 88 per microsecond), and the FP64
+// adds of finished paths into the pixel accumulator.
 #ifndef MFX_WAVEFRONT_H
 #define MFX_WAVEFRONT_H
 
@@ -17,15 +19,12 @@
 #define WF_FREE 0
 #define WF_NEED_EXT 1
 #define WF_EXT_DONE 2
-#define WF_SHADOW_CONT 3
-#define WF_SHADOW_END 4
-#define WF_DONE 5
 
 #define WF_SHARDS 8
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_PATH 0                 // [WF_SHARDS] path counters, shard g owns [g*T/8, (g+1)*T/8)
-#define WF_CTL_EXT (WF_SHARDS)        // [WF_SHARDS] extend-kernel slot-chunk heads
-#define WF_CTL_SHD (2 * WF_SHARDS)    // [WF_SHARDS] shadow-kernel slot-chunk heads
+#define WF_CTL_EXT (WF_SHARDS)        // [WF_SHARDS] k_extend slot-chunk heads
+#define WF_CTL_SHD (2 * WF_SHARDS)    // [WF_SHARDS] k_shadow slot-chunk heads
 #define WF_NCTL (3 * WF_SHARDS)
 
 struct WfParams {
@@ -38,22 +37,21 @@ struct WfParams {
     const MfxCamera* cam;
     double* accum;  // [3][w*h]
     // path slots (SoA)
-    double *ox, *oy, *oz, *dx, *dy, *dz;  // current ray; origin = last hit point after shading
-    double *tx, *ty, *tz;                 // throughput
-    double *lx, *ly, *lz;                 // radiance
-    double *sdx, *sdy, *sdz, *stmax;      // shadow ray direction, tmax = dist - 1e-6
-    double *scx, *scy, *scz;              // this vertex's direct term if unoccluded
-    double* hit_t;                        // closest hit t, -1 = miss
-    int32_t* hit_slot;
-    uint64_t* key;
-    uint32_t* rn;
-    int32_t* depth;
-    int32_t* pixel;
+    double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
+    double *dx, *dy, *dz;  // ray direction
+    double *tx, *ty, *tz;  // throughput
+    double *lx, *ly, *lz;  // radiance
+    uint64_t* key;         // RNG key of the path
+    uint32_t* rn;          // RNG draws used so far
+    int32_t* depth;        // remaining depth (PathIntegrator's d)
+    int32_t* pixel;        // x-major pixel index
+    int32_t* hit_slot;     // shade[] slot of the closest hit, -1 = miss
     int32_t* state;
     // control
     unsigned long long* ctl;              // [WF_NCTL]
-    unsigned long long* counters;         // [16] ray / traversal counters
-    int64_t total;                        // path indices this call (incl. padding of edge tiles)
+    unsigned long long* counters;         // [WF_SHARDS][16] ray / traversal counters
+    int64_t total;                        // path indices of this sub-pool (incl. padding of edge tiles)
+    int64_t path_base;                    // first path index of this sub-pool
     uint64_t seed;
     int64_t sample_base;
     int32_t part_index, part_count;
@@ -61,17 +59,19 @@ struct WfParams {
     int32_t width, height, max_depth;
     int32_t root_is_leaf;
     int32_t stack_size;
-    int32_t chunk;                        // slots per chunk fetch of the traversal kernels
+    int32_t chunk;                        // slots per chunk fetch of the kernels
 };
 
-// doubles and 4-byte words per slot in the SoA pool
-#define WF_DOUBLES_PER_SLOT 21
-#define WF_WORDS_PER_SLOT 7  // key (2), rn, depth, pixel, state, hit_slot
+// 8-byte and 4-byte words per slot in the SoA pool
+#define WF_DOUBLES_PER_SLOT 13  // o, d, throughput, radiance (12) + key
+#define WF_WORDS_PER_SLOT 5     // rn, depth, pixel, hit_slot, state
+
+// P with every SoA slot array advanced by `first` slots (a sub-pool of `n` slots)
+WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n);
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu);
-// one iteration (logic, extend, shade, shadow); ev[0..2] are recorded after logic, extend, shade
+// one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);
-hipError_t mfx_wf_finish(const WfParams& P, hipStream_t st);
 
 #endif

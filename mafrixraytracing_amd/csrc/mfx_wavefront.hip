@@ -1,19 +1,24 @@
 // mfx_wavefront.hip — wavefront path tracing on gfx950: the integrator loop
-// (Integrators.fs:107-137, 161-172) split into four kernels over a pool of path slots:
+// (Integrators.fs:107-137, 161-172) as two persistent kernels per iteration over a pool of
+// path slots:
 //
-//   k_logic    DONE slots -> FP64 atomic add of L into the pixel sums; FREE slots take new path
-//              indices (block-aggregated allocation from 8 sharded counters) and generate camera
-//              rays (PixelIntegrator.Sample + PinholeCamera.GetRay)
-//   k_traverse<closest>  persistent bvh.Hit(ray, 1e-6, 1e8) over NEED_EXT slots
-//   k_shade    LambertianBrdf.SampleF (rejection hemisphere), NewAreaLight.Sample_Li, throughput,
-//              the shadow ray of the vertex and the continuing ray
-//   k_traverse<shadow>   persistent any-hit over SHADOW_* slots; unoccluded -> L += direct term
+//   k_extend   bvh.Hit(ray, 1e-6, 99999999.) (Integrators.fs:108) for NEED_EXT slots; FREE slots
+//              first take a new path index (PixelIntegrator.Sample + PinholeCamera.GetRay,
+//              Integrators.fs:161-169, Camera.fs:134-139). Writes the hit point and hit slot.
+//   k_shadow   one vertex of PathIntegrator.TraceRay for EXT_DONE slots: LambertianBrdf.SampleF,
+//              NewAreaLight.Sample_Li and the throughput update (Integrators.fs:110-136), then
+//              the vertex's shadow ray (Integrators.fs:44) traced by the same lane; unoccluded ->
+//              L += direct term. Finished paths (miss, or depth exhausted) are retired here: an
+//              FP64 atomic add of L into the pixel sums, and the slot is FREE again.
 //
-// The traversal kernels keep lanes busy: a lane that finishes its ray takes the next pending
-// slot at the next step (persistent while-while with dynamic fetch, Aila & Laine 2009). Pending
-// slots are found by scanning 64-slot windows: wave ballot of the state test + popcount ranks
-// (the active-ray compaction), parked in a 64-entry LDS list per wave. Path state lives in HBM
-// as SoA FP64; every arithmetic step is the same FP64 expression as the megakernel / oracle.
+// Both kernels keep lanes busy: a lane that finishes its ray takes the next pending ray at the
+// next step (persistent while-while with dynamic fetch, Aila & Laine 2009). Pending rays come
+// from scanning 64-slot windows with the whole wave: lane j handles slot win+j (coalesced SoA
+// loads), does that slot's non-traversal work with all 64 lanes — the camera ray of a new path,
+// or the shading of a hit — and the rays to trace are compacted (ballot + popcount ranks) into a
+// 64-entry LDS list per wave, with their origin / direction / tmax / direct term, so a ray never
+// round-trips through HBM between its generation and its traversal. Path state lives in HBM as
+// SoA FP64; every arithmetic step is the same FP64 expression as the megakernel and the oracle.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -27,6 +32,12 @@
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ uint64_t lanes_below() { return (1ULL << lane_id()) - 1ULL; }
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
 
 // per-block reduction of a per-lane counter, one atomic per block (the counters are sharded too)
 template <int NW>
@@ -43,364 +54,460 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, uint32_t v, u
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_logic: retire finished paths, start new ones (1024 threads per block)
+// Slot windows: a wave takes chunks of P.chunk slots (its block's shard first, then the others)
+// and scans them 64 at a time.
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(1024) k_logic(WfParams P) {
-    __shared__ uint32_t wcnt[16];
-    __shared__ unsigned long long blk_base;
-    __shared__ uint32_t blk_got;
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    const int wave = threadIdx.x >> 6;
-    const bool in = s < P.pool;
-    int st = in ? P.state[s] : WF_NEED_EXT;
-    if (st == WF_DONE) {
-        const int64_t pix = P.pixel[s];
-        const int64_t npix = (int64_t)P.width * P.height;
-        const double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
-        if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
-        if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
-        if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
-        st = WF_FREE;
-    }
-    const bool need = in && st == WF_FREE;
-    const uint64_t m = __ballot(need);
-    if (lane_id() == 0) wcnt[wave] = (uint32_t)__popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint32_t want = 0;
-        for (int w = 0; w < 16; ++w) want += wcnt[w];
-        unsigned long long base = 0;
-        uint32_t got = 0;
-        if (want) {
-            // block-aggregated allocation from the path-index shards (shard g owns [g*T/8, (g+1)*T/8))
-            for (int k = 0; k < WF_SHARDS && got == 0; ++k) {
-                const int g = (blockIdx.x + k) & (WF_SHARDS - 1);
-                const int64_t lo = P.total * g / WF_SHARDS, hi = P.total * (g + 1) / WF_SHARDS;
-                const unsigned long long c = atomicAdd(P.ctl + WF_CTL_PATH + g, (unsigned long long)want);
-                if ((int64_t)c < hi - lo) {
-                    base = (unsigned long long)lo + c;
-                    got = (uint32_t)min((int64_t)want, hi - lo - (int64_t)c);
-                }
+struct Scanner {
+    int win_next, win_end, shard_try;
+    bool exhausted;
+    // Make [win_next, win_end) non-empty; false once every chunk has been taken.
+    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size) {
+        if (win_next < win_end) return true;
+        while (shard_try < WF_SHARDS) {
+            const int g = (blockIdx.x + shard_try) & (WF_SHARDS - 1);
+            unsigned long long c = 0;
+            if (lane_id() == 0) c = atomicAdd(heads + g, (unsigned long long)chunk);
+            c = __shfl(c, 0);
+            if ((int64_t)c < shard_size) {
+                win_next = g * shard_size + (int)c;
+                win_end = g * shard_size + min((int)c + chunk, shard_size);
+                return true;
             }
+            ++shard_try;
         }
-        blk_base = base;
-        blk_got = got;
+        exhausted = true;
+        return false;
     }
-    __syncthreads();
-    uint32_t off = 0;
-    for (int w = 0; w < wave; ++w) off += wcnt[w];
-    const uint32_t idx = off + (uint32_t)__popcll(m & lanes_below());
-    bool started = false;
-    if (need && idx < blk_got) {
-        const int64_t p = (int64_t)blk_base + idx;
-        // path index -> (sample, 8x8 tile, pixel): sample-major, tile-coherent
-        const int W = P.width, H = P.height;
-        const int tiles_x = (W + 7) >> 3;
-        const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
-        const int64_t smp = p / per_sample;
-        const int64_t q = p - smp * per_sample;
-        const int64_t tile = q >> 6;
-        const int within = (int)(q & 63);
-        const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-        const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
-        if (x < W && y < H) {
-            const MfxCamera& CAM = *P.cam;
-            const int64_t pixel = (int64_t)x * H + y;  // Color[w,h] x-major
-            const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
-            const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
-            uint32_t rn = 0;
-            // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
-            const double u = ((double)x + rng_next(key, rn)) / (double)W;
-            const double v = ((double)y + rng_next(key, rn)) / (double)H;
-            const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
-            const DV o = ld3(CAM.position);
-            const DV d = vnormalize(vsub(target, o));
-            P.ox[s] = o.x; P.oy[s] = o.y; P.oz[s] = o.z;
-            P.dx[s] = d.x; P.dy[s] = d.y; P.dz[s] = d.z;
-            P.tx[s] = 1.0; P.ty[s] = 1.0; P.tz[s] = 1.0;
-            P.lx[s] = 0.0; P.ly[s] = 0.0; P.lz[s] = 0.0;
-            P.key[s] = key;
-            P.rn[s] = rn;
-            P.depth[s] = P.max_depth;
-            P.pixel[s] = (int32_t)pixel;
-            st = WF_NEED_EXT;
-            started = true;
+};
+
+// Per-wave LDS list of pending rays: slot index, a flag word, and up to 7 doubles per entry,
+// each field a 64-entry column (conflict-free).
+#define WF_PEND_DOUBLES 7
+#define WF_PEND_BYTES (64 * (8 + 8 * WF_PEND_DOUBLES))
+struct Pend {
+    int* slot;
+    int* flag;
+    double* v;  // v[f * 64 + entry]
+    __device__ __forceinline__ Pend(uint8_t* base) {
+        slot = (int*)base;
+        flag = slot + 64;
+        v = (double*)(base + 512);
+    }
+};
+
+// Traversal state of one lane (one ray) across outer-loop iterations
+struct Trav {
+    DV o, d;
+    double tmax64, best_t;
+    RayF rf;
+    float tlim;
+    int node, sp, best_slot, best_first;
+    bool found;
+};
+
+__device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
+    T.o = o;
+    T.d = d;
+    T.tmax64 = tmax;
+    T.rf = make_rayf(o, d);
+    T.tlim = f_round_up(tmax);
+    T.best_t = tmax;
+    T.best_slot = -1;
+    T.best_first = -1;
+    T.found = false;
+    T.sp = 0;
+    T.node = S.root_is_leaf ? ~0 : 0;
+}
+
+// Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
+// exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
+// stack empty).
+template <bool SHADOW, bool STATS>
+__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __restrict__ stack, Stats& st) {
+    while (T.node >= 0) {
+        if (STATS) st.nodes++;
+        T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
+    }
+    if (T.node == MFX_TRAV_EXIT) return true;
+    double t;
+    int sl, f;
+    if (cluster_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.found ? T.best_t : __builtin_inf(), t,
+                                   sl, f, st)) {
+        if (SHADOW) {
+            T.found = true;
+            return true;
+        }
+        if (!T.found || t < T.best_t || (t == T.best_t && f > T.best_first)) {
+            T.found = true;
+            T.best_t = t;
+            T.best_slot = sl;
+            T.best_first = f;
+            T.tlim = f_round_up(t);
         }
     }
-    if (in) P.state[s] = st;
-    block_add<16>(P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1)) + 0, started ? 1u : 0u, wcnt);
+    if (T.sp == 0) return true;
+    T.node = stack[(--T.sp) * 64];
+    return false;
+}
+
+// Retire a finished path: FP64 atomic add of its radiance into the pixel sums (the
+// PixelIntegrator's `color <- color + ...`, Integrators.fs:169); the slot becomes FREE.
+__device__ __forceinline__ void retire(const WfParams& P, int s, double lx, double ly, double lz) {
+    const int64_t pix = P.pixel[s];
+    const int64_t npix = (int64_t)P.width * P.height;
+    if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
+    if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
+    if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
+    P.state[s] = WF_FREE;
 }
 
 // ------------------------------------------------------------------------------------------------
-// Persistent traversal (closest hit or shadow) with per-lane dynamic fetch
+// k_extend: closest hit for NEED_EXT slots; FREE slots start new paths
 // ------------------------------------------------------------------------------------------------
-template <bool SHADOW, bool STATS>
-__global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_traverse(WfParams P) {
+template <bool STATS>
+__global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    int* pend = lds + 4 * P.stack_size * 64 + wave * 64;  // this wave's list of pending slots
-    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_size * 64 + 4 * 64);
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
+    const Pend pd(pend_base + wave * WF_PEND_BYTES);
+    uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
     const SceneView S{P.nodes, P.blob, P.root_is_leaf};
     const int shard_size = P.pool / WF_SHARDS;
-    unsigned long long* heads = P.ctl + (SHADOW ? WF_CTL_SHD : WF_CTL_EXT);
+    const int W = P.width, H = P.height;
+    const int tiles_x = (W + 7) >> 3;
+    const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
 
+    Scanner sc{0, 0, 0, false};
+    bool paths_left = true;  // wave-uniform: path indices remain in some shard
+    int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
-    DV o = dv(0, 0, 0), d = dv(0, 0, 0);
-    double tmax64 = 0.0, best_t = 0.0;
-    RayF rf{0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    float tlim = 0.f;
-    int node = 0, sp = 0, best_slot = -1, best_first = -1;
-    bool found = false;
-    int win_next = 0, win_end = 0;   // slot window being scanned (wave-uniform)
-    int pend_lo = 0, pend_hi = 0;    // pending list [pend_lo, pend_hi) in LDS (wave-uniform)
-    int shard_try = 0;
-    bool exhausted = false;
-    uint32_t c_rays = 0, c_ext = 0;
+    Trav T{};
+    uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
 
     while (true) {
-        // ---- dynamic fetch: idle lanes take pending slots by rank ----
+        // ---- dynamic fetch: idle lanes take pending rays by rank ----
         bool idle = !active;
         uint64_t m = __ballot(idle);
-        while (m != 0 && !exhausted) {
+        while (m != 0 && !sc.exhausted) {
             if (pend_lo == pend_hi) {
-                if (win_next >= win_end) {
-                    // next chunk of slots from this block's shard, then the others
-                    int base = -1, g = 0;
-                    while (shard_try < WF_SHARDS) {
-                        g = (blockIdx.x + shard_try) & (WF_SHARDS - 1);
-                        unsigned long long c = 0;
-                        if (lane == 0) c = atomicAdd(heads + g, (unsigned long long)P.chunk);
-                        c = __shfl(c, 0);
-                        if ((int64_t)c < shard_size) {
-                            base = (int)c;
-                            break;
+                if (!sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size)) break;
+                // scan a 64-slot window with the whole wave; its FREE slots share one allocation
+                const int j = sc.win_next + lane;
+                const int sj = j < sc.win_end ? P.state[j] : -1;
+                const bool fr = paths_left && sj == WF_FREE;
+                const uint64_t fm = __ballot(fr);
+                const int nf = __popcll(fm);
+                int got = 0;
+                int64_t pbase = 0;
+                if (nf) {
+                    if (lane == 0) {
+                        // path shard g owns [g*T/8, (g+1)*T/8) of this sub-pool's path indices
+                        for (int k = 0; k < WF_SHARDS && got == 0; ++k) {
+                            const int g = (blockIdx.x * 4 + wave + k) & (WF_SHARDS - 1);
+                            const int64_t lo = P.total * g / WF_SHARDS, hi = P.total * (g + 1) / WF_SHARDS;
+                            const unsigned long long c = atomicAdd(P.ctl + WF_CTL_PATH + g, (unsigned long long)nf);
+                            if ((int64_t)c < hi - lo) {
+                                pbase = lo + (int64_t)c;
+                                got = (int)min((int64_t)nf, hi - lo - (int64_t)c);
+                            }
                         }
-                        ++shard_try;
                     }
-                    if (base < 0) {
-                        exhausted = true;
-                        break;
-                    }
-                    win_next = g * shard_size + base;
-                    win_end = g * shard_size + min(base + P.chunk, shard_size);
+                    got = __shfl(got, 0);
+                    pbase = __shfl(pbase, 0);
+                    if (got == 0) paths_left = false;
                 }
-                // scan a 64-slot window: ballot + rank = compacted pending list
-                const int j = win_next + lane;
-                const int sj = j < win_end ? P.state[j] : WF_FREE;
-                const bool cand = SHADOW ? (sj == WF_SHADOW_CONT || sj == WF_SHADOW_END) : (sj == WF_NEED_EXT);
-                const uint64_t cm = __ballot(cand);
-                if (cand) pend[__popcll(cm & lanes_below())] = j;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                bool take = false;
+                DV o = dv(0, 0, 0), d = dv(0, 0, 0);
+                if (sj == WF_NEED_EXT) {
+                    o = dv(P.ox[j], P.oy[j], P.oz[j]);
+                    d = dv(P.dx[j], P.dy[j], P.dz[j]);
+                    take = true;
+                    c_ext++;
+                } else if (fr && __popcll(fm & lanes_below()) < got) {
+                    // new path: index -> (sample, 8x8 tile, pixel), sample-major, tile-coherent
+                    const int64_t p = P.path_base + pbase + __popcll(fm & lanes_below());
+                    const int64_t smp = p / per_sample;
+                    const int64_t q = p - smp * per_sample;
+                    const int64_t tile = q >> 6;
+                    const int within = (int)(q & 63);
+                    const int x = (int)(tile % tiles_x) * 8 + (within & 7);
+                    const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
+                    if (x < W && y < H) {  // edge-tile padding indices start no path
+                        const MfxCamera& CAM = *P.cam;
+                        const int64_t pixel = (int64_t)x * H + y;  // Color[w,h] x-major
+                        const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
+                        const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
+                        uint32_t rn = 0;
+                        // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
+                        const double u = ((double)x + rng_next(key, rn)) / (double)W;
+                        const double v = ((double)y + rng_next(key, rn)) / (double)H;
+                        const DV target =
+                            vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
+                        o = ld3(CAM.position);
+                        d = vnormalize(vsub(target, o));
+                        P.tx[j] = 1.0; P.ty[j] = 1.0; P.tz[j] = 1.0;
+                        P.lx[j] = 0.0; P.ly[j] = 0.0; P.lz[j] = 0.0;
+                        P.key[j] = key;
+                        P.rn[j] = rn;
+                        P.depth[j] = P.max_depth;
+                        P.pixel[j] = (int32_t)pixel;
+                        take = true;
+                        c_primary++;
+                    }
+                }
+                const uint64_t cm = __ballot(take);
+                if (take) {
+                    const int r = __popcll(cm & lanes_below());
+                    pd.slot[r] = j;
+                    pd.v[0 * 64 + r] = o.x; pd.v[1 * 64 + r] = o.y; pd.v[2 * 64 + r] = o.z;
+                    pd.v[3 * 64 + r] = d.x; pd.v[4 * 64 + r] = d.y; pd.v[5 * 64 + r] = d.z;
+                }
+                wave_lds_sync();
                 pend_lo = 0;
                 pend_hi = __popcll(cm);
-                win_next += 64;
+                sc.win_next += 64;
                 continue;
             }
             const int avail = pend_hi - pend_lo;
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
-                s = pend[pend_lo + rank];
+                const int e = pend_lo + rank;
+                s = pd.slot[e];
+                trav_begin(T, S, dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
+                           dv(pd.v[3 * 64 + e], pd.v[4 * 64 + e], pd.v[5 * 64 + e]), 99999999.);  // Integrators.fs:108
                 idle = false;
                 active = true;
-                o = dv(P.ox[s], P.oy[s], P.oz[s]);
-                if (SHADOW) {
-                    d = dv(P.sdx[s], P.sdy[s], P.sdz[s]);
-                    tmax64 = P.stmax[s];  // dist - 1e-6 (Integrators.fs:44)
-                } else {
-                    d = dv(P.dx[s], P.dy[s], P.dz[s]);
-                    tmax64 = 99999999.;   // Integrators.fs:108
-                    if (P.depth[s] != P.max_depth) c_ext++;
-                }
-                c_rays++;
-                rf = make_rayf(o, d);
-                tlim = f_round_up(tmax64);
-                best_t = tmax64;
-                best_slot = -1;
-                best_first = -1;
-                found = false;
-                sp = 0;
-                node = S.root_is_leaf ? ~0 : 0;
             }
             const int pm = __popcll(m);
             pend_lo += pm < avail ? pm : avail;
             m = __ballot(idle);
         }
-        if (!__any(active)) break;  // every chunk taken and every pending slot traced
-        if (active) {
-            // ---- internal nodes until this lane reaches a leaf (while-while) ----
-            while (node >= 0) {
-                if (STATS) st.nodes++;
-                node = node_step(S.nodes, node, rf, tlim, stack, sp);
+        if (!__any(active)) break;  // every chunk taken and every pending ray traced
+        if (active && trav_step<false, STATS>(T, S, stack, st)) {
+            if (T.found) {
+                const DV hp = vadd(T.o, vmul(T.d, T.best_t));  // Ray.PointAtParameter (Ray.fs:8-9)
+                P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
             }
-            bool done = node == MFX_TRAV_EXIT;
-            // ---- one reference leaf (exact FP64) ----
-            if (!done) {
-                double t;
-                int sl, f;
-                if (cluster_hit<SHADOW, STATS>(S, ~node, o, d, 1e-6, tmax64, found ? best_t : __builtin_inf(), t, sl,
-                                               f, st)) {
-                    if (SHADOW) {
-                        found = true;
-                        done = true;
-                    } else if (!found || t < best_t || (t == best_t && f > best_first)) {
-                        found = true;
-                        best_t = t;
-                        best_slot = sl;
-                        best_first = f;
-                        tlim = f_round_up(t);
-                    }
-                }
-                if (!done) {
-                    if (sp == 0) done = true;
-                    else node = stack[(--sp) * 64];
-                }
-            }
-            if (done) {
-                if (SHADOW) {
-                    if (!found) {  // unoccluded: add this vertex's direct-light term
-                        P.lx[s] += P.scx[s];
-                        P.ly[s] += P.scy[s];
-                        P.lz[s] += P.scz[s];
-                    }
-                    P.state[s] = P.state[s] == WF_SHADOW_CONT ? WF_NEED_EXT : WF_DONE;
-                } else {
-                    P.hit_t[s] = found ? best_t : -1.0;
-                    P.hit_slot[s] = best_slot;
-                    P.state[s] = WF_EXT_DONE;
-                }
-                active = false;
-            }
+            P.hit_slot[s] = T.found ? T.best_slot : -1;
+            P.state[s] = WF_EXT_DONE;
+            active = false;
         }
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
-    block_add<4>(cnt + (SHADOW ? 2 : 1), SHADOW ? c_rays : c_ext, red);
+    block_add<4>(cnt + 0, c_primary, red);
+    block_add<4>(cnt + 1, c_ext, red);
     if (STATS) {
-        const int b = SHADOW ? 7 : 4;
-        block_add<4>(cnt + b, st.nodes, red);
-        block_add<4>(cnt + b + 1, st.clusters, red);
-        block_add<4>(cnt + b + 2, st.prims, red);
+        block_add<4>(cnt + 4, st.nodes, red);
+        block_add<4>(cnt + 5, st.clusters, red);
+        block_add<4>(cnt + 6, st.prims, red);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_shade: one vertex of PathIntegrator.TraceRay (Integrators.fs:109-136) per EXT_DONE slot
+// k_shadow: shade EXT_DONE slots at fetch time, trace the vertex's shadow ray, retire or continue
 // ------------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) k_shade(WfParams P) {
-    const int s = blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= P.pool || P.state[s] != WF_EXT_DONE) return;
-    const double th = P.hit_t[s];
-    if (th < 0.0) {
-        P.state[s] = WF_DONE;  // miss: TraceRay returns black (Integrators.fs:137)
-        return;
+template <bool STATS>
+__global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
+    extern __shared__ int lds[];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    int* stack = lds + wave * P.stack_size * 64 + lane;
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
+    const Pend pd(pend_base + wave * WF_PEND_BYTES);
+    uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
+    const SceneView S{P.nodes, P.blob, P.root_is_leaf};
+    const int shard_size = P.pool / WF_SHARDS;
+
+    Scanner sc{0, 0, 0, false};
+    int pend_lo = 0, pend_hi = 0;
+    bool active = false;
+    int s = 0;
+    Trav T{};
+    double scx = 0.0, scy = 0.0, scz = 0.0;  // this vertex's direct term if unoccluded
+    bool cont = false;                        // the path continues after this vertex
+    uint32_t c_shadow = 0;
+    Stats st{0, 0, 0};
+
+    while (true) {
+        bool idle = !active;
+        uint64_t m = __ballot(idle);
+        while (m != 0 && !sc.exhausted) {
+            if (pend_lo == pend_hi) {
+                if (!sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size)) break;
+                // scan a 64-slot window with the whole wave: shade every hit, retire every miss
+                const int j = sc.win_next + lane;
+                bool take = false;
+                DV unit = dv(0, 0, 0);
+                double tmax = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
+                bool cn = false;
+                if (j < sc.win_end && P.state[j] == WF_EXT_DONE) {
+                    const int slot = P.hit_slot[j];
+                    if (slot < 0) {
+                        retire(P, j, P.lx[j], P.ly[j], P.lz[j]);  // miss: TraceRay returns black (Integrators.fs:137)
+                    } else {
+                        // ---- one vertex of PathIntegrator.TraceRay (Integrators.fs:109-136) ----
+                        const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
+                        const MfxShade sh = P.shade[slot];
+                        DV nm;
+                        if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
+                        else nm = ld3(sh.n);
+                        const uint64_t key = P.key[j];
+                        uint32_t rn = P.rn[j];
+                        // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
+                        DV p = dv(20, 20, 20);
+                        while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
+                            const double rx = rng_next(key, rn);
+                            const double ry = rng_next(key, rn);
+                            const double rz = rng_next(key, rn);
+                            p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
+                        }
+                        const DV wi = vnormalize(p);
+                        const double ei = vdot(nm, wi);
+                        const double* a = P.albedo + 3 * sh.material;
+                        // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
+                        const MfxLight& LT = *P.light;
+                        const double sel = rng_next(key, rn);
+                        const int lt = sel < 0.5 ? 0 : 1;
+                        const double tu = rng_next(key, rn);
+                        const double tv = rng_next(key, rn);
+                        double uu = tu, vv = tv;
+                        if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
+                        const double sq = sqrt(1. - uu);
+                        const double s1 = 1. - sq, s2 = vv * sq;
+                        const DV lp = vadd(vadd(ld3(LT.v0[lt]), vmul(ld3(LT.e1[lt]), s1)), vmul(ld3(LT.e2[lt]), s2));
+                        const DV toLight = vsub(lp, hp);
+                        const double dist = vlen(toLight);
+                        unit = vdiv(toLight, dist);
+                        // NewAreaLight.L (Light.fs:48-56) and the unclamped cosine (Integrators.fs:52)
+                        const double cos_o = vdot(toLight, ld3(LT.normal));
+                        const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
+                        const double solid = fabs(cos_o) * LT.area / dist2;
+                        const double cs = vdot(unit, nm);
+                        const double Tx = P.tx[j] * (TWOPI * (ei * (INVPI * a[0])));
+                        const double Ty = P.ty[j] * (TWOPI * (ei * (INVPI * a[1])));
+                        const double Tz = P.tz[j] * (TWOPI * (ei * (INVPI * a[2])));
+                        // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
+                        if (cos_o < 0.) {
+                            dx = Tx * ((cs * (solid * LT.color[0])) / LT.pdf);
+                            dy = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
+                            dz = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
+                        }
+                        P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
+                        P.rn[j] = rn;
+                        const int depth = P.depth[j] - 1;
+                        P.depth[j] = depth;
+                        // the depth -1 query's result is discarded (Integrators.fs:109): never traced
+                        cn = depth >= 0;
+                        if (cn) { P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z; }
+                        tmax = dist - 1e-6;  // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (:44)
+                        take = true;
+                        c_shadow++;
+                    }
+                }
+                const uint64_t cm = __ballot(take);
+                if (take) {
+                    const int r = __popcll(cm & lanes_below());
+                    pd.slot[r] = j;
+                    pd.flag[r] = cn ? 1 : 0;
+                    pd.v[0 * 64 + r] = unit.x; pd.v[1 * 64 + r] = unit.y; pd.v[2 * 64 + r] = unit.z;
+                    pd.v[3 * 64 + r] = tmax;
+                    pd.v[4 * 64 + r] = dx; pd.v[5 * 64 + r] = dy; pd.v[6 * 64 + r] = dz;
+                }
+                wave_lds_sync();
+                pend_lo = 0;
+                pend_hi = __popcll(cm);
+                sc.win_next += 64;
+                continue;
+            }
+            const int avail = pend_hi - pend_lo;
+            const int rank = __popcll(m & lanes_below());
+            if (idle && rank < avail) {
+                const int e = pend_lo + rank;
+                s = pd.slot[e];
+                cont = pd.flag[e] != 0;
+                scx = pd.v[4 * 64 + e]; scy = pd.v[5 * 64 + e]; scz = pd.v[6 * 64 + e];
+                // origin = the hit point k_extend stored (a cache hit: the scan just read it)
+                trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
+                           pd.v[3 * 64 + e]);
+                idle = false;
+                active = true;
+            }
+            const int pm = __popcll(m);
+            pend_lo += pm < avail ? pm : avail;
+            m = __ballot(idle);
+        }
+        if (!__any(active)) break;
+        if (active && trav_step<true, STATS>(T, S, stack, st)) {
+            double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
+            if (!T.found) {  // unoccluded: add this vertex's direct-light term
+                lx += scx;
+                ly += scy;
+                lz += scz;
+            }
+            if (cont) {
+                if (!T.found) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
+                P.state[s] = WF_NEED_EXT;
+            } else {
+                retire(P, s, lx, ly, lz);
+            }
+            active = false;
+        }
     }
-    const int slot = P.hit_slot[s];
-    const DV o = dv(P.ox[s], P.oy[s], P.oz[s]), d = dv(P.dx[s], P.dy[s], P.dz[s]);
-    const MfxShade sh = P.shade[slot];
-    const DV hp = vadd(o, vmul(d, th));  // Ray.PointAtParameter (Ray.fs:8-9)
-    DV nm;
-    if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
-    else nm = ld3(sh.n);
-    const uint64_t key = P.key[s];
-    uint32_t rn = P.rn[s];
-    // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
-    DV p = dv(20, 20, 20);
-    while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
-        const double rx = rng_next(key, rn);
-        const double ry = rng_next(key, rn);
-        const double rz = rng_next(key, rn);
-        p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
-    }
-    const DV wi = vnormalize(p);
-    const double ei = vdot(nm, wi);
-    const double* a = P.albedo + 3 * sh.material;
-    // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
-    const MfxLight& LT = *P.light;
-    const double sel = rng_next(key, rn);
-    const int lt = sel < 0.5 ? 0 : 1;
-    const double tu = rng_next(key, rn);
-    const double tv = rng_next(key, rn);
-    double uu = tu, vv = tv;
-    if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
-    const double sq = sqrt(1. - uu);
-    const double s1 = 1. - sq, s2 = vv * sq;
-    const DV lp = vadd(vadd(ld3(LT.v0[lt]), vmul(ld3(LT.e1[lt]), s1)), vmul(ld3(LT.e2[lt]), s2));
-    const DV toLight = vsub(lp, hp);
-    const double dist = vlen(toLight);
-    const DV unit = vdiv(toLight, dist);
-    // NewAreaLight.L (Light.fs:48-56) and the unclamped cosine (Integrators.fs:52)
-    const double cos_o = vdot(toLight, ld3(LT.normal));
-    const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
-    const double solid = fabs(cos_o) * LT.area / dist2;
-    const double cs = vdot(unit, nm);
-    const double Tx = P.tx[s] * (TWOPI * (ei * (INVPI * a[0])));
-    const double Ty = P.ty[s] * (TWOPI * (ei * (INVPI * a[1])));
-    const double Tz = P.tz[s] * (TWOPI * (ei * (INVPI * a[2])));
-    // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
-    if (cos_o < 0.) {
-        P.scx[s] = Tx * ((cs * (solid * LT.color[0])) / LT.pdf);
-        P.scy[s] = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
-        P.scz[s] = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
-    } else {
-        P.scx[s] = 0.0; P.scy[s] = 0.0; P.scz[s] = 0.0;
-    }
-    P.tx[s] = Tx; P.ty[s] = Ty; P.tz[s] = Tz;
-    P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
-    P.sdx[s] = unit.x; P.sdy[s] = unit.y; P.sdz[s] = unit.z;
-    P.stmax[s] = dist - 1e-6;
-    P.rn[s] = rn;
-    const int depth = P.depth[s] - 1;
-    P.depth[s] = depth;
-    if (depth < 0) {
-        P.state[s] = WF_SHADOW_END;  // the depth -1 query's result is discarded (Integrators.fs:109)
-    } else {
-        P.dx[s] = wi.x; P.dy[s] = wi.y; P.dz[s] = wi.z;
-        P.state[s] = WF_SHADOW_CONT;
+    unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
+    block_add<4>(cnt + 2, c_shadow, red);
+    if (STATS) {
+        block_add<4>(cnt + 7, st.nodes, red);
+        block_add<4>(cnt + 8, st.clusters, red);
+        block_add<4>(cnt + 9, st.prims, red);
     }
 }
 
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-static size_t wf_lds_bytes(int stack_size) { return (size_t)4 * (stack_size * 64 + 64) * sizeof(int) + 64; }
+WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n) {
+    WfParams S = P;
+    double** dbl[] = {&S.ox, &S.oy, &S.oz, &S.dx, &S.dy, &S.dz, &S.tx, &S.ty, &S.tz, &S.lx, &S.ly, &S.lz};
+    static_assert(sizeof(dbl) / sizeof(dbl[0]) == WF_DOUBLES_PER_SLOT - 1, "slot arrays");
+    for (double** d : dbl) *d += first;
+    S.key += first;
+    S.rn += first;
+    S.depth += first;
+    S.pixel += first;
+    S.hit_slot += first;
+    S.state += first;
+    S.pool = n;
+    return S;
+}
+
+static size_t wf_lds_bytes(int stack_size) {
+    return (size_t)4 * stack_size * 64 * sizeof(int) + 4 * WF_PEND_BYTES + 64;
+}
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
     const size_t lds = wf_lds_bytes(stack_size);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, k_traverse<false, false>, 256, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, k_extend<false>, 256, lds);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, k_traverse<true, false>, 256, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, k_shadow<false>, 256, lds);
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
-    const unsigned logic_blocks = (unsigned)((P.pool + 1023) / 1024);
-    const unsigned pool_blocks = (unsigned)((P.pool + 255) / 256);
     const size_t lds = wf_lds_bytes(P.stack_size);
     hipError_t e = hipMemsetAsync(P.ctl + WF_CTL_EXT, 0, 2 * WF_SHARDS * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_logic, dim3(logic_blocks), dim3(1024), 0, st, P);
+    if (stats)
+        hipLaunchKernelGGL(k_extend<true>, dim3(ext_grid), dim3(256), lds, st, P);
+    else
+        hipLaunchKernelGGL(k_extend<false>, dim3(ext_grid), dim3(256), lds, st, P);
     if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return e;
     if (stats)
-        hipLaunchKernelGGL((k_traverse<false, true>), dim3(ext_grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL(k_shadow<true>, dim3(shd_grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_traverse<false, false>), dim3(ext_grid), dim3(256), lds, st, P);
-    if ((e = hipEventRecord(ev[1], st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(k_shade, dim3(pool_blocks), dim3(256), 0, st, P);
-    if ((e = hipEventRecord(ev[2], st)) != hipSuccess) return e;
-    if (stats)
-        hipLaunchKernelGGL((k_traverse<true, true>), dim3(shd_grid), dim3(256), lds, st, P);
-    else
-        hipLaunchKernelGGL((k_traverse<true, false>), dim3(shd_grid), dim3(256), lds, st, P);
-    return hipGetLastError();
-}
-
-hipError_t mfx_wf_finish(const WfParams& P, hipStream_t st) {
-    const unsigned logic_blocks = (unsigned)((P.pool + 1023) / 1024);
-    hipLaunchKernelGGL(k_logic, dim3(logic_blocks), dim3(1024), 0, st, P);
+        hipLaunchKernelGGL(k_shadow<false>, dim3(shd_grid), dim3(256), lds, st, P);
     return hipGetLastError();
 }
