@@ -11,7 +11,7 @@ Rays counted = primary + extension (closest-hit queries actually traced) + shado
 from the kernel's own counters. Inputs (scene, BVH) are resident in HBM before timing starts.
 
 Extra objects on the JSON line:
-  roofline      the dominant kernel — k_traverse<false,false>, the closest-hit traversal of the
+  roofline      the dominant kernel — k_extend<false>, path start + closest-hit traversal of the
                 wavefront pipeline — algorithmic bytes per launch / its HIP-event duration vs HBM
                 8 TB/s; bytes per ray from the kernel's traversal counters; traffic =
                 PMC HBM bytes per launch (profiles/traffic_spot_1080p.json, scripts/profile_r01.sh)
@@ -204,7 +204,7 @@ def main():
                     n_c, n_s = fixture["closest_rays"], fixture["shadow_rays"]
                     bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
             else:
-                kname, kms, krays = "k_traverse<false, false>", stage_ms["extend_ms"], closest_rays / args.steps
+                kname, kms, krays = "k_extend<false>", stage_ms["extend_ms"], closest_rays / args.steps
                 launches = stage_ms["launches"]
                 bray = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
             # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
