@@ -50,6 +50,7 @@ struct mfx_ctx {
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
     uint8_t* d_blob = nullptr;
+    uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
     double* d_albedo = nullptr;
     MfxLight* d_light = nullptr;
@@ -93,7 +94,7 @@ struct mfx_ctx {
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    void* bufs[] = {c->d_nodes, c->d_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_blob, c->d_ref_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -161,6 +162,7 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
     CK(upload(&c->d_blob, c->host.blob));
+    CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
     CK(upload(&c->d_albedo, c->host.albedo));
     CK(upload(&c->d_light, std::vector<MfxLight>{c->host.light}));
@@ -231,6 +233,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
     P.blob = c->d_blob;
+    P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.albedo = c->d_albedo;
     P.light = c->d_light;
@@ -367,6 +370,7 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
     P.blob = c->d_blob;
+    P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.albedo = c->d_albedo;
     P.accum = c->d_accum;
@@ -554,6 +558,7 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
         Q.blob = c->d_blob;
+        Q.ref_blob = c->d_ref_blob;
         Q.shade = c->d_shade;
         Q.rays = d_rays;
         Q.tmax_per_ray = d_tmax;

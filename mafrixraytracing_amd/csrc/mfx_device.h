@@ -10,6 +10,7 @@
 struct TraceParams {
     const MfxNode* nodes;
     const uint8_t* blob;
+    const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* albedo;
     double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
@@ -30,6 +31,7 @@ struct TraceParams {
 struct QueryParams {
     const MfxNode* nodes;
     const uint8_t* blob;
+    const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* rays;
     const double* tmax_per_ray;

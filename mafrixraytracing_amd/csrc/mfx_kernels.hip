@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
     const MfxLight& LT = *P.light;
     const MfxCamera& CAM = *P.cam;
     const int W = P.width, H = P.height;
@@ -115,9 +115,10 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
         if (!alive) continue;
 
         // ---- closest hit: bvh.Hit(ray, 1e-6, 99999999.)  (Integrators.fs:108) ----
-        double th;
-        int slot;
-        const bool hit = traverse<false, STATS>(S, o, d, 1e-6, 99999999., stack, th, slot, st);
+        Best hb;
+        const bool hit = traverse<false, STATS>(S, o, d, 1e-6, 99999999., stack, hb, st);
+        const double th = hb.t;
+        const int slot = hb.info & MFX_INFO_SHADE_MASK;
         if (depth != P.max_depth) c_ext++;
         bool finish = !hit;
         if (hit) {
@@ -163,9 +164,8 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             const bool lit = cos_o < 0.;
             T = dv(T.x * col.x, T.y * col.y, T.z * col.z);  // path throughput incl. this vertex's col
             // SingleDirectLightIntegrator.Eval — Integrators.fs:41-52
-            double tsh;
-            int ssh;
-            const bool occluded = traverse<true, STATS>(S, hp, unit, 1e-6, dist - 1e-6, stack, tsh, ssh, st2);
+            Best sb;
+            const bool occluded = traverse<true, STATS>(S, hp, unit, 1e-6, dist - 1e-6, stack, sb, st2);
             c_shadow++;
             if (!occluded && lit) {
                 // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
@@ -226,12 +226,13 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.blob, Q.root_is_leaf};
+    const SceneView S{Q.nodes, Q.blob, Q.ref_blob, Q.root_is_leaf};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
-    double t;
-    int slot;
+    Best B;
     Stats st{0, 0, 0};
-    const bool h = traverse<false, false>(S, o, d, Q.tmin, Q.tmax, stack, t, slot, st);
+    const bool h = traverse<false, false>(S, o, d, Q.tmin, Q.tmax, stack, B, st);
+    const double t = B.t;
+    const int slot = B.info & MFX_INFO_SHADE_MASK;
     if (h) {
         const MfxShade sh = Q.shade[slot];
         Q.t_out[k] = t;
@@ -257,12 +258,11 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.blob, Q.root_is_leaf};
+    const SceneView S{Q.nodes, Q.blob, Q.ref_blob, Q.root_is_leaf};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
-    double t;
-    int slot;
+    Best B;
     Stats st{0, 0, 0};
-    Q.occ_out[k] = traverse<true, false>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, t, slot, st) ? 1 : 0;
+    Q.occ_out[k] = traverse<true, false>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, B, st) ? 1 : 0;
 }
 
 // ----------------------------------------------------------------------------------------------

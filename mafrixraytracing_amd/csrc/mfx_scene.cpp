@@ -7,13 +7,15 @@
 //    is hit beyond tMax (Triangle.Hit ignores tMax, Trangle.fs:148; the leaf minBy, :76-80).
 //    Its median split sorts with F#'s Array.sortInPlaceBy = .NET 6 introsort, restated here so
 //    ties fall the same way.
-// 3. A binned-SAH BVH2 over those leaves ("clusters") is what the GPU traverses, in FP32
-//    with conservatively widened boxes; the exact FP64 leaf test happens at each cluster.
+// 3. A binned-SAH BVH2 over the individual primitives is what the GPU traverses, in FP32 with
+//    conservatively widened boxes. Every primitive slot carries its reference leaf and position,
+//    so the reference's leaf semantics are applied exactly per candidate hit.
 #include "mfx_scene.h"
 
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 namespace {
@@ -213,27 +215,39 @@ struct FBox {
 };
 
 struct SahBuilder {
-    std::vector<FBox> cb;      // cluster boxes (conservative FP32)
-    std::vector<float> cent;   // centroids [3*n]
-    std::vector<int32_t> ids;  // permutation being partitioned
+    std::vector<FBox> cb;       // item boxes (conservative FP32)
+    std::vector<float> cent;    // centroids [3*n]
+    std::vector<float> weight;  // intersection cost of an item (slots it tests)
+    std::vector<int32_t> ids;   // permutation being partitioned
+    std::vector<std::pair<int, int>> leaves;  // [b, e) ranges of ids, in creation order
     std::vector<MfxNode>& nodes;
     int max_depth = 0;
+    int max_leaf = 4;
+    float c_isect = 1.5f;  // cost of one primitive slot test relative to one node step
     static constexpr int NB = 32;
 
     explicit SahBuilder(std::vector<MfxNode>& n) : nodes(n) {}
 
-    // returns child reference; fills `out` with the subtree box
+    int make_leaf(int b, int e, FBox& out) {
+        out = FBox::empty();
+        for (int i = b; i < e; ++i) out.grow(cb[ids[i]]);
+        leaves.emplace_back(b, e);
+        return ~(int)(leaves.size() - 1);
+    }
+
+    // returns child reference (>= 0 node, < 0 ~leaf); fills `out` with the subtree box
     int build(int b, int e, int depth, FBox& out) {
         max_depth = std::max(max_depth, depth);
-        if (e - b == 1) {
-            out = cb[ids[b]];
-            return ~ids[b];
-        }
-        FBox cbox = FBox::empty();
+        const int n = e - b;
+        if (n == 1) return make_leaf(b, e, out);
+        FBox cbox = FBox::empty(), box = FBox::empty();
+        float wsum = 0.f;
         for (int i = b; i < e; ++i) {
             FBox p;
             for (int a = 0; a < 3; ++a) p.lo[a] = p.hi[a] = cent[3 * ids[i] + a];
             cbox.grow(p);
+            box.grow(cb[ids[i]]);
+            wsum += weight[ids[i]];
         }
         int best_axis = -1, best_split = 0;
         float best_cost = FLT_MAX;
@@ -241,31 +255,38 @@ struct SahBuilder {
             float ext = cbox.hi[a] - cbox.lo[a];
             if (!(ext > 0.f)) continue;
             FBox bb[NB];
+            float wb[NB] = {0};
             int cnt[NB] = {0};
             for (int k = 0; k < NB; ++k) bb[k] = FBox::empty();
             for (int i = b; i < e; ++i) {
                 int k = (int)((cent[3 * ids[i] + a] - cbox.lo[a]) / ext * NB);
                 k = std::min(NB - 1, std::max(0, k));
                 cnt[k]++;
+                wb[k] += weight[ids[i]];
                 bb[k].grow(cb[ids[i]]);
             }
-            float ra[NB];
+            float ra[NB], rw[NB];
             int rc[NB];
             FBox acc = FBox::empty();
             int c = 0;
+            float w = 0.f;
             for (int k = NB - 1; k > 0; --k) {
                 acc.grow(bb[k]);
                 c += cnt[k];
+                w += wb[k];
                 ra[k] = acc.area();
                 rc[k] = c;
+                rw[k] = w;
             }
             acc = FBox::empty();
             c = 0;
+            w = 0.f;
             for (int k = 0; k < NB - 1; ++k) {
                 acc.grow(bb[k]);
                 c += cnt[k];
+                w += wb[k];
                 if (c == 0 || rc[k + 1] == 0) continue;
-                float cost = acc.area() * c + ra[k + 1] * rc[k + 1];
+                float cost = acc.area() * w + ra[k + 1] * rw[k + 1];
                 if (cost < best_cost) {
                     best_cost = cost;
                     best_axis = a;
@@ -273,6 +294,10 @@ struct SahBuilder {
                 }
             }
         }
+        // SAH: leaf if testing everything here is no dearer than one more node step plus the split
+        const float area = box.area();
+        if (n <= max_leaf && (best_axis < 0 || c_isect * wsum * area <= area + c_isect * best_cost))
+            return make_leaf(b, e, out);
         int mid;
         if (best_axis < 0) {
             mid = (b + e) / 2;  // all centroids coincide: split by position
@@ -291,13 +316,13 @@ struct SahBuilder {
         FBox lb, rb;
         int l = build(b, mid, depth + 1, lb);
         int r = build(mid, e, depth + 1, rb);
-        MfxNode& n = nodes[self];
-        n.c0lox = lb.lo[0]; n.c0hix = lb.hi[0]; n.c0loy = lb.lo[1]; n.c0hiy = lb.hi[1];
-        n.c1lox = rb.lo[0]; n.c1hix = rb.hi[0]; n.c1loy = rb.lo[1]; n.c1hiy = rb.hi[1];
-        n.c0loz = lb.lo[2]; n.c0hiz = lb.hi[2]; n.c1loz = rb.lo[2]; n.c1hiz = rb.hi[2];
-        n.child0 = l;
-        n.child1 = r;
-        n.pad0 = n.pad1 = 0;
+        MfxNode& nd = nodes[self];
+        nd.c0lox = lb.lo[0]; nd.c0hix = lb.hi[0]; nd.c0loy = lb.lo[1]; nd.c0hiy = lb.hi[1];
+        nd.c1lox = rb.lo[0]; nd.c1hix = rb.hi[0]; nd.c1loy = rb.lo[1]; nd.c1hiy = rb.hi[1];
+        nd.c0loz = lb.lo[2]; nd.c0hiz = lb.hi[2]; nd.c1loz = rb.lo[2]; nd.c1hiz = rb.hi[2];
+        nd.child0 = l;
+        nd.child1 = r;
+        nd.pad0 = nd.pad1 = 0;
         out = lb;
         out.grow(rb);
         return self;
@@ -413,6 +438,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         put(lf.hi, b.hi);
         lf.first = s.leaf_first[c];
         lf.count = s.leaf_count[c];
+        lf.pad = 0;
         lf.kinds = 0;
         for (int k = 0; k < lf.count; ++k) lf.kinds |= d->prims[s.ref_indices[lf.first + k]].kind << (2 * k);
     }
@@ -459,7 +485,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         put(s.light.color, d3(L.intensity));
     }
 
-    // ---- conservative FP32 cluster boxes + SAH BVH2 ----------------------------------------
+    // ---- conservative FP32 primitive boxes + SAH BVH2 over primitives ----------------------
     double R = 0, T = 0;
     {
         Box all = pb[0];
@@ -473,36 +499,56 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
     s.eps = (float)std::ldexp(R + T, -19);
     s.nodes.clear();
     SahBuilder sb(s.nodes);
-    sb.cb.resize(nc);
-    sb.cent.resize(3 * (size_t)nc);
-    sb.ids.resize(nc);
-    for (int c = 0; c < nc; ++c) {
+    if (const char* e = getenv("MFX_LEAF_MAX")) sb.max_leaf = std::max(1, std::min(4, atoi(e)));
+    if (const char* e = getenv("MFX_SAH_CI")) sb.c_isect = (float)atof(e);
+    sb.cb.resize(n);
+    sb.cent.resize(3 * (size_t)n);
+    sb.weight.resize(n);
+    sb.ids.resize(n);
+    for (int i = 0; i < n; ++i) {
         FBox f;
         for (int a = 0; a < 3; ++a) {
-            f.lo[a] = round_down(leaves[c].lo[a] - (double)s.eps);
-            f.hi[a] = round_up(leaves[c].hi[a] + (double)s.eps);
-            sb.cent[3 * c + a] = 0.5f * (f.lo[a] + f.hi[a]);
+            const double lo = comp(pb[i].lo, a), hi = comp(pb[i].hi, a);
+            f.lo[a] = round_down(lo - (double)s.eps);
+            f.hi[a] = round_up(hi + (double)s.eps);
+            sb.cent[3 * i + a] = 0.5f * (f.lo[a] + f.hi[a]);
         }
-        sb.cb[c] = f;
-        sb.ids[c] = c;
+        sb.cb[i] = f;
+        sb.weight[i] = (float)nslot_of[i];
+        sb.ids[i] = i;
     }
-    if (nc == 1) {
-        s.root_is_leaf = 1;
-        s.bvh_depth = 0;
-    } else {
-        FBox rootbox;
-        sb.build(0, nc, 0, rootbox);
-        s.root_is_leaf = 0;
-        s.bvh_depth = sb.max_depth;
+    FBox rootbox;
+    const int root = sb.build(0, n, 0, rootbox);
+    s.root_is_leaf = root < 0 ? 1 : 0;
+    s.bvh_depth = root < 0 ? 0 : sb.max_depth;
+    const int nl = (int)sb.leaves.size();
+
+    // ---- where each primitive sits in the reference grouping --------------------------------
+    std::vector<int32_t> ref_leaf_of(n), pos_of(n);
+    for (int c = 0; c < nc; ++c)
+        for (int k = 0; k < leaves[c].count; ++k) {
+            ref_leaf_of[s.ref_indices[leaves[c].first + k]] = c;
+            pos_of[s.ref_indices[leaves[c].first + k]] = k;
+        }
+    std::vector<int32_t> ref16(nc);
+    {
+        size_t off = 0;
+        for (int c = 0; c < nc; ++c) {
+            ref16[c] = (int32_t)(off / 16);
+            off += sizeof(MfxLeaf);
+            for (int k = 0; k < leaves[c].count; ++k) off += sizeof(MfxSlot) * nslot_of[s.ref_indices[leaves[c].first + k]];
+        }
+        if (off / 16 >= (size_t)0x7fffffff) {
+            err = "reference-leaf image too large";
+            return false;
+        }
     }
 
-    // ---- leaf blob in depth-first leaf order; child refs become ~(16-byte offset) ----------
+    // ---- traversal leaves in depth-first order; child refs become ~(16-byte offset) --------
     std::vector<int> order;
-    order.reserve(nc);
-    if (nc == 1) {
-        order.push_back(0);
-    } else {
-        std::vector<int> st{0};  // depth-first, child0 before child1
+    order.reserve(nl);
+    {
+        std::vector<int> st{root};  // depth-first, child0 before child1
         while (!st.empty()) {
             const int ref = st.back();
             st.pop_back();
@@ -514,29 +560,58 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             }
         }
     }
-    std::vector<int32_t> offset16(nc);
+    std::vector<int32_t> offset16(nl), shade_of(n);
     s.blob.clear();
     s.shade.clear();
-    for (int c : order) {
-        MfxLeaf lf = leaves[c];
-        lf.shade_base = (int32_t)s.shade.size();
-        offset16[c] = (int32_t)(s.blob.size() / 16);
-        const uint8_t* hp = (const uint8_t*)&lf;
-        s.blob.insert(s.blob.end(), hp, hp + sizeof(MfxLeaf));
-        for (int k = 0; k < lf.count; ++k) {
-            const int p = s.ref_indices[lf.first + k];
+    for (int l : order) {
+        const int b = sb.leaves[l].first, e = sb.leaves[l].second;
+        MfxTLeaf h{};
+        h.count = e - b;
+        for (int k = 0; k < h.count; ++k) h.kinds |= d->prims[sb.ids[b + k]].kind << (2 * k);
+        offset16[l] = (int32_t)(s.blob.size() / 16);
+        const uint8_t* hp = (const uint8_t*)&h;
+        s.blob.insert(s.blob.end(), hp, hp + sizeof(MfxTLeaf));
+        for (int k = 0; k < h.count; ++k) {
+            const int p = sb.ids[b + k];
+            shade_of[p] = (int32_t)s.shade.size();
             for (int j = 0; j < nslot_of[p]; ++j) {
-                const uint8_t* sp = (const uint8_t*)&pslots[slot_of[p] + j];
+                MfxSlot sl = pslots[slot_of[p] + j];
+                sl.ref16 = ref16[ref_leaf_of[p]];
+                sl.info = (int32_t)s.shade.size() | (pos_of[p] << MFX_INFO_POS_SHIFT);
+                const uint8_t* sp = (const uint8_t*)&sl;
                 s.blob.insert(s.blob.end(), sp, sp + sizeof(MfxSlot));
                 s.shade.push_back(pshade[slot_of[p] + j]);
             }
         }
+    }
+    if (s.blob.size() / 16 >= (size_t)0x7fffffff || s.shade.size() > MFX_INFO_SHADE_MASK) {
+        err = "scene too large for the traversal image";
+        return false;
     }
     s.blob.resize(s.blob.size() + 3 * sizeof(MfxSlot), 0);  // speculative slot loads stay in bounds
     for (MfxNode& nd : s.nodes) {
         if (nd.child0 < 0) nd.child0 = ~offset16[~nd.child0];
         if (nd.child1 < 0) nd.child1 = ~offset16[~nd.child1];
     }
+
+    // ---- reference leaves (heap order): FP64 box header + slot copies ----------------------
+    s.ref_blob.clear();
+    for (int c = 0; c < nc; ++c) {
+        const uint8_t* hp = (const uint8_t*)&leaves[c];
+        s.ref_blob.insert(s.ref_blob.end(), hp, hp + sizeof(MfxLeaf));
+        for (int k = 0; k < leaves[c].count; ++k) {
+            const int p = s.ref_indices[leaves[c].first + k];
+            for (int j = 0; j < nslot_of[p]; ++j) {
+                MfxSlot sl = pslots[slot_of[p] + j];
+                sl.ref16 = ref16[c];
+                sl.info = (shade_of[p] + j) | (k << MFX_INFO_POS_SHIFT);
+                const uint8_t* sp = (const uint8_t*)&sl;
+                s.ref_blob.insert(s.ref_blob.end(), sp, sp + sizeof(MfxSlot));
+            }
+        }
+    }
+    s.ref_blob.resize(s.ref_blob.size() + 3 * sizeof(MfxSlot), 0);
     s.nclusters = nc;
+    s.ntleaves = nl;
     return true;
 }

@@ -13,10 +13,12 @@ struct MfxHostScene {
     std::vector<int32_t> ref_indices;                  // `indices` after Subdivide
     std::vector<int32_t> leaf_first, leaf_count;       // leaves in heap (DFS) order
     // device images
-    std::vector<MfxNode> nodes;
-    std::vector<uint8_t> blob;    // MfxLeaf headers + inline MfxSlot records, DFS leaf order
-    std::vector<MfxShade> shade;  // per slot, in blob order
-    int32_t nclusters = 0;
+    std::vector<MfxNode> nodes;     // BVH2 over primitives
+    std::vector<uint8_t> blob;      // traversal leaves: MfxTLeaf headers + MfxSlot records, DFS order
+    std::vector<uint8_t> ref_blob;  // reference leaves: MfxLeaf headers + slot copies, heap order
+    std::vector<MfxShade> shade;    // per traversal slot, in blob order
+    int32_t nclusters = 0;          // reference leaves
+    int32_t ntleaves = 0;           // traversal leaves
     std::vector<double> albedo;  // [nmat][3]
     MfxLight light;
     MfxCamera camera;

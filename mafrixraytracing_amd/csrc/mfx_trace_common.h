@@ -115,45 +115,48 @@ __device__ __forceinline__ bool sphere_hit64(const MfxSlot& s, DV o, DV d, doubl
 
 struct SceneView {
     const MfxNode* __restrict__ nodes;
-    const uint8_t* __restrict__ blob;  // MfxLeaf + inline MfxSlot records
+    const uint8_t* __restrict__ blob;      // traversal leaves: MfxTLeaf + MfxSlot records
+    const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
     int32_t root_is_leaf;
 };
 
 struct Stats {
-    uint32_t nodes, clusters, prims;
+    uint32_t nodes, clusters, prims;  // internal-node visits, leaf visits, primitive tests
 };
 
-// One reference leaf: exact FP64 box test, then Array.minBy over its primitives with key
-// (hit ? t : tMax), first minimum wins (BvhNode.fs:76-80). Returns whether the leaf's result is
-// a hit; t and the shade[] index of the hit slot. The header and the slots are contiguous.
-//
-// The leaf's result is (box hit) && (minBy result is a hit); neither test has side effects, so
-// the primitives run first and the FP64 box test (six divisions) only when it can still change
-// the answer: the minBy result is a hit and, for closest queries, its t does not exceed the best
-// hit so far (`reject_above`; a larger t can never be accepted by the caller's tie rule). SHADOW
-// queries stop at the first primitive hit with t < tMax: its key is below every miss's key
-// (tMax), so the minBy result is a hit whatever follows. A hit beyond tMax (Triangle.Hit ignores
-// tMax, Trangle.fs:148) does not stop the scan — a later miss can still win the minBy.
-template <bool SHADOW, bool STATS>
-__device__ __forceinline__ bool cluster_hit(const SceneView& S, int off16, DV o, DV d, double tMin, double tMax,
-                                            double reject_above, double& t_out, int& slot_out, int& first_out,
-                                            Stats& st) {
-    const MfxLeaf* __restrict__ lf = (const MfxLeaf*)(S.blob + (size_t)off16 * 16);
+// The best hit so far under the reference's order: smallest t; equal t -> the later reference
+// leaf (larger `first`: `if l.t < r.t then l else r`, BvhNode.fs:70, ties go right); equal t in
+// one leaf -> the earlier primitive (Array.minBy keeps the first minimum, BvhNode.fs:80).
+struct Best {
+    double t;
+    int info;   // MfxSlot.info of the hit slot: shade[] index | position in its reference leaf
+    int first;  // MfxLeaf.first of its reference leaf
+    bool found;
+};
+__device__ __forceinline__ bool beats(const Best& B, double t, int first, int info) {
+    if (!B.found || t < B.t) return true;
+    if (t > B.t) return false;
+    const unsigned pos = (unsigned)info >> MFX_INFO_POS_SHIFT, bpos = (unsigned)B.info >> MFX_INFO_POS_SHIFT;
+    return first > B.first || (first == B.first && pos < bpos);
+}
+
+// One whole reference leaf, exactly as CheckHit evaluates it (BvhNode.fs:64-80): its FP64 box
+// test, then Array.minBy over its primitives with key (hit ? t : tMax), first minimum wins.
+// Returns whether the leaf's result is a hit, with its t, the hit slot's info and the leaf's
+// `first`. The two tests have no side effects, so the primitives run first and the box (six
+// FP64 divisions) only when the answer still depends on it.
+template <bool SHADOW>
+__device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV o, DV d, double tMin, double tMax,
+                             double& t_out, int& info_out, int& first_out) {
+    const MfxLeaf* __restrict__ lf = (const MfxLeaf*)(ref_blob + (size_t)off16 * 16);
     const MfxSlot* __restrict__ sl = (const MfxSlot*)(lf + 1);
-    // only the 16-B tail (count, kinds, first, shade_base) now; the box is read (L1/L2 hit)
-    // after the primitives, when needed — keeping six doubles live costs occupancy
-    struct Meta {
-        int32_t count, kinds, first, shade_base;
-    };
-    const Meta c = *(const Meta*)((const uint8_t*)lf + offsetof(MfxLeaf, count));
-    if (STATS) st.clusters++;
+    const int count = lf->count, kinds = lf->kinds;
     bool best_hit = false;
     double best_key = 0.0, best_t = 0.0;
-    int best_slot = -1;
+    int best_slot = 0;
     int cur = 0;
-    for (int k = 0; k < c.count; ++k) {
-        const int kind = (c.kinds >> (2 * k)) & 3;
-        if (STATS) st.prims++;
+    for (int k = 0; k < count; ++k) {
+        const int kind = (kinds >> (2 * k)) & 3;
         double t = 0.0;
         int hs = cur;
         bool h;
@@ -179,14 +182,81 @@ __device__ __forceinline__ bool cluster_hit(const SceneView& S, int off16, DV o,
             best_t = t;
             best_slot = hs;
         }
+        // a hit below tMax has a key below every miss's: the minBy result is a hit
         if (SHADOW && h && t < tMax) break;
     }
-    if (!best_hit || best_t > reject_above) return false;
+    if (!best_hit) return false;
     if (!aabb_hit64(lf->lo, lf->hi, o, d, tMin, tMax)) return false;
     t_out = best_t;
-    slot_out = c.shade_base + best_slot;
-    first_out = c.first;
+    info_out = sl[best_slot].info;
+    first_out = lf->first;
     return true;
+}
+
+// One traversal leaf (1..4 primitives of possibly different reference leaves). Each primitive
+// hit is a candidate for its reference leaf's result: with t < tMax the reference leaf's minBy
+// result is a hit of t no larger (the leaf's other primitives are tested in their own traversal
+// leaves), so the candidate counts iff it beats the best hit under the reference's order and its
+// reference leaf passes the exact FP64 box test (ancestor boxes contain it, and the rounded slab
+// test is monotone in the bounds, so they pass too). A hit at t >= tMax (Triangle.Hit ignores
+// tMax, Trangle.fs:148) is where the leaf's minBy can prefer a miss: that reference leaf is then
+// evaluated whole. SHADOW: returns true at the first occluding candidate. Closest: returns true
+// when B improved.
+template <bool SHADOW, bool STATS>
+__device__ __forceinline__ bool leaf_hit(const SceneView& S, int off16, DV o, DV d, double tMin, double tMax,
+                                         Best& B, Stats& st) {
+    const uint8_t* base = S.blob + (size_t)off16 * 16;
+    const MfxTLeaf h = *(const MfxTLeaf*)base;
+    const MfxSlot* __restrict__ sl = (const MfxSlot*)(base + sizeof(MfxTLeaf));
+    if (STATS) st.clusters++;
+    bool improved = false;
+    int cur = 0;
+    for (int k = 0; k < h.count; ++k) {
+        const int kind = (h.kinds >> (2 * k)) & 3;
+        if (STATS) st.prims++;
+        double t = 0.0;
+        int hs = cur;
+        bool hit;
+        if (kind == MFX_KIND_SPHERE) {
+            hit = sphere_hit64(sl[cur], o, d, tMin, tMax, t);
+            cur += 1;
+        } else {
+            hit = tri_hit64(sl[cur], o, d, tMin, t);
+            if (kind == MFX_KIND_RECT) {
+                if (!hit) {  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31)
+                    hs = cur + 1;
+                    hit = tri_hit64(sl[cur + 1], o, d, tMin, t);
+                }
+                cur += 2;
+            } else {
+                cur += 1;
+            }
+        }
+        if (!hit) continue;
+        const int ref16 = sl[hs].ref16;
+        if (t >= tMax) {
+            double t2;
+            int info2, first2;
+            if (ref_leaf_hit<SHADOW>(S.ref_blob, ref16, o, d, tMin, tMax, t2, info2, first2)) {
+                if (SHADOW) return true;
+                if (beats(B, t2, first2, info2)) {
+                    B = Best{t2, info2, first2, true};
+                    improved = true;
+                }
+            }
+            continue;
+        }
+        const int info = sl[hs].info;
+        if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
+        const MfxLeaf* __restrict__ rl = (const MfxLeaf*)(S.ref_blob + (size_t)ref16 * 16);
+        const int first = rl->first;
+        if (!SHADOW && !beats(B, t, first, info)) continue;
+        if (!aabb_hit64(rl->lo, rl->hi, o, d, tMin, tMax)) continue;
+        if (SHADOW) return true;
+        B = Best{t, info, first, true};
+        improved = true;
+    }
+    return improved;
 }
 
 __device__ __forceinline__ float f_round_up(double x) {
@@ -246,27 +316,15 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     return any ? near : (pop ? top : MFX_TRAV_EXIT);
 }
 
-// Bvh.Hit over the cluster BVH2. SHADOW: returns occluded (any leaf reporting a hit; the
-// reference's combine returns a hit iff some visited leaf does). Otherwise: closest leaf hit,
-// ties going to the later leaf (the reference's `if l.t < r.t then l else r`, BvhNode.fs:70).
-// The stack lives in LDS, one column per lane (stride 64 dwords: conflict-free).
+// Bvh.Hit over the primitive BVH2 (megakernel and query kernels). SHADOW: returns occluded
+// (the reference's combine returns a hit iff some visited leaf does). Otherwise: the closest hit
+// under the reference's order (Best). The stack lives in LDS, one column per lane (stride 64
+// dwords: conflict-free).
 template <bool SHADOW, bool STATS>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
-                         double& t_best, int& slot_best, Stats& st) {
-    t_best = tMax;
-    slot_best = -1;
-    int first_best = -1;
-    bool found = false;
-    if (S.root_is_leaf) {
-        double t;
-        int s, f;
-        if (cluster_hit<SHADOW, STATS>(S, 0, o, d, tMin, tMax, __builtin_inf(), t, s, f, st)) {
-            t_best = t;
-            slot_best = s;
-            return true;
-        }
-        return false;
-    }
+                         Best& B, Stats& st) {
+    B = Best{tMax, -1, -1, false};
+    if (S.root_is_leaf) return leaf_hit<SHADOW, STATS>(S, 0, o, d, tMin, tMax, B, st) && (SHADOW || B.found);
     const RayF rf = make_rayf(o, d);
     float tlim = f_round_up(tMax);
     int sp = 0;
@@ -277,28 +335,16 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
             if (STATS) st.nodes++;
             node = node_step(S.nodes, node, rf, tlim, stack, sp);
         }
-        if (node == MFX_TRAV_EXIT) return found;
-        // ---- leaf: one reference leaf (cluster) ----
-        {
-            double t;
-            int s, f;
-            if (cluster_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, found ? t_best : __builtin_inf(), t, s, f,
-                                           st)) {
-                if (SHADOW) {
-                    t_best = t;
-                    slot_best = s;
-                    return true;
-                }
-                if (!found || t < t_best || (t == t_best && f > first_best)) {
-                    found = true;
-                    t_best = t;
-                    slot_best = s;
-                    first_best = f;
-                    tlim = f_round_up(t);
-                }
+        if (node == MFX_TRAV_EXIT) return B.found;
+        // ---- leaf ----
+        if (leaf_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, B, st)) {
+            if (SHADOW) {
+                B.found = true;
+                return true;
             }
+            tlim = f_round_up(B.t);
         }
-        if (sp == 0) return found;
+        if (sp == 0) return B.found;
         node = stack[(--sp) * 64];
     }
 }

@@ -31,6 +31,7 @@ struct WfParams {
     // scene
     const MfxNode* nodes;
     const uint8_t* blob;
+    const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* albedo;
     const MfxLight* light;

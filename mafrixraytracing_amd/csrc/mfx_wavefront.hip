@@ -98,11 +98,11 @@ struct Pend {
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
     DV o, d;
-    double tmax64, best_t;
+    double tmax64;
+    Best B;
     RayF rf;
     float tlim;
-    int node, sp, best_slot, best_first;
-    bool found;
+    int node, sp;
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
@@ -111,10 +111,7 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.tmax64 = tmax;
     T.rf = make_rayf(o, d);
     T.tlim = f_round_up(tmax);
-    T.best_t = tmax;
-    T.best_slot = -1;
-    T.best_first = -1;
-    T.found = false;
+    T.B = Best{tmax, -1, -1, false};
     T.sp = 0;
     T.node = S.root_is_leaf ? ~0 : 0;
 }
@@ -129,21 +126,12 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
         T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
     }
     if (T.node == MFX_TRAV_EXIT) return true;
-    double t;
-    int sl, f;
-    if (cluster_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.found ? T.best_t : __builtin_inf(), t,
-                                   sl, f, st)) {
+    if (leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st)) {
         if (SHADOW) {
-            T.found = true;
+            T.B.found = true;
             return true;
         }
-        if (!T.found || t < T.best_t || (t == T.best_t && f > T.best_first)) {
-            T.found = true;
-            T.best_t = t;
-            T.best_slot = sl;
-            T.best_first = f;
-            T.tlim = f_round_up(t);
-        }
+        T.tlim = f_round_up(T.B.t);
     }
     if (T.sp == 0) return true;
     T.node = stack[(--T.sp) * 64];
@@ -173,7 +161,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
     const Pend pd(pend_base + wave * WF_PEND_BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
-    const SceneView S{P.nodes, P.blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
     const int shard_size = P.pool / WF_SHARDS;
     const int W = P.width, H = P.height;
     const int tiles_x = (W + 7) >> 3;
@@ -288,11 +276,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         }
         if (!__any(active)) break;  // every chunk taken and every pending ray traced
         if (active && trav_step<false, STATS>(T, S, stack, st)) {
-            if (T.found) {
-                const DV hp = vadd(T.o, vmul(T.d, T.best_t));  // Ray.PointAtParameter (Ray.fs:8-9)
+            if (T.B.found) {
+                const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
                 P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
             }
-            P.hit_slot[s] = T.found ? T.best_slot : -1;
+            P.hit_slot[s] = T.B.found ? (T.B.info & MFX_INFO_SHADE_MASK) : -1;
             P.state[s] = WF_EXT_DONE;
             active = false;
         }
@@ -319,7 +307,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
     const Pend pd(pend_base + wave * WF_PEND_BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
-    const SceneView S{P.nodes, P.blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{0, 0, 0, false};
@@ -443,13 +431,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         if (!__any(active)) break;
         if (active && trav_step<true, STATS>(T, S, stack, st)) {
             double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
-            if (!T.found) {  // unoccluded: add this vertex's direct-light term
+            if (!T.B.found) {  // unoccluded: add this vertex's direct-light term
                 lx += scx;
                 ly += scy;
                 lz += scz;
             }
             if (cont) {
-                if (!T.found) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
+                if (!T.B.found) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
                 P.state[s] = WF_NEED_EXT;
             } else {
                 retire(P, s, lx, ly, lz);
