@@ -49,7 +49,8 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
-    uint8_t* d_blob = nullptr;
+    MfxSlot* d_slots = nullptr;
+    int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
     double* d_albedo = nullptr;
@@ -94,7 +95,7 @@ struct mfx_ctx {
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    void* bufs[] = {c->d_nodes, c->d_blob, c->d_ref_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -142,7 +143,7 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     c->part_index = opt->part_index;
     c->part_count = opt->part_count;
     c->npix = (int64_t)c->host.width * c->host.height;
-    c->stack_size = std::max(1, c->host.bvh_depth + 1);
+    c->stack_size = std::max(1, c->host.stack_entries);
     if (c->stack_size > 96) {
         free_ctx(c);
         return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
@@ -161,7 +162,8 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
-    CK(upload(&c->d_blob, c->host.blob));
+    CK(upload(&c->d_slots, c->host.slots));
+    CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
     CK(upload(&c->d_albedo, c->host.albedo));
@@ -232,7 +234,8 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
-    P.blob = c->d_blob;
+    P.slots = c->d_slots;
+    P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.albedo = c->d_albedo;
@@ -266,7 +269,6 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     base.width = W;
     base.height = H;
     base.max_depth = c->host.max_depth;
-    base.root_is_leaf = c->host.root_is_leaf;
     base.stack_size = c->stack_size;
     base.chunk = 256;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
@@ -369,7 +371,8 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
-    P.blob = c->d_blob;
+    P.slots = c->d_slots;
+    P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.albedo = c->d_albedo;
@@ -386,7 +389,6 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.width = c->host.width;
     P.height = c->host.height;
     P.max_depth = c->host.max_depth;
-    P.root_is_leaf = c->host.root_is_leaf;
     P.stack_size = c->stack_size;
     P.chunk = 256;
     HIPCHECK(hipEventRecord(c->ev0, c->stream));
@@ -557,7 +559,8 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         QueryParams Q;
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
-        Q.blob = c->d_blob;
+        Q.slots = c->d_slots;
+    Q.slot_ref = c->d_slot_ref;
         Q.ref_blob = c->d_ref_blob;
         Q.shade = c->d_shade;
         Q.rays = d_rays;
@@ -569,7 +572,6 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         Q.n = n;
         Q.tmin = tmin;
         Q.tmax = tmax;
-        Q.root_is_leaf = c->host.root_is_leaf;
         Q.stack_size = c->stack_size;
         e = mfx_launch_query(Q, shadow, c->stream);
     }
@@ -620,7 +622,7 @@ int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t*
         info_out[0] = s.nclusters;
         info_out[1] = (int32_t)s.nodes.size();
         info_out[2] = s.bvh_depth;
-        info_out[3] = s.root_is_leaf;
+        info_out[3] = (int32_t)s.slots.size();
     }
     return MFX_OK;
 }

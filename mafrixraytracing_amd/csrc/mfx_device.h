@@ -9,7 +9,8 @@
 
 struct TraceParams {
     const MfxNode* nodes;
-    const uint8_t* blob;
+    const MfxSlot* slots;
+    const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* albedo;
@@ -23,14 +24,14 @@ struct TraceParams {
     int64_t nsamples;                // samples this context renders per pixel in this call
     int32_t part_index, part_count;  // global sample = sample_base + part_index + s * part_count
     int32_t width, height, max_depth;
-    int32_t root_is_leaf;
     int32_t stack_size;              // LDS traversal stack entries per lane
     int32_t chunk;                   // path indices a wave takes per atomic
 };
 
 struct QueryParams {
     const MfxNode* nodes;
-    const uint8_t* blob;
+    const MfxSlot* slots;
+    const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* rays;
@@ -41,7 +42,6 @@ struct QueryParams {
     int32_t* occ_out;
     int64_t n;
     double tmin, tmax;
-    int32_t root_is_leaf;
     int32_t stack_size;
 };
 

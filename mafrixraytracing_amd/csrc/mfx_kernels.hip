@@ -32,7 +32,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const MfxLight& LT = *P.light;
     const MfxCamera& CAM = *P.cam;
     const int W = P.width, H = P.height;
@@ -226,7 +226,7 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.blob, Q.ref_blob, Q.root_is_leaf};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.blob, Q.ref_blob, Q.root_is_leaf};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};

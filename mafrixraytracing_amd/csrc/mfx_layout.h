@@ -1,16 +1,17 @@
 // mfx_layout.h — HBM data layout shared by the host builder (mfx_scene.cpp) and the gfx950
 // kernels. See DESIGN.md §2 for the layout rationale.
 //
-//   nodes[]     BVH2 over the individual primitives (binned SAH, leaves of <= 4 primitives),
-//               64 B per internal node with both child boxes stored in the parent (one node
-//               fetch = two FP32 slab tests). child >= 0 is an internal node index; child < 0 is
-//               ~(16-byte offset of a leaf record in blob[]). Boxes are the primitives' FP64
+//   nodes[]     BVH4 over the individual primitives (binned-SAH BVH2, leaves of <= 4 primitives,
+//               collapsed to 4-wide), 128 B per internal node with all child boxes stored in the
+//               parent (one node fetch = four FP32 slab tests). child >= 0 is an internal node
+//               index; child < 0 is ~(16-byte offset of a leaf record in blob[]). Boxes are the primitives' FP64
 //               boxes widened by eps and rounded outward (conservative: every primitive whose
 //               reference leaf the F#'s FP64 slab test accepts is reached).
-//   blob[]      traversal leaves in DFS order: a 16-B MfxTLeaf header, then the leaf's primitives'
-//               FP64 MfxSlot records (Triangle 1 slot, Rect 2, Sphere 1). Every slot names its
-//               reference leaf (`ref16`) and its position in it (`info`), which is all the exact
-//               semantics need (mfx_trace_common.h: leaf_hit).
+//   slots[]     traversal leaves in DFS order, each a run of 128-B FP64 MfxSlot records (Triangle 1
+//               slot, Rect 2, Sphere 1). Every slot carries its reference leaf's FP64 box, `first`
+//               and its position in it, which is all the exact semantics need
+//               (mfx_trace_common.h: leaf_hit); slot_ref[] names the reference leaf record for
+//               the rare whole-leaf evaluation.
 //   ref_blob[]  one record per leaf of the reference's heap BVH (BvhNode.fs:36-39, count <= 3): a
 //               64-B MfxLeaf header (its exact FP64 box, InitNode BvhNode.fs:32-37; its position in
 //               `indices`) followed by copies of its primitives' slots. Read for the FP64 leaf-box
@@ -26,12 +27,12 @@
 #define MFX_KIND_RECT 1
 #define MFX_KIND_SPHERE 2
 
-struct alignas(16) MfxNode {
-    float c0lox, c0hix, c0loy, c0hiy;  // child 0 box x,y
-    float c1lox, c1hix, c1loy, c1hiy;  // child 1 box x,y
-    float c0loz, c0hiz, c1loz, c1hiz;  // both z
-    int32_t child0, child1, pad0, pad1;
+struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache line)
+    float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+    int32_t child[4];  // >= 0 node index, < 0 ~(leaf code), MFX_CHILD_EMPTY (box lo = hi = FLT_MAX: never hit)
+    int32_t pad[4];
 };
+#define MFX_CHILD_EMPTY (-0x7fffffff - 1)
 
 // reference leaf header (ref_blob[]); copies of its primitives' slots follow
 struct alignas(16) MfxLeaf {
@@ -43,23 +44,28 @@ struct alignas(16) MfxLeaf {
     int32_t pad;
 };
 
-#define MFX_INFO_SHADE_MASK 0x0fffffff  // MfxSlot.info: shade[] index | position in its reference leaf << 28
-#define MFX_INFO_POS_SHIFT 28
+// MfxSlot.info: shade[] index | position in its reference leaf | kind | second triangle of a rect
+#define MFX_INFO_SHADE_MASK 0x03ffffff
+#define MFX_INFO_POS_SHIFT 26
+#define MFX_INFO_KIND_SHIFT 28
+#define MFX_INFO_RECT2 (1 << 30)
 
+// One traversal slot, 128 B (one cache line): the geometry the exact FP64 test reads, then what a
+// winning candidate needs — its reference leaf's FP64 box and `first` — so a leaf visit is one
+// round of independent loads. A leaf is a run of consecutive slots; the node's child code says
+// where it starts and how many slots it has.
 struct alignas(16) MfxSlot {
-    double a[3];   // tri: v0      sphere: center
-    double b[3];   // tri: e1      sphere: {radius, 0, 0}
-    double c[3];   // tri: e2
-    int32_t ref16;  // 16-byte offset of the primitive's reference leaf in ref_blob[]
-    int32_t info;   // shade[] index of this slot | (position of the primitive in its reference leaf) << 28
+    double a[3];    // tri: v0      sphere: center
+    double b[3];    // tri: e1      sphere: {radius, 0, 0}
+    double c[3];    // tri: e2
+    double lo[3];   // FP64 box of the primitive's reference leaf (InitNode, BvhNode.fs:32-37)
+    double hi[3];
+    int32_t first;  // MfxLeaf.first of that reference leaf
+    int32_t info;   // MFX_INFO_* fields
 };
 
-// traversal leaf header (blob[]); the slots follow
-struct alignas(16) MfxTLeaf {
-    int32_t count;  // primitives, 1..4
-    int32_t kinds;  // 2 bits per primitive
-    int32_t pad0, pad1;
-};
+// leaf child code: ~((first slot << 3) | (slots - 1)), at most 8 slots (4 primitives, rects take 2)
+#define MFX_LEAF_SLOTS_MAX 8
 
 struct alignas(16) MfxShade {
     double n[3];        // face normal of this triangle slot; a sphere's centre

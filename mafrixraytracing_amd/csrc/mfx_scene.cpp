@@ -7,8 +7,8 @@
 //    is hit beyond tMax (Triangle.Hit ignores tMax, Trangle.fs:148; the leaf minBy, :76-80).
 //    Its median split sorts with F#'s Array.sortInPlaceBy = .NET 6 introsort, restated here so
 //    ties fall the same way.
-// 3. A binned-SAH BVH2 over the individual primitives is what the GPU traverses, in FP32 with
-//    conservatively widened boxes. Every primitive slot carries its reference leaf and position,
+// 3. A binned-SAH BVH2 over the individual primitives, collapsed to a BVH4, is what the GPU
+//    traverses, in FP32 with conservatively widened boxes. Every primitive slot carries its reference leaf and position,
 //    so the reference's leaf semantics are applied exactly per candidate hit.
 #include "mfx_scene.h"
 
@@ -214,19 +214,24 @@ struct FBox {
     }
 };
 
+struct Node2 {  // binned-SAH BVH2 node (host only; collapsed to MfxNode BVH4 for the device)
+    FBox box[2];
+    int32_t child[2];
+};
+
 struct SahBuilder {
     std::vector<FBox> cb;       // item boxes (conservative FP32)
     std::vector<float> cent;    // centroids [3*n]
     std::vector<float> weight;  // intersection cost of an item (slots it tests)
     std::vector<int32_t> ids;   // permutation being partitioned
     std::vector<std::pair<int, int>> leaves;  // [b, e) ranges of ids, in creation order
-    std::vector<MfxNode>& nodes;
+    std::vector<Node2>& nodes;
     int max_depth = 0;
     int max_leaf = 4;
     float c_isect = 1.5f;  // cost of one primitive slot test relative to one node step
     static constexpr int NB = 32;
 
-    explicit SahBuilder(std::vector<MfxNode>& n) : nodes(n) {}
+    explicit SahBuilder(std::vector<Node2>& n) : nodes(n) {}
 
     int make_leaf(int b, int e, FBox& out) {
         out = FBox::empty();
@@ -312,19 +317,83 @@ struct SahBuilder {
             if (mid == b || mid == e) mid = (b + e) / 2;
         }
         int self = (int)nodes.size();
-        nodes.push_back(MfxNode{});
+        nodes.push_back(Node2{});
         FBox lb, rb;
         int l = build(b, mid, depth + 1, lb);
         int r = build(mid, e, depth + 1, rb);
-        MfxNode& nd = nodes[self];
-        nd.c0lox = lb.lo[0]; nd.c0hix = lb.hi[0]; nd.c0loy = lb.lo[1]; nd.c0hiy = lb.hi[1];
-        nd.c1lox = rb.lo[0]; nd.c1hix = rb.hi[0]; nd.c1loy = rb.lo[1]; nd.c1hiy = rb.hi[1];
-        nd.c0loz = lb.lo[2]; nd.c0hiz = lb.hi[2]; nd.c1loz = rb.lo[2]; nd.c1hiz = rb.hi[2];
-        nd.child0 = l;
-        nd.child1 = r;
-        nd.pad0 = nd.pad1 = 0;
+        Node2& nd = nodes[self];
+        nd.box[0] = lb;
+        nd.box[1] = rb;
+        nd.child[0] = l;
+        nd.child[1] = r;
         out = lb;
         out.grow(rb);
+        return self;
+    }
+};
+
+// BVH2 -> BVH4: a node adopts the children of its largest-area internal child until it has four
+// (Wald et al. 2008 style collapse). Preorder output; records the depth and the stack bound
+// (max over nodes of the pushes its ancestors can leave on the stack, plus the 3-slot window
+// node_step writes unconditionally).
+struct Collapse4 {
+    const std::vector<Node2>& n2;
+    std::vector<MfxNode>& out;
+    int max_depth = 0, max_stack = 0;
+
+    int run(int ref, int depth, int pushed, const FBox* leaf_box = nullptr) {
+        if (ref < 0 && depth > 0) return ref;
+        max_depth = std::max(max_depth, depth);
+        int ch[4];
+        FBox bx[4];
+        int nc = 2;
+        if (ref < 0) {  // the whole scene is one leaf: a root node with one child
+            nc = 1;
+            ch[0] = ref;
+            bx[0] = *leaf_box;
+        } else {
+            for (int k = 0; k < 2; ++k) {
+                ch[k] = n2[ref].child[k];
+                bx[k] = n2[ref].box[k];
+            }
+        }
+        while (nc > 1 && nc < 4) {
+            int best = -1;
+            float ba = -1.f;
+            for (int k = 0; k < nc; ++k)
+                if (ch[k] >= 0 && bx[k].area() > ba) {
+                    ba = bx[k].area();
+                    best = k;
+                }
+            if (best < 0) break;
+            const Node2& m = n2[ch[best]];
+            for (int k = nc; k > best + 1; --k) {  // children of `best` replace it in place
+                ch[k] = ch[k - 1];
+                bx[k] = bx[k - 1];
+            }
+            ch[best] = m.child[0];
+            bx[best] = m.box[0];
+            ch[best + 1] = m.child[1];
+            bx[best + 1] = m.box[1];
+            ++nc;
+        }
+        max_stack = std::max(max_stack, pushed + 3);
+        const int self = (int)out.size();
+        out.push_back(MfxNode{});
+        int ref4[4];
+        for (int k = 0; k < nc; ++k) ref4[k] = run(ch[k], depth + 1, pushed + nc - 1);
+        MfxNode& nd = out[self];
+        for (int k = 0; k < 4; ++k) {
+            const bool v = k < nc;
+            nd.lox[k] = v ? bx[k].lo[0] : FLT_MAX;
+            nd.hix[k] = v ? bx[k].hi[0] : FLT_MAX;
+            nd.loy[k] = v ? bx[k].lo[1] : FLT_MAX;
+            nd.hiy[k] = v ? bx[k].hi[1] : FLT_MAX;
+            nd.loz[k] = v ? bx[k].lo[2] : FLT_MAX;
+            nd.hiz[k] = v ? bx[k].hi[2] : FLT_MAX;
+            nd.child[k] = v ? ref4[k] : MFX_CHILD_EMPTY;
+            nd.pad[k] = 0;
+        }
         return self;
     }
 };
@@ -497,8 +566,8 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             for (int a = 0; a < 3; ++a) R = std::max(R, std::fabs(d->light.p[k][a]));
     }
     s.eps = (float)std::ldexp(R + T, -19);
-    s.nodes.clear();
-    SahBuilder sb(s.nodes);
+    std::vector<Node2> nodes2;
+    SahBuilder sb(nodes2);
     if (const char* e = getenv("MFX_LEAF_MAX")) sb.max_leaf = std::max(1, std::min(4, atoi(e)));
     if (const char* e = getenv("MFX_SAH_CI")) sb.c_isect = (float)atof(e);
     sb.cb.resize(n);
@@ -518,9 +587,12 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         sb.ids[i] = i;
     }
     FBox rootbox;
-    const int root = sb.build(0, n, 0, rootbox);
-    s.root_is_leaf = root < 0 ? 1 : 0;
-    s.bvh_depth = root < 0 ? 0 : sb.max_depth;
+    const int root2 = sb.build(0, n, 0, rootbox);
+    s.nodes.clear();
+    Collapse4 c4{nodes2, s.nodes};
+    const int root = c4.run(root2, 0, 0, &rootbox);  // always an internal node (a lone leaf gets a parent)
+    s.bvh_depth = c4.max_depth;
+    s.stack_entries = std::max(1, c4.max_stack);
     const int nl = (int)sb.leaves.size();
 
     // ---- where each primitive sits in the reference grouping --------------------------------
@@ -544,55 +616,60 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         }
     }
 
-    // ---- traversal leaves in depth-first order; child refs become ~(16-byte offset) --------
+    // ---- traversal leaves in depth-first order: runs of slots; child refs become leaf codes ---
     std::vector<int> order;
     order.reserve(nl);
     {
-        std::vector<int> st{root};  // depth-first, child0 before child1
+        std::vector<int> st{root};  // depth-first, children in order
         while (!st.empty()) {
             const int ref = st.back();
             st.pop_back();
             if (ref < 0) {
                 order.push_back(~ref);
             } else {
-                st.push_back(s.nodes[ref].child1);
-                st.push_back(s.nodes[ref].child0);
+                for (int k = 3; k >= 0; --k)
+                    if (s.nodes[ref].child[k] != MFX_CHILD_EMPTY) st.push_back(s.nodes[ref].child[k]);
             }
         }
     }
-    std::vector<int32_t> offset16(nl), shade_of(n);
-    s.blob.clear();
+    std::vector<int32_t> code_of(nl), shade_of(n);
+    s.slots.clear();
+    s.slot_ref.clear();
     s.shade.clear();
     for (int l : order) {
         const int b = sb.leaves[l].first, e = sb.leaves[l].second;
-        MfxTLeaf h{};
-        h.count = e - b;
-        for (int k = 0; k < h.count; ++k) h.kinds |= d->prims[sb.ids[b + k]].kind << (2 * k);
-        offset16[l] = (int32_t)(s.blob.size() / 16);
-        const uint8_t* hp = (const uint8_t*)&h;
-        s.blob.insert(s.blob.end(), hp, hp + sizeof(MfxTLeaf));
-        for (int k = 0; k < h.count; ++k) {
-            const int p = sb.ids[b + k];
+        const int s0 = (int)s.slots.size();
+        for (int k = b; k < e; ++k) {
+            const int p = sb.ids[k];
+            const MfxLeaf& rl = leaves[ref_leaf_of[p]];
             shade_of[p] = (int32_t)s.shade.size();
             for (int j = 0; j < nslot_of[p]; ++j) {
                 MfxSlot sl = pslots[slot_of[p] + j];
-                sl.ref16 = ref16[ref_leaf_of[p]];
-                sl.info = (int32_t)s.shade.size() | (pos_of[p] << MFX_INFO_POS_SHIFT);
-                const uint8_t* sp = (const uint8_t*)&sl;
-                s.blob.insert(s.blob.end(), sp, sp + sizeof(MfxSlot));
+                std::memcpy(sl.lo, rl.lo, sizeof(sl.lo));
+                std::memcpy(sl.hi, rl.hi, sizeof(sl.hi));
+                sl.first = rl.first;
+                sl.info = (int32_t)s.shade.size() | (pos_of[p] << MFX_INFO_POS_SHIFT) |
+                          (d->prims[p].kind << MFX_INFO_KIND_SHIFT) | (j == 1 ? MFX_INFO_RECT2 : 0);
+                s.slots.push_back(sl);
+                s.slot_ref.push_back(ref16[ref_leaf_of[p]]);
                 s.shade.push_back(pshade[slot_of[p] + j]);
             }
         }
+        const int ns = (int)s.slots.size() - s0;
+        if (ns > MFX_LEAF_SLOTS_MAX || s0 >= (1 << 28)) {
+            err = "scene too large for the traversal image";
+            return false;
+        }
+        code_of[l] = (s0 << 3) | (ns - 1);
     }
-    if (s.blob.size() / 16 >= (size_t)0x7fffffff || s.shade.size() > MFX_INFO_SHADE_MASK) {
+    if (s.shade.size() > MFX_INFO_SHADE_MASK) {
         err = "scene too large for the traversal image";
         return false;
     }
-    s.blob.resize(s.blob.size() + 3 * sizeof(MfxSlot), 0);  // speculative slot loads stay in bounds
-    for (MfxNode& nd : s.nodes) {
-        if (nd.child0 < 0) nd.child0 = ~offset16[~nd.child0];
-        if (nd.child1 < 0) nd.child1 = ~offset16[~nd.child1];
-    }
+    s.slots.resize(s.slots.size() + MFX_LEAF_SLOTS_MAX, MfxSlot{});  // speculative slot loads stay in bounds
+    for (MfxNode& nd : s.nodes)
+        for (int k = 0; k < 4; ++k)
+            if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~code_of[~nd.child[k]];
 
     // ---- reference leaves (heap order): FP64 box header + slot copies ----------------------
     s.ref_blob.clear();
@@ -603,7 +680,9 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             const int p = s.ref_indices[leaves[c].first + k];
             for (int j = 0; j < nslot_of[p]; ++j) {
                 MfxSlot sl = pslots[slot_of[p] + j];
-                sl.ref16 = ref16[c];
+                std::memcpy(sl.lo, leaves[c].lo, sizeof(sl.lo));
+                std::memcpy(sl.hi, leaves[c].hi, sizeof(sl.hi));
+                sl.first = leaves[c].first;
                 sl.info = (shade_of[p] + j) | (k << MFX_INFO_POS_SHIFT);
                 const uint8_t* sp = (const uint8_t*)&sl;
                 s.ref_blob.insert(s.ref_blob.end(), sp, sp + sizeof(MfxSlot));

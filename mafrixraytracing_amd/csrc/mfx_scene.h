@@ -13,18 +13,19 @@ struct MfxHostScene {
     std::vector<int32_t> ref_indices;                  // `indices` after Subdivide
     std::vector<int32_t> leaf_first, leaf_count;       // leaves in heap (DFS) order
     // device images
-    std::vector<MfxNode> nodes;     // BVH2 over primitives
-    std::vector<uint8_t> blob;      // traversal leaves: MfxTLeaf headers + MfxSlot records, DFS order
+    std::vector<MfxNode> nodes;     // BVH4 over primitives (preorder)
+    std::vector<MfxSlot> slots;     // traversal leaves: runs of MfxSlot records, DFS order
+    std::vector<int32_t> slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     std::vector<uint8_t> ref_blob;  // reference leaves: MfxLeaf headers + slot copies, heap order
-    std::vector<MfxShade> shade;    // per traversal slot, in blob order
+    std::vector<MfxShade> shade;    // per traversal slot, in slots[] order
     int32_t nclusters = 0;          // reference leaves
     int32_t ntleaves = 0;           // traversal leaves
     std::vector<double> albedo;  // [nmat][3]
     MfxLight light;
     MfxCamera camera;
     int32_t width = 0, height = 0, max_depth = 3;
-    int32_t root_is_leaf = 0;  // 1 => a single cluster, no internal nodes
-    int32_t bvh_depth = 0;     // longest root-to-leaf path in nodes[] (traversal stack bound)
+    int32_t bvh_depth = 0;     // longest root-to-leaf path in nodes[]
+    int32_t stack_entries = 1; // traversal stack bound: pushes along any path + the 3-slot write window
     float eps = 0.f;           // conservative box widening
 };
 

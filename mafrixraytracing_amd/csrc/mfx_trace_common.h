@@ -53,6 +53,11 @@ __device__ __forceinline__ uint64_t path_key(uint64_t seed, uint64_t pixel, uint
 }
 __device__ __forceinline__ double rng_next(uint64_t key, uint32_t& n) {
     n += 1;
+#ifdef MFX_DIAG_CHEAP_RNG
+    uint32_t h = (uint32_t)key ^ (uint32_t)(key >> 32) ^ (n * 0x9e3779b9u);
+    h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
+    return (double)h * (1.0 / 4294967296.0);
+#endif
     uint64_t z = mix64(key + (uint64_t)n * 0x9e3779b97f4a7c15ULL);
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
@@ -115,9 +120,9 @@ __device__ __forceinline__ bool sphere_hit64(const MfxSlot& s, DV o, DV d, doubl
 
 struct SceneView {
     const MfxNode* __restrict__ nodes;
-    const uint8_t* __restrict__ blob;      // traversal leaves: MfxTLeaf + MfxSlot records
+    const MfxSlot* __restrict__ slots;     // traversal leaves: runs of MfxSlot records
+    const int32_t* __restrict__ slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
-    int32_t root_is_leaf;
 };
 
 struct Stats {
@@ -136,7 +141,7 @@ struct Best {
 __device__ __forceinline__ bool beats(const Best& B, double t, int first, int info) {
     if (!B.found || t < B.t) return true;
     if (t > B.t) return false;
-    const unsigned pos = (unsigned)info >> MFX_INFO_POS_SHIFT, bpos = (unsigned)B.info >> MFX_INFO_POS_SHIFT;
+    const unsigned pos = ((unsigned)info >> MFX_INFO_POS_SHIFT) & 3u, bpos = ((unsigned)B.info >> MFX_INFO_POS_SHIFT) & 3u;
     return first > B.first || (first == B.first && pos < bpos);
 }
 
@@ -193,51 +198,48 @@ __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV
     return true;
 }
 
-// One traversal leaf (1..4 primitives of possibly different reference leaves). Each primitive
-// hit is a candidate for its reference leaf's result: with t < tMax the reference leaf's minBy
-// result is a hit of t no larger (the leaf's other primitives are tested in their own traversal
-// leaves), so the candidate counts iff it beats the best hit under the reference's order and its
-// reference leaf passes the exact FP64 box test (ancestor boxes contain it, and the rounded slab
-// test is monotone in the bounds, so they pass too). A hit at t >= tMax (Triangle.Hit ignores
+// One traversal leaf (1..4 primitives of possibly different reference leaves; child code = first
+// slot << 3 | slots - 1). Each primitive hit is a candidate for its reference leaf's result: with
+// t < tMax the reference leaf's minBy result is a hit of t no larger (the leaf's other primitives
+// are tested in their own traversal leaves), so the candidate counts iff it beats the best hit
+// under the reference's order and its reference leaf passes the exact FP64 box test (ancestor
+// boxes contain it, and the rounded slab test is monotone in the bounds, so they pass too). Both
+// the box and `first` sit in the slot's own cache line. A hit at t >= tMax (Triangle.Hit ignores
 // tMax, Trangle.fs:148) is where the leaf's minBy can prefer a miss: that reference leaf is then
 // evaluated whole. SHADOW: returns true at the first occluding candidate. Closest: returns true
 // when B improved.
 template <bool SHADOW, bool STATS>
-__device__ __forceinline__ bool leaf_hit(const SceneView& S, int off16, DV o, DV d, double tMin, double tMax,
+__device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
                                          Best& B, Stats& st) {
-    const uint8_t* base = S.blob + (size_t)off16 * 16;
-    const MfxTLeaf h = *(const MfxTLeaf*)base;
-    const MfxSlot* __restrict__ sl = (const MfxSlot*)(base + sizeof(MfxTLeaf));
+    const int s0 = code >> 3, n = (code & 7) + 1;
+    const MfxSlot* __restrict__ sl = S.slots + s0;
     if (STATS) st.clusters++;
     bool improved = false;
-    int cur = 0;
-    for (int k = 0; k < h.count; ++k) {
-        const int kind = (h.kinds >> (2 * k)) & 3;
+    for (int k = 0; k < n; ++k) {
+        int info = sl[k].info;
+        const int kind = (info >> MFX_INFO_KIND_SHIFT) & 3;
         if (STATS) st.prims++;
         double t = 0.0;
-        int hs = cur;
+        int hs = k;
         bool hit;
         if (kind == MFX_KIND_SPHERE) {
-            hit = sphere_hit64(sl[cur], o, d, tMin, tMax, t);
-            cur += 1;
+            hit = sphere_hit64(sl[k], o, d, tMin, tMax, t);
         } else {
-            hit = tri_hit64(sl[cur], o, d, tMin, t);
+            hit = tri_hit64(sl[k], o, d, tMin, t);
             if (kind == MFX_KIND_RECT) {
-                if (!hit) {  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31)
-                    hs = cur + 1;
-                    hit = tri_hit64(sl[cur + 1], o, d, tMin, t);
+                ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
+                if (!hit) {
+                    hs = k;
+                    hit = tri_hit64(sl[k], o, d, tMin, t);
+                    info = sl[k].info;
                 }
-                cur += 2;
-            } else {
-                cur += 1;
             }
         }
         if (!hit) continue;
-        const int ref16 = sl[hs].ref16;
         if (t >= tMax) {
             double t2;
             int info2, first2;
-            if (ref_leaf_hit<SHADOW>(S.ref_blob, ref16, o, d, tMin, tMax, t2, info2, first2)) {
+            if (ref_leaf_hit<SHADOW>(S.ref_blob, S.slot_ref[s0 + hs], o, d, tMin, tMax, t2, info2, first2)) {
                 if (SHADOW) return true;
                 if (beats(B, t2, first2, info2)) {
                     B = Best{t2, info2, first2, true};
@@ -246,12 +248,10 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int off16, DV o, DV
             }
             continue;
         }
-        const int info = sl[hs].info;
         if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
-        const MfxLeaf* __restrict__ rl = (const MfxLeaf*)(S.ref_blob + (size_t)ref16 * 16);
-        const int first = rl->first;
+        const int first = sl[hs].first;
         if (!SHADOW && !beats(B, t, first, info)) continue;
-        if (!aabb_hit64(rl->lo, rl->hi, o, d, tMin, tMax)) continue;
+        if (!aabb_hit64(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
         if (SHADOW) return true;
         B = Best{t, info, first, true};
         improved = true;
@@ -284,39 +284,61 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
 
-// One internal-node step of the cluster BVH2, branch-free: both child slab tests, then
-// near-first descent / push of the far child / pop, chosen with selects. The far child is
-// written to the stack slot unconditionally and sp only advances when both children are hit;
-// the pop candidate (top of stack) is read before the node's boxes arrive, so the LDS read
-// overlaps the HBM/L2 load. Returns the next node: >= 0 internal, < 0 a leaf (~offset), or
-// MFX_TRAV_EXIT when nothing is left.
+// One internal-node step of the BVH4, branch-free: four child slab tests, the hit children sorted
+// near to far (5-comparator network over (entry distance, child), misses sorted last at +inf),
+// then descend into the nearest, push the others far-first, or pop. The push window
+// stack[sp .. sp+2] is written unconditionally and sp advances by (hits - 1), so only the pushed
+// entries survive; the pop candidate (top of stack) is read before the node's boxes arrive, so
+// the LDS read overlaps the L2 load. Returns the next node: >= 0 internal, < 0 a leaf (~offset),
+// or MFX_TRAV_EXIT when nothing is left. An empty child (box at FLT_MAX) never hits.
+__device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
+    const bool s = db < da;
+    const float t = da;
+    const int u = ca;
+    da = s ? db : da;
+    ca = s ? cb : ca;
+    db = s ? t : db;
+    cb = s ? u : cb;
+}
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          int* __restrict__ stack, int& sp) {
     const int top = stack[(sp > 0 ? sp - 1 : 0) * 64];
-    const MfxNode nd = nodes[node];
-    float a0 = fmaf(nd.c0lox, r.ix, -r.oix), a1 = fmaf(nd.c0hix, r.ix, -r.oix);
-    float b0 = fmaf(nd.c0loy, r.iy, -r.oiy), b1 = fmaf(nd.c0hiy, r.iy, -r.oiy);
-    float c0 = fmaf(nd.c0loz, r.iz, -r.oiz), c1 = fmaf(nd.c0hiz, r.iz, -r.oiz);
-    const float n0 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-    const float f0 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-    a0 = fmaf(nd.c1lox, r.ix, -r.oix); a1 = fmaf(nd.c1hix, r.ix, -r.oix);
-    b0 = fmaf(nd.c1loy, r.iy, -r.oiy); b1 = fmaf(nd.c1hiy, r.iy, -r.oiy);
-    c0 = fmaf(nd.c1loz, r.iz, -r.oiz); c1 = fmaf(nd.c1hiz, r.iz, -r.oiz);
-    const float n1 = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-    const float f1 = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-    const bool h0 = n0 <= f0, h1 = n1 <= f1;
-    const bool both = h0 && h1;
-    const bool take1 = h1 && (!h0 || n1 < n0);  // child 1 is the one to descend into
-    const int near = take1 ? nd.child1 : nd.child0;
-    const int far = take1 ? nd.child0 : nd.child1;
-    stack[sp * 64] = far;  // kept only if sp advances
-    const bool any = h0 || h1;
-    const bool pop = !any && sp > 0;
-    sp += (both ? 1 : 0) - (pop ? 1 : 0);
-    return any ? near : (pop ? top : MFX_TRAV_EXIT);
+    const float4* __restrict__ q = (const float4*)(nodes + node);
+    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+    const int4 ch = *(const int4*)(q + 6);
+    float d[4];
+    int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    int nh = 0;
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float a0 = fmaf(LX[k], r.ix, -r.oix), a1 = fmaf(HX[k], r.ix, -r.oix);
+        const float b0 = fmaf(LY[k], r.iy, -r.oiy), b1 = fmaf(HY[k], r.iy, -r.oiy);
+        const float c0 = fmaf(LZ[k], r.iz, -r.oiz), c1 = fmaf(HZ[k], r.iz, -r.oiz);
+        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+        const bool h = n <= f;
+        d[k] = h ? n : __builtin_inff();
+        nh += h ? 1 : 0;
+    }
+    cswap(d[0], c[0], d[1], c[1]);
+    cswap(d[2], c[2], d[3], c[3]);
+    cswap(d[0], c[0], d[2], c[2]);
+    cswap(d[1], c[1], d[3], c[3]);
+    cswap(d[1], c[1], d[2], c[2]);
+    // far-first pushes: stack[sp + j] = c[nh - 1 - j] for j < nh - 1
+    stack[sp * 64] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
+    stack[(sp + 1) * 64] = nh == 4 ? c[2] : c[1];
+    stack[(sp + 2) * 64] = c[1];
+    const bool pop = nh == 0 && sp > 0;
+    const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
+    sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
+    return next;
 }
 
-// Bvh.Hit over the primitive BVH2 (megakernel and query kernels). SHADOW: returns occluded
+// Bvh.Hit over the primitive BVH4 (megakernel and query kernels). SHADOW: returns occluded
 // (the reference's combine returns a hit iff some visited leaf does). Otherwise: the closest hit
 // under the reference's order (Best). The stack lives in LDS, one column per lane (stride 64
 // dwords: conflict-free).
@@ -324,7 +346,6 @@ template <bool SHADOW, bool STATS>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
                          Best& B, Stats& st) {
     B = Best{tMax, -1, -1, false};
-    if (S.root_is_leaf) return leaf_hit<SHADOW, STATS>(S, 0, o, d, tMin, tMax, B, st) && (SHADOW || B.found);
     const RayF rf = make_rayf(o, d);
     float tlim = f_round_up(tMax);
     int sp = 0;

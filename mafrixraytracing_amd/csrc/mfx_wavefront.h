@@ -30,7 +30,8 @@
 struct WfParams {
     // scene
     const MfxNode* nodes;
-    const uint8_t* blob;
+    const MfxSlot* slots;
+    const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const double* albedo;
@@ -58,7 +59,6 @@ struct WfParams {
     int32_t part_index, part_count;
     int32_t pool;
     int32_t width, height, max_depth;
-    int32_t root_is_leaf;
     int32_t stack_size;
     int32_t chunk;                        // slots per chunk fetch of the kernels
 };

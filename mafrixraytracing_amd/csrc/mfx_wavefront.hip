@@ -31,6 +31,28 @@
 #endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
+
+#ifndef MFX_DIAG_STAMPS
+#define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow
+#endif
+struct DiagAcc {
+    uint64_t fetch, node, leaf, fin, last;
+};
+__device__ __forceinline__ uint64_t stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define DIAG_MARK(acc, field, on)              \
+    do {                                       \
+        if (on) {                              \
+            const uint64_t _t = stamp();       \
+            (acc).field += _t - (acc).last;    \
+            (acc).last = _t;                   \
+        }                                      \
+    } while (0)
 __device__ __forceinline__ uint64_t lanes_below() { return (1ULL << lane_id()) - 1ULL; }
 
 __device__ __forceinline__ void wave_lds_sync() {
@@ -113,18 +135,20 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.tlim = f_round_up(tmax);
     T.B = Best{tmax, -1, -1, false};
     T.sp = 0;
-    T.node = S.root_is_leaf ? ~0 : 0;
+    T.node = 0;
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
 template <bool SHADOW, bool STATS>
-__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __restrict__ stack, Stats& st) {
+__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __restrict__ stack, Stats& st,
+                                          DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
         T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
     }
+    DIAG_MARK(dg, node, diag);
     if (T.node == MFX_TRAV_EXIT) return true;
     if (leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st)) {
         if (SHADOW) {
@@ -161,7 +185,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
     const Pend pd(pend_base + wave * WF_PEND_BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
-    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
     const int W = P.width, H = P.height;
     const int tiles_x = (W + 7) >> 3;
@@ -175,6 +199,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     Trav T{};
     uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
+    constexpr bool DG = MFX_DIAG_STAMPS == 1;
+    DiagAcc dg{0, 0, 0, 0, 0};
+    if (DG) dg.last = stamp();
 
     while (true) {
         // ---- dynamic fetch: idle lanes take pending rays by rank ----
@@ -275,7 +302,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             m = __ballot(idle);
         }
         if (!__any(active)) break;  // every chunk taken and every pending ray traced
-        if (active && trav_step<false, STATS>(T, S, stack, st)) {
+        DIAG_MARK(dg, fetch, DG);
+        bool fin = false;
+        if (active) fin = trav_step<false, STATS>(T, S, stack, st, dg, DG);
+        DIAG_MARK(dg, leaf, DG);
+        if (fin) {
             if (T.B.found) {
                 const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
                 P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
@@ -284,10 +315,17 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             P.state[s] = WF_EXT_DONE;
             active = false;
         }
+        DIAG_MARK(dg, fin, DG);
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 0, c_primary, red);
     block_add<4>(cnt + 1, c_ext, red);
+    if (DG && lane == 0) {
+        atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
+        atomicAdd(cnt + 11, (unsigned long long)dg.node);
+        atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
+        atomicAdd(cnt + 13, (unsigned long long)dg.fin);
+    }
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
         block_add<4>(cnt + 5, st.clusters, red);
@@ -307,7 +345,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
     const Pend pd(pend_base + wave * WF_PEND_BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
-    const SceneView S{P.nodes, P.blob, P.ref_blob, P.root_is_leaf};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{0, 0, 0, false};
@@ -319,6 +357,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     bool cont = false;                        // the path continues after this vertex
     uint32_t c_shadow = 0;
     Stats st{0, 0, 0};
+    constexpr bool DG = MFX_DIAG_STAMPS == 2;
+    DiagAcc dg{0, 0, 0, 0, 0};
+    if (DG) dg.last = stamp();
 
     while (true) {
         bool idle = !active;
@@ -429,7 +470,18 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
             m = __ballot(idle);
         }
         if (!__any(active)) break;
-        if (active && trav_step<true, STATS>(T, S, stack, st)) {
+        DIAG_MARK(dg, fetch, DG);
+        bool fin = false;
+#ifdef MFX_DIAG_SKIP_SHADOW_TRAV
+        if (active) {
+            T.B.found = false;
+            fin = true;
+        }
+#else
+        if (active) fin = trav_step<true, STATS>(T, S, stack, st, dg, DG);
+#endif
+        DIAG_MARK(dg, leaf, DG);
+        if (fin) {
             double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
             if (!T.B.found) {  // unoccluded: add this vertex's direct-light term
                 lx += scx;
@@ -444,9 +496,16 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
             }
             active = false;
         }
+        DIAG_MARK(dg, fin, DG);
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
+    if (DG && lane == 0) {
+        atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
+        atomicAdd(cnt + 11, (unsigned long long)dg.node);
+        atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
+        atomicAdd(cnt + 13, (unsigned long long)dg.fin);
+    }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);
         block_add<4>(cnt + 8, st.clusters, red);

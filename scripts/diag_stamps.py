@@ -1,0 +1,21 @@
+#!/usr/bin/env python3
+"""Phase shares of the wavefront kernels from a stamp build (-DMFX_DIAG_STAMPS=1 k_extend, =2
+k_shadow): wave-cycles spent in fetch/scan, node steps, leaf tests and result writes.
+Usage: diag_stamps.py LIB.so [SCENE] [SPP]"""
+import os, sys, json
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import mafrixraytracing_amd.abi as abi
+lib = sys.argv[1]
+abi._lib = abi.load_library(lib)
+from mafrixraytracing_amd.native import NativeContext, DEFAULT_SEED
+from mafrixraytracing_amd.scene_io import load_scene_file
+scene = sys.argv[2] if len(sys.argv) > 2 else os.path.join(ROOT, "scenes", "spot.xml")
+spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64
+ctx = NativeContext(load_scene_file(scene), seed=DEFAULT_SEED)
+ctx.accum_clear(); ctx.trace_accumulate(spp, 0); ctx.sync()
+c = ctx.ray_counts()
+ph = dict(zip(["fetch", "node", "leaf", "fin"], c[10:14]))
+tot = sum(ph.values())
+print(os.path.basename(lib), json.dumps({k: round(v / tot, 4) for k, v in ph.items()}), "total wave-cycles %.4g" % tot,
+      json.dumps(ctx.trace_timing()))
