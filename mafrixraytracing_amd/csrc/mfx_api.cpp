@@ -53,9 +53,6 @@ struct mfx_ctx {
     int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
-    double* d_albedo = nullptr;
-    MfxLight* d_light = nullptr;
-    MfxCamera* d_cam = nullptr;
     double* d_accum = nullptr;   // [3][npix] (the active accumulator)
     double* d_accum_own = nullptr;
     double* d_film = nullptr;    // [3][npix]
@@ -90,12 +87,13 @@ struct mfx_ctx {
     int launches = 0;    // launches per stage kernel, all sub-pools
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
+    int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
 };
 
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_albedo, c->d_light, c->d_cam, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -166,9 +164,6 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
-    CK(upload(&c->d_albedo, c->host.albedo));
-    CK(upload(&c->d_light, std::vector<MfxLight>{c->host.light}));
-    CK(upload(&c->d_cam, std::vector<MfxCamera>{c->host.camera}));
     const size_t plane = sizeof(double) * (size_t)c->npix;
     CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
     c->d_accum = c->d_accum_own;
@@ -180,6 +175,7 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_wfctl, MFX_MAX_SUB * WF_NCTL * sizeof(unsigned long long)));
     CK(hipHostMalloc((void**)&c->h_pin, MFX_MAX_SUB * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
+    if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, atoi(ck) / 64 * 64);
     if (const char* ns = getenv("MFX_SUBPOOLS")) c->nsub = std::max(1, std::min(MFX_MAX_SUB, atoi(ns)));
     CK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
     for (int k = 0; k < c->nsub; ++k) {
@@ -197,6 +193,10 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     c->grid = prop.multiProcessorCount * bpc;
     int ebpc = 0, sbpc = 0;
     CK(mfx_wf_occupancy(c->stack_size, &ebpc, &sbpc));
+    if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
+        ebpc = std::min(ebpc, std::max(1, atoi(b)));
+        sbpc = std::min(sbpc, std::max(1, atoi(b)));
+    }
     c->wf_ext_grid = prop.multiProcessorCount * std::max(1, std::min(ebpc, 8));
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
 #undef CK
@@ -238,9 +238,8 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
-    P.albedo = c->d_albedo;
-    P.light = c->d_light;
-    P.cam = c->d_cam;
+    P.light = c->host.light;
+    P.cam = c->host.camera;
     P.accum = c->d_accum;
 }
 
@@ -270,7 +269,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     base.height = H;
     base.max_depth = c->host.max_depth;
     base.stack_size = c->stack_size;
-    base.chunk = 256;
+    base.chunk = c->wf_chunk;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     struct Sub {
         WfParams P;
@@ -375,12 +374,11 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
-    P.albedo = c->d_albedo;
     P.accum = c->d_accum;
     P.work_counter = c->d_work;
     P.counters = c->d_counters;
-    P.light = c->d_light;
-    P.cam = c->d_cam;
+    P.light = c->host.light;
+    P.cam = c->host.camera;
     P.seed = c->seed;
     P.sample_base = sample_base;
     P.nsamples = ns;

@@ -13,12 +13,11 @@ struct TraceParams {
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
-    const double* albedo;
     double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
     unsigned long long* work_counter;
     unsigned long long* counters;    // [8] ray / traversal counters
-    const MfxLight* light;           // device copies (scalar-loaded where used; keeps SGPRs free)
-    const MfxCamera* cam;
+    MfxLight light;                  // by value: kernel arguments are scalar-loaded, never per-lane gathers
+    MfxCamera cam;
     uint64_t seed;
     int64_t sample_base;             // first global sample index of this call
     int64_t nsamples;                // samples this context renders per pixel in this call

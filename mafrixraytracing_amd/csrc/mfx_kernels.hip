@@ -33,8 +33,8 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
-    const MfxLight& LT = *P.light;
-    const MfxCamera& CAM = *P.cam;
+    const MfxLight& LT = P.light;
+    const MfxCamera& CAM = P.cam;
     const int W = P.width, H = P.height;
     const int64_t npix = (int64_t)W * H;
     const int tiles_x = (W + 7) >> 3;
@@ -140,7 +140,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             }
             const DV wi = vnormalize(p);
             const double ei = vdot(nm, wi);
-            const double* a = P.albedo + 3 * sh.material;
+            const double* a = sh.albedo;
             const DV col = dv(TWOPI * (ei * (INVPI * a[0])), TWOPI * (ei * (INVPI * a[1])), TWOPI * (ei * (INVPI * a[2])));
             // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
             const double sel = rng_next(key, rn);
@@ -151,7 +151,10 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
             const double sq = sqrt(1. - uu);
             const double s1 = 1. - sq, s2 = vv * sq;
-            const DV lp = vadd(vadd(ld3(LT.v0[lt]), vmul(ld3(LT.e1[lt]), s1)), vmul(ld3(LT.e2[lt]), s2));
+            const DV lv0 = lt ? ld3(LT.v0[1]) : ld3(LT.v0[0]);
+            const DV le1 = lt ? ld3(LT.e1[1]) : ld3(LT.e1[0]);
+            const DV le2 = lt ? ld3(LT.e2[1]) : ld3(LT.e2[0]);
+            const DV lp = vadd(vadd(lv0, vmul(le1, s1)), vmul(le2, s2));
             const DV toLight = vsub(lp, hp);
             const double dist = vlen(toLight);
             const DV unit = vdiv(toLight, dist);

@@ -58,10 +58,10 @@ struct alignas(16) MfxSlot {
     double a[3];    // tri: v0      sphere: center
     double b[3];    // tri: e1      sphere: {radius, 0, 0}
     double c[3];    // tri: e2
-    double lo[3];   // FP64 box of the primitive's reference leaf (InitNode, BvhNode.fs:32-37)
+    int32_t first;  // MfxLeaf.first of the primitive's reference leaf
+    int32_t info;   // MFX_INFO_* fields        (bytes 0..79: five 16-B loads per test)
+    double lo[3];   // FP64 box of that reference leaf (InitNode, BvhNode.fs:32-37)
     double hi[3];
-    int32_t first;  // MfxLeaf.first of that reference leaf
-    int32_t info;   // MFX_INFO_* fields
 };
 
 // leaf child code: ~((first slot << 3) | (slots - 1)), at most 8 slots (4 primitives, rects take 2)
@@ -69,6 +69,7 @@ struct alignas(16) MfxSlot {
 
 struct alignas(16) MfxShade {
     double n[3];        // face normal of this triangle slot; a sphere's centre
+    double albedo[3];   // MaterialManager[material] flattened to its Lambert albedo (Material.fs:52-68)
     int32_t material;   // MaterialManager slot
     int32_t prim_kind;  // original primitive index (mfx_prim order) << 2 | MFX_KIND_*
 };

@@ -447,6 +447,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         double al = len(a);
         put(sh.n, D3{a.x / al, a.y / al, a.z / al});  // Trangle.fs:110-111
         sh.material = mat;
+        std::memcpy(sh.albedo, d->albedo + 3 * (size_t)mat, sizeof(sh.albedo));
         sh.prim_kind = (prim << 2) | kind;
         pshade.push_back(sh);
     };
@@ -478,6 +479,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
             MfxShade sh{};
             put(sh.n, c);  // the shade record of a sphere carries its centre
             sh.material = p.material;
+            std::memcpy(sh.albedo, d->albedo + 3 * (size_t)p.material, sizeof(sh.albedo));
             sh.prim_kind = (i << 2) | MFX_KIND_SPHERE;
             pshade.push_back(sh);
         } else {

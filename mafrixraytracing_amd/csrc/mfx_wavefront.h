@@ -34,9 +34,8 @@ struct WfParams {
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
-    const double* albedo;
-    const MfxLight* light;
-    const MfxCamera* cam;
+    MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
+    MfxCamera cam;
     double* accum;  // [3][w*h]
     // path slots (SoA)
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point

@@ -37,6 +37,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #endif
 struct DiagAcc {
     uint64_t fetch, node, leaf, fin, last;
+    uint32_t outer, node_iters, windows;
 };
 __device__ __forceinline__ uint64_t stamp() {
     uint64_t t;
@@ -146,6 +147,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
                                           DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
+        if (diag) dg.node_iters++;
         T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
     }
     DIAG_MARK(dg, node, diag);
@@ -167,6 +169,11 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
 __device__ __forceinline__ void retire(const WfParams& P, int s, double lx, double ly, double lz) {
     const int64_t pix = P.pixel[s];
     const int64_t npix = (int64_t)P.width * P.height;
+#ifdef MFX_DIAG_NO_ACCUM_ATOMICS
+    if (lx == 12345.0) P.accum[pix] = lx + ly + lz;
+    P.state[s] = WF_FREE;
+    return;
+#endif
     if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
     if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
     if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
@@ -200,7 +207,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
     constexpr bool DG = MFX_DIAG_STAMPS == 1;
-    DiagAcc dg{0, 0, 0, 0, 0};
+    DiagAcc dg{0, 0, 0, 0, 0, 0, 0, 0};
     if (DG) dg.last = stamp();
 
     while (true) {
@@ -210,6 +217,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         while (m != 0 && !sc.exhausted) {
             if (pend_lo == pend_hi) {
                 if (!sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size)) break;
+                if (DG) dg.windows++;
                 // scan a 64-slot window with the whole wave; its FREE slots share one allocation
                 const int j = sc.win_next + lane;
                 const int sj = j < sc.win_end ? P.state[j] : -1;
@@ -252,7 +260,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     const int x = (int)(tile % tiles_x) * 8 + (within & 7);
                     const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
                     if (x < W && y < H) {  // edge-tile padding indices start no path
-                        const MfxCamera& CAM = *P.cam;
+                        const MfxCamera& CAM = P.cam;
                         const int64_t pixel = (int64_t)x * H + y;  // Color[w,h] x-major
                         const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
                         const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
@@ -303,6 +311,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         }
         if (!__any(active)) break;  // every chunk taken and every pending ray traced
         DIAG_MARK(dg, fetch, DG);
+        if (DG) dg.outer++;
         bool fin = false;
         if (active) fin = trav_step<false, STATS>(T, S, stack, st, dg, DG);
         DIAG_MARK(dg, leaf, DG);
@@ -325,6 +334,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         atomicAdd(cnt + 11, (unsigned long long)dg.node);
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
+        atomicAdd(cnt + 14, (unsigned long long)dg.outer);
+        atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
+        atomicAdd(cnt + 9, (unsigned long long)dg.windows);
     }
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
@@ -358,7 +370,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     uint32_t c_shadow = 0;
     Stats st{0, 0, 0};
     constexpr bool DG = MFX_DIAG_STAMPS == 2;
-    DiagAcc dg{0, 0, 0, 0, 0};
+    DiagAcc dg{0, 0, 0, 0, 0, 0, 0, 0};
     if (DG) dg.last = stamp();
 
     while (true) {
@@ -367,6 +379,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         while (m != 0 && !sc.exhausted) {
             if (pend_lo == pend_hi) {
                 if (!sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size)) break;
+                if (DG) dg.windows++;
                 // scan a 64-slot window with the whole wave: shade every hit, retire every miss
                 const int j = sc.win_next + lane;
                 bool take = false;
@@ -396,9 +409,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                         }
                         const DV wi = vnormalize(p);
                         const double ei = vdot(nm, wi);
-                        const double* a = P.albedo + 3 * sh.material;
+                        const double* a = sh.albedo;
                         // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
-                        const MfxLight& LT = *P.light;
+                        const MfxLight& LT = P.light;
                         const double sel = rng_next(key, rn);
                         const int lt = sel < 0.5 ? 0 : 1;
                         const double tu = rng_next(key, rn);
@@ -407,7 +420,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                         if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
                         const double sq = sqrt(1. - uu);
                         const double s1 = 1. - sq, s2 = vv * sq;
-                        const DV lp = vadd(vadd(ld3(LT.v0[lt]), vmul(ld3(LT.e1[lt]), s1)), vmul(ld3(LT.e2[lt]), s2));
+                        // both halves from scalar registers, selected per lane
+                        const DV lv0 = lt ? ld3(LT.v0[1]) : ld3(LT.v0[0]);
+                        const DV le1 = lt ? ld3(LT.e1[1]) : ld3(LT.e1[0]);
+                        const DV le2 = lt ? ld3(LT.e2[1]) : ld3(LT.e2[0]);
+                        const DV lp = vadd(vadd(lv0, vmul(le1, s1)), vmul(le2, s2));
                         const DV toLight = vsub(lp, hp);
                         const double dist = vlen(toLight);
                         unit = vdiv(toLight, dist);
@@ -471,6 +488,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         }
         if (!__any(active)) break;
         DIAG_MARK(dg, fetch, DG);
+        if (DG) dg.outer++;
         bool fin = false;
 #ifdef MFX_DIAG_SKIP_SHADOW_TRAV
         if (active) {
@@ -505,6 +523,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         atomicAdd(cnt + 11, (unsigned long long)dg.node);
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
+        atomicAdd(cnt + 14, (unsigned long long)dg.outer);
+        atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
+        atomicAdd(cnt + 9, (unsigned long long)dg.windows);
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);

@@ -36,7 +36,14 @@ def main():
         for l in libs:
             code = CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(l)).replace("SCENE", repr(scene)) \
                 .replace("STEPS", "2").replace("SPP", str(spp))
-            p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+            env = dict(os.environ)
+            ef = l[:-3] + ".env"  # optional KEY=VALUE lines for this variant (e.g. MFX_CHUNK=1024)
+            if os.path.exists(ef):
+                for line in open(ef):
+                    if "=" in line:
+                        k, v = line.strip().split("=", 1)
+                        env[k] = v
+            p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300, env=env)
             if p.returncode != 0:
                 print(os.path.basename(l), "FAILED", p.stderr[-2000:], flush=True)
                 continue

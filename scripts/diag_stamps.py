@@ -17,5 +17,7 @@ ctx.accum_clear(); ctx.trace_accumulate(spp, 0); ctx.sync()
 c = ctx.ray_counts()
 ph = dict(zip(["fetch", "node", "leaf", "fin"], c[10:14]))
 tot = sum(ph.values())
+nw = ctx.trace_timing()["launches"]
+print("per launch: outer iters %.4g, wave node iters %.4g, windows %.4g; rays %s" % (c[14] / nw, c[15] / nw, c[9] / nw, c[:3] / nw))
 print(os.path.basename(lib), json.dumps({k: round(v / tot, 4) for k, v in ph.items()}), "total wave-cycles %.4g" % tot,
       json.dumps(ctx.trace_timing()))
