@@ -336,7 +336,6 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
         atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
-        atomicAdd(cnt + 9, (unsigned long long)dg.windows);
     }
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
@@ -360,7 +359,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
+    int* shl = (int*)(red + 16) + wave * 256;  // shade list: [0,128) path slots, [128,256) hit slots
     Scanner sc{0, 0, 0, false};
+    int nshade = 0;  // wave-uniform: hits listed for shading
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
@@ -376,97 +377,112 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     while (true) {
         bool idle = !active;
         uint64_t m = __ballot(idle);
-        while (m != 0 && !sc.exhausted) {
+        while (m != 0) {
             if (pend_lo == pend_hi) {
-                if (!sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size)) break;
-                if (DG) dg.windows++;
-                // scan a 64-slot window with the whole wave: shade every hit, retire every miss
-                const int j = sc.win_next + lane;
-                bool take = false;
-                DV unit = dv(0, 0, 0);
-                double tmax = 0.0, dx = 0.0, dy = 0.0, dz = 0.0;
-                bool cn = false;
-                if (j < sc.win_end && P.state[j] == WF_EXT_DONE) {
-                    const int slot = P.hit_slot[j];
-                    if (slot < 0) {
-                        retire(P, j, P.lx[j], P.ly[j], P.lz[j]);  // miss: TraceRay returns black (Integrators.fs:137)
-                    } else {
-                        // ---- one vertex of PathIntegrator.TraceRay (Integrators.fs:109-136) ----
-                        const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
-                        const MfxShade sh = P.shade[slot];
-                        DV nm;
-                        if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
-                        else nm = ld3(sh.n);
-                        const uint64_t key = P.key[j];
-                        uint32_t rn = P.rn[j];
-                        // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
-                        DV p = dv(20, 20, 20);
-                        while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
-                            const double rx = rng_next(key, rn);
-                            const double ry = rng_next(key, rn);
-                            const double rz = rng_next(key, rn);
-                            p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
-                        }
-                        const DV wi = vnormalize(p);
-                        const double ei = vdot(nm, wi);
-                        const double* a = sh.albedo;
-                        // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
-                        const MfxLight& LT = P.light;
-                        const double sel = rng_next(key, rn);
-                        const int lt = sel < 0.5 ? 0 : 1;
-                        const double tu = rng_next(key, rn);
-                        const double tv = rng_next(key, rn);
-                        double uu = tu, vv = tv;
-                        if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
-                        const double sq = sqrt(1. - uu);
-                        const double s1 = 1. - sq, s2 = vv * sq;
-                        // both halves from scalar registers, selected per lane
-                        const DV lv0 = lt ? ld3(LT.v0[1]) : ld3(LT.v0[0]);
-                        const DV le1 = lt ? ld3(LT.e1[1]) : ld3(LT.e1[0]);
-                        const DV le2 = lt ? ld3(LT.e2[1]) : ld3(LT.e2[0]);
-                        const DV lp = vadd(vadd(lv0, vmul(le1, s1)), vmul(le2, s2));
-                        const DV toLight = vsub(lp, hp);
-                        const double dist = vlen(toLight);
-                        unit = vdiv(toLight, dist);
-                        // NewAreaLight.L (Light.fs:48-56) and the unclamped cosine (Integrators.fs:52)
-                        const double cos_o = vdot(toLight, ld3(LT.normal));
-                        const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
-                        const double solid = fabs(cos_o) * LT.area / dist2;
-                        const double cs = vdot(unit, nm);
-                        const double Tx = P.tx[j] * (TWOPI * (ei * (INVPI * a[0])));
-                        const double Ty = P.ty[j] * (TWOPI * (ei * (INVPI * a[1])));
-                        const double Tz = P.tz[j] * (TWOPI * (ei * (INVPI * a[2])));
-                        // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
-                        if (cos_o < 0.) {
-                            dx = Tx * ((cs * (solid * LT.color[0])) / LT.pdf);
-                            dy = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
-                            dz = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
-                        }
-                        P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
-                        P.rn[j] = rn;
-                        const int depth = P.depth[j] - 1;
-                        P.depth[j] = depth;
-                        // the depth -1 query's result is discarded (Integrators.fs:109): never traced
-                        cn = depth >= 0;
-                        if (cn) { P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z; }
-                        tmax = dist - 1e-6;  // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (:44)
-                        take = true;
-                        c_shadow++;
+                if (nshade < 64 && !sc.exhausted && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size)) {
+                    if (DG) dg.windows++;
+                    // scan a 64-slot window with the whole wave: retire every miss (TraceRay returns
+                    // black, Integrators.fs:137), append every hit to the wave's shade list
+                    const int j = sc.win_next + lane;
+                    int hs = -1;
+                    if (j < sc.win_end && P.state[j] == WF_EXT_DONE) {
+                        hs = P.hit_slot[j];
+                        if (hs < 0) retire(P, j, P.lx[j], P.ly[j], P.lz[j]);
                     }
+                    const uint64_t hm = __ballot(hs >= 0);
+                    if (hs >= 0) {
+                        const int r = nshade + __popcll(hm & lanes_below());
+                        shl[r] = j;
+                        shl[128 + r] = hs;
+                    }
+                    wave_lds_sync();
+                    nshade += __popcll(hm);
+                    sc.win_next += 64;
+                    continue;
                 }
-                const uint64_t cm = __ballot(take);
-                if (take) {
-                    const int r = __popcll(cm & lanes_below());
-                    pd.slot[r] = j;
-                    pd.flag[r] = cn ? 1 : 0;
-                    pd.v[0 * 64 + r] = unit.x; pd.v[1 * 64 + r] = unit.y; pd.v[2 * 64 + r] = unit.z;
-                    pd.v[3 * 64 + r] = tmax;
-                    pd.v[4 * 64 + r] = dx; pd.v[5 * 64 + r] = dy; pd.v[6 * 64 + r] = dz;
+                if (nshade == 0) break;  // every chunk scanned, every hit shaded, every ray handed out
+                // ---- shade up to 64 listed hits with all lanes: one vertex of PathIntegrator.TraceRay
+                //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
+                const int cnt = nshade < 64 ? nshade : 64;
+                if (lane < cnt) {
+                    const int j = shl[lane];
+                    const int slot = shl[128 + lane];
+                    const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
+                    const MfxShade sh = P.shade[slot];
+                    DV nm;
+                    if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
+                    else nm = ld3(sh.n);
+                    const uint64_t key = P.key[j];
+                    uint32_t rn = P.rn[j];
+                    // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
+                    DV p = dv(20, 20, 20);
+                    while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
+                        const double rx = rng_next(key, rn);
+                        const double ry = rng_next(key, rn);
+                        const double rz = rng_next(key, rn);
+                        p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
+                    }
+                    const DV wi = vnormalize(p);
+                    const double ei = vdot(nm, wi);
+                    const double* a = sh.albedo;
+                    // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
+                    const MfxLight& LT = P.light;
+                    const double sel = rng_next(key, rn);
+                    const int lt = sel < 0.5 ? 0 : 1;
+                    const double tu = rng_next(key, rn);
+                    const double tv = rng_next(key, rn);
+                    double uu = tu, vv = tv;
+                    if (tu + tv > 1.) { uu = 1. - tu; vv = 1. - tv; }
+                    const double sq = sqrt(1. - uu);
+                    const double s1 = 1. - sq, s2 = vv * sq;
+                    // both halves from scalar registers, selected per lane
+                    const DV lv0 = lt ? ld3(LT.v0[1]) : ld3(LT.v0[0]);
+                    const DV le1 = lt ? ld3(LT.e1[1]) : ld3(LT.e1[0]);
+                    const DV le2 = lt ? ld3(LT.e2[1]) : ld3(LT.e2[0]);
+                    const DV lp = vadd(vadd(lv0, vmul(le1, s1)), vmul(le2, s2));
+                    const DV toLight = vsub(lp, hp);
+                    const double dist = vlen(toLight);
+                    const DV unit = vdiv(toLight, dist);
+                    // NewAreaLight.L (Light.fs:48-56) and the unclamped cosine (Integrators.fs:52)
+                    const double cos_o = vdot(toLight, ld3(LT.normal));
+                    const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
+                    const double solid = fabs(cos_o) * LT.area / dist2;
+                    const double cs = vdot(unit, nm);
+                    const double Tx = P.tx[j] * (TWOPI * (ei * (INVPI * a[0])));
+                    const double Ty = P.ty[j] * (TWOPI * (ei * (INVPI * a[1])));
+                    const double Tz = P.tz[j] * (TWOPI * (ei * (INVPI * a[2])));
+                    // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
+                    double dx = 0.0, dy = 0.0, dz = 0.0;
+                    if (cos_o < 0.) {
+                        dx = Tx * ((cs * (solid * LT.color[0])) / LT.pdf);
+                        dy = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
+                        dz = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
+                    }
+                    P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
+                    P.rn[j] = rn;
+                    const int depth = P.depth[j] - 1;
+                    P.depth[j] = depth;
+                    // the depth -1 query's result is discarded (Integrators.fs:109): never traced
+                    const bool cn = depth >= 0;
+                    if (cn) { P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z; }
+                    // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
+                    pd.slot[lane] = j;
+                    pd.flag[lane] = cn ? 1 : 0;
+                    pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
+                    pd.v[3 * 64 + lane] = dist - 1e-6;
+                    pd.v[4 * 64 + lane] = dx; pd.v[5 * 64 + lane] = dy; pd.v[6 * 64 + lane] = dz;
+                    c_shadow++;
                 }
+                // the unshaded rest of the list moves to its front
+                const int rest = nshade - cnt;
+                int mv_j = 0, mv_s = 0;
+                if (lane < rest) { mv_j = shl[cnt + lane]; mv_s = shl[128 + cnt + lane]; }
                 wave_lds_sync();
+                if (lane < rest) { shl[lane] = mv_j; shl[128 + lane] = mv_s; }
+                wave_lds_sync();
+                nshade = rest;
                 pend_lo = 0;
-                pend_hi = __popcll(cm);
-                sc.win_next += 64;
+                pend_hi = cnt;
                 continue;
             }
             const int avail = pend_hi - pend_lo;
@@ -525,7 +541,6 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
         atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
-        atomicAdd(cnt + 9, (unsigned long long)dg.windows);
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);
@@ -553,7 +568,8 @@ WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n) {
 }
 
 static size_t wf_lds_bytes(int stack_size) {
-    return (size_t)4 * stack_size * 64 * sizeof(int) + 4 * WF_PEND_BYTES + 64;
+    // stacks, pending-ray lists, block reduction scratch (64 B), k_shadow's shade lists (1 KB / wave)
+    return (size_t)4 * stack_size * 64 * sizeof(int) + 4 * WF_PEND_BYTES + 64 + 4 * 256 * sizeof(int);
 }
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
