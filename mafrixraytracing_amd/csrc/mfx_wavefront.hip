@@ -32,6 +32,10 @@
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+#ifndef MFX_NODE_LANES_MIN
+#define MFX_NODE_LANES_MIN 12  // node-loop early exit: fewer lanes than this still stepping
+#endif
+
 #ifndef MFX_DIAG_STAMPS
 #define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow
 #endif
@@ -147,10 +151,14 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
                                           DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
-        if (diag) dg.node_iters++;
+        if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
         T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
+        // leave the node loop once few lanes still step: the rest resume next round, after the
+        // leaf tests and a refill of the idle lanes
+        if (__popcll(__ballot(T.node >= 0)) < MFX_NODE_LANES_MIN) break;
     }
     DIAG_MARK(dg, node, diag);
+    if (T.node >= 0) return false;
     if (T.node == MFX_TRAV_EXIT) return true;
     if (leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st)) {
         if (SHADOW) {
@@ -329,13 +337,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 0, c_primary, red);
     block_add<4>(cnt + 1, c_ext, red);
+    if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
         atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
         atomicAdd(cnt + 11, (unsigned long long)dg.node);
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
-        atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
     }
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
@@ -534,13 +542,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
+    if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
         atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
         atomicAdd(cnt + 11, (unsigned long long)dg.node);
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
-        atomicAdd(cnt + 15, (unsigned long long)dg.node_iters);
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);

@@ -20,7 +20,7 @@ ph = dict(zip(["fetch", "node", "leaf", "fin"], c[10:14]))
 tot = sum(ph.values())
 nw = ctx.trace_timing()["launches"]
 ext = "extend" in open(lib, "rb").read().decode("latin1") and os.path.basename(lib) == "st1.so"
-ln, ll, lp = (c[4], c[5], c[6]) if os.path.basename(lib) == "st1.so" else (c[7], c[8], c[9])
+ln, ll, lp = (c[4], c[5], c[6]) if os.path.basename(lib).startswith("st1") else (c[7], c[8], c[9])
 print("per launch: outer %.4g, wave node iters %.4g (%.1f lanes each), lane leaf visits %.4g, lane prim tests %.4g; rays %s"
       % (c[14] / nw, c[15] / nw, ln / max(c[15], 1), ll / nw, lp / nw, c[:3] / nw))
 print(os.path.basename(lib), json.dumps({k: round(v / tot, 4) for k, v in ph.items()}), "total wave-cycles %.4g" % tot,

@@ -41,11 +41,12 @@ int main() {
     printf("%10s %4s %8s %14s\n", "table_KB", "NL", "waves/CU", "cycles/step");
     for (size_t nodes : {(size_t)256, (size_t)1 << 11, (size_t)1 << 14, (size_t)1 << 20})
         for (int bpc : {1, 3})
-            for (int nl : {1, 7}) {
+            for (int nl : {1, 4, 7}) {
                 const uint32_t mask = (uint32_t)(nodes - 1);
                 const int blocks = cus * bpc;
                 hipMemset(cyc, 0, 8);
                 if (nl == 1) hipLaunchKernelGGL((chase<1>), dim3(blocks), dim3(256), 0, 0, tab, mask, steps, out, cyc);
+                else if (nl == 4) hipLaunchKernelGGL((chase<4>), dim3(blocks), dim3(256), 0, 0, tab, mask, steps, out, cyc);
                 else hipLaunchKernelGGL((chase<7>), dim3(blocks), dim3(256), 0, 0, tab, mask, steps, out, cyc);
                 if (hipDeviceSynchronize() != hipSuccess) { printf("error\n"); return 1; }
                 unsigned long long c = 0;
