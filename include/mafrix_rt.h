@@ -192,8 +192,9 @@ int mfx_ref_leaves(mfx_ctx* ctx, int32_t* indices_out, int32_t* leaf_first_out,
                    int32_t* leaf_count_out, int32_t* nleaves_out);
 
 /* Host-only (no device needed): the same leaf grouping computed straight from a scene
- * description, plus the traversal BVH's shape: info[0] = clusters, info[1] = internal nodes,
- * info[2] = depth. Any output pointer may be NULL.                                          */
+ * description, plus the traversal BVH's shape: info[0] = clusters, info[1] = internal BVH4
+ * nodes, info[2] = LDS stack entries per lane, info[3] = traversal slots. Any output pointer
+ * may be NULL.                                                                                */
 int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t* leaf_first_out,
                      int32_t* leaf_count_out, int32_t* nleaves_out, int32_t info_out[4]);
 

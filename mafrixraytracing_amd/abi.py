@@ -187,5 +187,5 @@ def build_leaves(arrays: SceneArrays):
     info = np.zeros(4, dtype=np.int32)
     check(lib.mfx_build_leaves(C.byref(d), iptr(idx), iptr(lf), iptr(lc), iptr(nl), iptr(info)), "mfx_build_leaves")
     k = int(nl[0])
-    return idx, lf[:k], lc[:k], {"clusters": int(info[0]), "nodes": int(info[1]), "depth": int(info[2]),
-                                 "root_is_leaf": int(info[3])}
+    return idx, lf[:k], lc[:k], {"clusters": int(info[0]), "nodes": int(info[1]), "stack": int(info[2]),
+                                 "slots": int(info[3])}

@@ -619,7 +619,7 @@ int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t*
     if (info_out) {
         info_out[0] = s.nclusters;
         info_out[1] = (int32_t)s.nodes.size();
-        info_out[2] = s.bvh_depth;
+        info_out[2] = s.stack_entries;
         info_out[3] = (int32_t)s.slots.size();
     }
     return MFX_OK;

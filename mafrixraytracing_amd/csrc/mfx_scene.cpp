@@ -334,8 +334,7 @@ struct SahBuilder {
 
 // BVH2 -> BVH4: a node adopts the children of its largest-area internal child until it has four
 // (Wald et al. 2008 style collapse). Preorder output; records the depth and the stack bound
-// (max over nodes of the pushes its ancestors can leave on the stack, plus the 3-slot window
-// node_step writes unconditionally).
+// (max over nodes of the pushes its ancestors can leave on the stack plus its own).
 struct Collapse4 {
     const std::vector<Node2>& n2;
     std::vector<MfxNode>& out;
@@ -377,7 +376,7 @@ struct Collapse4 {
             bx[best + 1] = m.box[1];
             ++nc;
         }
-        max_stack = std::max(max_stack, pushed + 3);
+        max_stack = std::max(max_stack, pushed + nc - 1);  // node_step writes stack[pushed .. pushed + nc - 2]
         const int self = (int)out.size();
         out.push_back(MfxNode{});
         int ref4[4];

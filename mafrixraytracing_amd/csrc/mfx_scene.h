@@ -25,7 +25,7 @@ struct MfxHostScene {
     MfxCamera camera;
     int32_t width = 0, height = 0, max_depth = 3;
     int32_t bvh_depth = 0;     // longest root-to-leaf path in nodes[]
-    int32_t stack_entries = 1; // traversal stack bound: pushes along any path + the 3-slot write window
+    int32_t stack_entries = 1; // traversal stack bound: pushes along any root-to-node path
     float eps = 0.f;           // conservative box widening
 };
 

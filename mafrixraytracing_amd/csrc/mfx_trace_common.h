@@ -286,9 +286,7 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 
 // One internal-node step of the BVH4, branch-free: four child slab tests, the hit children sorted
 // near to far (5-comparator network over (entry distance, child), misses sorted last at +inf),
-// then descend into the nearest, push the others far-first, or pop. The push window
-// stack[sp .. sp+2] is written unconditionally and sp advances by (hits - 1), so only the pushed
-// entries survive; the pop candidate (top of stack) is read before the node's boxes arrive, so
+// then descend into the nearest, push the others far-first, or pop. The pop candidate (top of stack) is read before the node's boxes arrive, so
 // the LDS read overlaps the L2 load. Returns the next node: >= 0 internal, < 0 a leaf (~offset),
 // or MFX_TRAV_EXIT when nothing is left. An empty child (box at FLT_MAX) never hits.
 __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
@@ -305,7 +303,15 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     const int top = stack[(sp > 0 ? sp - 1 : 0) * 64];
     const float4* __restrict__ q = (const float4*)(nodes + node);
     const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
-    const int4 ch = *(const int4*)(q + 6);
+    int4 ch = *(const int4*)(q + 6);
+#ifdef MFX_DIAG_EXTRA_NODE_LOADS  // timing experiment: MFX_DIAG_EXTRA_NODE_LOADS more 16-B loads per step
+#pragma unroll
+    for (int k = 0; k < MFX_DIAG_EXTRA_NODE_LOADS; ++k) {
+        const int z = __float_as_int(tlim) == 0x7fffffff ? 1 : 0;  // a runtime 0 the compiler cannot fold
+        const int4 x = *((const int4*)(q + (k % 7)) + z);
+        if ((x.x ^ x.y ^ x.z ^ x.w) == 0x7fedcba9) ch.x = 0;  // never true for real node data
+    }
+#endif
     float d[4];
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     int nh = 0;
@@ -328,10 +334,11 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     cswap(d[0], c[0], d[2], c[2]);
     cswap(d[1], c[1], d[3], c[3]);
     cswap(d[1], c[1], d[2], c[2]);
-    // far-first pushes: stack[sp + j] = c[nh - 1 - j] for j < nh - 1
-    stack[sp * 64] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
-    stack[(sp + 1) * 64] = nh == 4 ? c[2] : c[1];
-    stack[(sp + 2) * 64] = c[1];
+    // far-first pushes: stack[sp + j] = c[nh - 1 - j] for j < nh - 1 (exec-masked stores, so the
+    // stack never holds more than the pushes themselves: mfx_scene.cpp's Collapse4 bound)
+    if (nh >= 2) stack[sp * 64] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
+    if (nh >= 3) stack[(sp + 1) * 64] = nh == 4 ? c[2] : c[1];
+    if (nh >= 4) stack[(sp + 2) * 64] = c[1];
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);

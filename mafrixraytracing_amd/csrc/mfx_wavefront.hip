@@ -107,20 +107,24 @@ struct Scanner {
     }
 };
 
-// Per-wave LDS list of pending rays: slot index, a flag word, and up to 7 doubles per entry,
-// each field a 64-entry column (conflict-free).
-#define WF_PEND_DOUBLES 7
-#define WF_PEND_BYTES (64 * (8 + 8 * WF_PEND_DOUBLES))
-struct Pend {
+// Per-wave LDS list of pending rays: slot index, (k_shadow) a flag word, and ND doubles per entry,
+// each field a 64-entry column (conflict-free). k_extend: origin + direction (6 doubles);
+// k_shadow: direction, tmax and the vertex's direct term (7).
+template <int ND, bool FLAG>
+struct PendT {
+    static constexpr int BYTES = 64 * (4 + (FLAG ? 4 : 0) + 8 * ND);
     int* slot;
     int* flag;
     double* v;  // v[f * 64 + entry]
-    __device__ __forceinline__ Pend(uint8_t* base) {
+    __device__ __forceinline__ PendT(uint8_t* base) {
         slot = (int*)base;
         flag = slot + 64;
-        v = (double*)(base + 512);
+        v = (double*)(base + (FLAG ? 512 : 256));
     }
 };
+using PendExt = PendT<6, false>;
+using PendShd = PendT<7, true>;
+constexpr int WF_SHADE_LIST_BYTES = 256 * 4;  // k_shadow shade list per wave: 128 path slots + 128 hit slots
 
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
@@ -198,8 +202,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
-    const Pend pd(pend_base + wave * WF_PEND_BYTES);
-    uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
+    const PendExt pd(pend_base + wave * PendExt::BYTES);
+    uint32_t* red = (uint32_t*)(pend_base + 4 * PendExt::BYTES);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
     const int W = P.width, H = P.height;
@@ -362,8 +366,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
-    const Pend pd(pend_base + wave * WF_PEND_BYTES);
-    uint32_t* red = (uint32_t*)(pend_base + 4 * WF_PEND_BYTES);
+    const PendShd pd(pend_base + wave * PendShd::BYTES);
+    uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
@@ -575,31 +579,33 @@ WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n) {
     return S;
 }
 
-static size_t wf_lds_bytes(int stack_size) {
-    // stacks, pending-ray lists, block reduction scratch (64 B), k_shadow's shade lists (1 KB / wave)
-    return (size_t)4 * stack_size * 64 * sizeof(int) + 4 * WF_PEND_BYTES + 64 + 4 * 256 * sizeof(int);
+// stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
+static size_t wf_lds_bytes(int stack_size, bool shadow) {
+    const size_t stacks = (size_t)4 * stack_size * 64 * sizeof(int);
+    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * WF_SHADE_LIST_BYTES : stacks + 4 * PendExt::BYTES + 64;
 }
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
-    const size_t lds = wf_lds_bytes(stack_size);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, k_extend<false>, 256, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, k_extend<false>, 256,
+                                                                 wf_lds_bytes(stack_size, false));
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, k_shadow<false>, 256, lds);
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, k_shadow<false>, 256,
+                                                        wf_lds_bytes(stack_size, true));
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
-    const size_t lds = wf_lds_bytes(P.stack_size);
+    const size_t lds_e = wf_lds_bytes(P.stack_size, false), lds_s = wf_lds_bytes(P.stack_size, true);
     hipError_t e = hipMemsetAsync(P.ctl + WF_CTL_EXT, 0, 2 * WF_SHARDS * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     if (stats)
-        hipLaunchKernelGGL(k_extend<true>, dim3(ext_grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL(k_extend<true>, dim3(ext_grid), dim3(256), lds_e, st, P);
     else
-        hipLaunchKernelGGL(k_extend<false>, dim3(ext_grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL(k_extend<false>, dim3(ext_grid), dim3(256), lds_e, st, P);
     if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return e;
     if (stats)
-        hipLaunchKernelGGL(k_shadow<true>, dim3(shd_grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL(k_shadow<true>, dim3(shd_grid), dim3(256), lds_s, st, P);
     else
-        hipLaunchKernelGGL(k_shadow<false>, dim3(shd_grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL(k_shadow<false>, dim3(shd_grid), dim3(256), lds_s, st, P);
     return hipGetLastError();
 }

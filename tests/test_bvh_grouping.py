@@ -175,4 +175,4 @@ def test_scene_grouping_matches_oracle(oracle, name):
     oi, of, oc = oracle.OracleScene(a).bvh_leaves()
     gi, gf, gc, info = build_leaves(a)
     assert np.array_equal(gi, oi) and np.array_equal(gf, of) and np.array_equal(gc, oc)
-    assert info["depth"] <= 95
+    assert 1 <= info["stack"] <= 96  # LDS traversal stack entries per lane
