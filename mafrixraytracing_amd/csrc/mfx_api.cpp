@@ -88,6 +88,7 @@ struct mfx_ctx {
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
+    bool diag_iter = false;
 };
 
 static void free_ctx(mfx_ctx* c) {
@@ -175,7 +176,8 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_wfctl, MFX_MAX_SUB * WF_NCTL * sizeof(unsigned long long)));
     CK(hipHostMalloc((void**)&c->h_pin, MFX_MAX_SUB * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
-    if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, atoi(ck) / 64 * 64);
+    c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
+    if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
     if (const char* ns = getenv("MFX_SUBPOOLS")) c->nsub = std::max(1, std::min(MFX_MAX_SUB, atoi(ns)));
     CK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
     for (int k = 0; k < c->nsub; ++k) {
@@ -327,6 +329,18 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
                 float f = 0.f;
                 HIPCHECK(hipEventElapsedTime(&f, u.ev[s], u.ev[s + 1]));
                 stage_ms[1 + 2 * s] += f;  // [1] extend, [3] shade + shadow
+            }
+            if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
+                unsigned long long h[16 * WF_SHARDS];
+                HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+                double r[3] = {0, 0, 0};
+                for (int g = 0; g < WF_SHARDS; ++g)
+                    for (int q = 0; q < 3; ++q) r[q] += (double)h[16 * g + q];
+                float fe = 0.f, fs = 0.f;
+                HIPCHECK(hipEventElapsedTime(&fe, u.ev[0], u.ev[1]));
+                HIPCHECK(hipEventElapsedTime(&fs, u.ev[1], u.ev[2]));
+                fprintf(stderr, "iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms\n",
+                        u.iters, r[0], r[1], r[2], fe, fs);
             }
             if (u.drain < 0) {
                 bool all = true;

@@ -20,9 +20,12 @@
 #define WF_NEED_EXT 1
 #define WF_EXT_DONE 2
 
-#define WF_SHARDS 8
+#ifndef WF_SHARDS
+#define WF_SHARDS 64  // returning atomics on one word serialize (~88 per us): 8 shards -> 64 is +13 % on C2
+#endif
+#define WF_CHUNK_MAX 4096  // slots per chunk fetch, at most
 // control words (unsigned long long) in WfParams.ctl
-#define WF_CTL_PATH 0                 // [WF_SHARDS] path counters, shard g owns [g*T/8, (g+1)*T/8)
+#define WF_CTL_PATH 0                 // [WF_SHARDS] path counters, shard g owns [g*T/S, (g+1)*T/S)
 #define WF_CTL_EXT (WF_SHARDS)        // [WF_SHARDS] k_extend slot-chunk heads
 #define WF_CTL_SHD (2 * WF_SHARDS)    // [WF_SHARDS] k_shadow slot-chunk heads
 #define WF_NCTL (3 * WF_SHARDS)

@@ -240,7 +240,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 int64_t pbase = 0;
                 if (nf) {
                     if (lane == 0) {
-                        // path shard g owns [g*T/8, (g+1)*T/8) of this sub-pool's path indices
+                        // path shard g owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices
                         for (int k = 0; k < WF_SHARDS && got == 0; ++k) {
                             const int g = (blockIdx.x * 4 + wave + k) & (WF_SHARDS - 1);
                             const int64_t lo = P.total * g / WF_SHARDS, hi = P.total * (g + 1) / WF_SHARDS;
