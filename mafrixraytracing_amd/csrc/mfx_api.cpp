@@ -272,6 +272,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     base.max_depth = c->host.max_depth;
     base.stack_size = c->stack_size;
     base.chunk = c->wf_chunk;
+    base.alloc = 1;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     struct Sub {
         WfParams P;
@@ -301,6 +302,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
         HIPCHECK(hipMemsetAsync(u.P.ctl, 0, WF_NCTL * sizeof(unsigned long long), u.st));
     }
     auto enqueue = [&](Sub& u) -> int {
+        u.P.alloc = u.drain < 0 ? 1 : 0;  // draining: no path indices left, skip the allocation atomics
         HIPCHECK(hipEventRecord(u.ev[0], u.st));
         HIPCHECK(mfx_wf_iteration(u.P, c->wf_ext_grid, c->wf_shd_grid, stats, u.st, u.ev + 1));
         HIPCHECK(hipEventRecord(u.ev[2], u.st));
@@ -333,14 +335,15 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
             if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
                 unsigned long long h[16 * WF_SHARDS];
                 HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-                double r[3] = {0, 0, 0};
+                double r[16] = {0};
                 for (int g = 0; g < WF_SHARDS; ++g)
-                    for (int q = 0; q < 3; ++q) r[q] += (double)h[16 * g + q];
+                    for (int q = 0; q < 16; ++q) r[q] += (double)h[16 * g + q];
                 float fe = 0.f, fs = 0.f;
                 HIPCHECK(hipEventElapsedTime(&fe, u.ev[0], u.ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, u.ev[1], u.ev[2]));
-                fprintf(stderr, "iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms\n",
-                        u.iters, r[0], r[1], r[2], fe, fs);
+                fprintf(stderr, "iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
+                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g\n",
+                        u.iters, r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15]);
             }
             if (u.drain < 0) {
                 bool all = true;

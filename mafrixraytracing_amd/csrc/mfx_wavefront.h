@@ -2,9 +2,9 @@
 //
 // Each slot carries one path through a three-state machine; each kernel scans the pool for the
 // slots in its state, so no ray queue (and no hot queue-tail atomic) exists:
-//   FREE -(extend: new camera ray)-> ...
-//   FREE | NEED_EXT -(k_extend: closest hit)-> EXT_DONE
-//   EXT_DONE -(k_shadow: shade + shadow ray)-> NEED_EXT, or FREE once the path is retired
+//   FREE | NEED_EXT -(k_extend: camera ray or extension ray, closest hit)-> HIT | MISS (| FRESH)
+//   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, or FREE once the path is retired
+//   MISS -(k_shadow)-> FREE (retired; a FRESH miss adds nothing)
 // The only atomics are per-wave chunk fetches and path allocations, spread over WF_SHARDS
 // counters (a returning atomic on one word saturates near 88 per microsecond), and the FP64
 // adds of finished paths into the pixel accumulator.
@@ -18,12 +18,18 @@
 
 #define WF_FREE 0
 #define WF_NEED_EXT 1
-#define WF_EXT_DONE 2
+#define WF_HIT 2    // k_extend found a hit: hit point (ox..oz) and hit_slot are written
+#define WF_MISS 3   // k_extend found no hit
+#define WF_FRESH 4  // flag on WF_HIT / WF_MISS: the path's camera ray. Its throughput (1), radiance
+                    // (0), draw count (2) and depth (max_depth) are implicit: never stored
 
 #ifndef WF_SHARDS
 #define WF_SHARDS 64  // returning atomics on one word serialize (~88 per us): 8 shards -> 64 is +13 % on C2
 #endif
 #define WF_CHUNK_MAX 4096  // slots per chunk fetch, at most
+#ifndef WF_LOOKAHEAD
+#define WF_LOOKAHEAD 4  // windows whose state words a scan loads in one round
+#endif
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_PATH 0                 // [WF_SHARDS] path counters, shard g owns [g*T/S, (g+1)*T/S)
 #define WF_CTL_EXT (WF_SHARDS)        // [WF_SHARDS] k_extend slot-chunk heads
@@ -63,6 +69,7 @@ struct WfParams {
     int32_t width, height, max_depth;
     int32_t stack_size;
     int32_t chunk;                        // slots per chunk fetch of the kernels
+    int32_t alloc;                        // 1 while path indices remain to be handed out
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool

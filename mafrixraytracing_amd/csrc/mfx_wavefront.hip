@@ -87,8 +87,15 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, uint32_t v, u
 struct Scanner {
     int win_next, win_end, shard_try;
     bool exhausted;
+    // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
+    // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
+    // work are skipped with no further memory round trip. Slots of a taken chunk change only
+    // through this wave, so the words stay current.
+    int b[WF_LOOKAHEAD];
+    int nbuf;
     // Make [win_next, win_end) non-empty; false once every chunk has been taken.
-    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size) {
+    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
+                                           const int32_t* __restrict__ state) {
         if (win_next < win_end) return true;
         while (shard_try < WF_SHARDS) {
             const int g = (blockIdx.x + shard_try) & (WF_SHARDS - 1);
@@ -98,12 +105,30 @@ struct Scanner {
             if ((int64_t)c < shard_size) {
                 win_next = g * shard_size + (int)c;
                 win_end = g * shard_size + min((int)c + chunk, shard_size);
+                fill(state);
                 return true;
             }
             ++shard_try;
         }
         exhausted = true;
         return false;
+    }
+    __device__ __forceinline__ void fill(const int32_t* __restrict__ state) {
+#pragma unroll
+        for (int k = 0; k < WF_LOOKAHEAD; ++k) {
+            const int j = win_next + 64 * k + lane_id();
+            b[k] = j < win_end ? state[j] : -1;
+        }
+        nbuf = WF_LOOKAHEAD;
+    }
+    // this lane's state word in the current window
+    __device__ __forceinline__ int word() const { return b[0]; }
+    __device__ __forceinline__ void advance(const int32_t* __restrict__ state) {
+        win_next += 64;
+#pragma unroll
+        for (int k = 0; k + 1 < WF_LOOKAHEAD; ++k) b[k] = b[k + 1];
+        b[WF_LOOKAHEAD - 1] = -1;
+        if (--nbuf == 0 && win_next < win_end) fill(state);
     }
 };
 
@@ -124,7 +149,7 @@ struct PendT {
 };
 using PendExt = PendT<6, false>;
 using PendShd = PendT<7, true>;
-constexpr int WF_SHADE_LIST_BYTES = 256 * 4;  // k_shadow shade list per wave: 128 path slots + 128 hit slots
+constexpr int WF_SHADE_LIST_BYTES = 384 * 4;  // k_shadow per wave: shade list (128 path + 128 hit slots), retire list (128)
 
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
@@ -176,20 +201,22 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
     return false;
 }
 
-// Retire a finished path: FP64 atomic add of its radiance into the pixel sums (the
-// PixelIntegrator's `color <- color + ...`, Integrators.fs:169); the slot becomes FREE.
-__device__ __forceinline__ void retire(const WfParams& P, int s, double lx, double ly, double lz) {
-    const int64_t pix = P.pixel[s];
-    const int64_t npix = (int64_t)P.width * P.height;
-#ifdef MFX_DIAG_NO_ACCUM_ATOMICS
-    if (lx == 12345.0) P.accum[pix] = lx + ly + lz;
-    P.state[s] = WF_FREE;
-    return;
-#endif
-    if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
-    if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
-    if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
-    P.state[s] = WF_FREE;
+// Retire finished paths: FP64 atomic adds of their radiance into the pixel sums (the
+// PixelIntegrator's `color <- color + ...`, Integrators.fs:169); the slots become FREE. k_shadow
+// lists the slots to retire (radiance in HBM) and flushes 64 at a time with all lanes, so the
+// wait for the memory-side atomics is paid once per 64 paths instead of once per window.
+__device__ __forceinline__ void retire_flush(const WfParams& P, const int* rl, int cnt) {
+    const int lane = lane_id();
+    if (lane < cnt) {
+        const int s = rl[lane];
+        const int64_t pix = P.pixel[s];
+        const int64_t npix = (int64_t)P.width * P.height;
+        const double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
+        if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
+        if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
+        if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
+        P.state[s] = WF_FREE;
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -210,11 +237,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const int tiles_x = (W + 7) >> 3;
     const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
 
-    Scanner sc{0, 0, 0, false};
-    bool paths_left = true;  // wave-uniform: path indices remain in some shard
+    Scanner sc{};
+    bool paths_left = P.alloc != 0;  // wave-uniform: path indices remain in some shard
+    int path_shard = (blockIdx.x * 4 + wave) & (WF_SHARDS - 1);
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
+    bool fresh = false;  // the lane's ray is its path's camera ray
     Trav T{};
     uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
@@ -228,11 +257,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         uint64_t m = __ballot(idle);
         while (m != 0 && !sc.exhausted) {
             if (pend_lo == pend_hi) {
-                if (!sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size)) break;
+                if (!sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) break;
                 if (DG) dg.windows++;
                 // scan a 64-slot window with the whole wave; its FREE slots share one allocation
                 const int j = sc.win_next + lane;
-                const int sj = j < sc.win_end ? P.state[j] : -1;
+                const int sj = sc.word();
                 const bool fr = paths_left && sj == WF_FREE;
                 const uint64_t fm = __ballot(fr);
                 const int nf = __popcll(fm);
@@ -240,19 +269,22 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 int64_t pbase = 0;
                 if (nf) {
                     if (lane == 0) {
-                        // path shard g owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices
+                        // path shard g owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices; a
+                        // wave stays on the last shard that had paths
                         for (int k = 0; k < WF_SHARDS && got == 0; ++k) {
-                            const int g = (blockIdx.x * 4 + wave + k) & (WF_SHARDS - 1);
+                            const int g = (path_shard + k) & (WF_SHARDS - 1);
                             const int64_t lo = P.total * g / WF_SHARDS, hi = P.total * (g + 1) / WF_SHARDS;
                             const unsigned long long c = atomicAdd(P.ctl + WF_CTL_PATH + g, (unsigned long long)nf);
                             if ((int64_t)c < hi - lo) {
                                 pbase = lo + (int64_t)c;
                                 got = (int)min((int64_t)nf, hi - lo - (int64_t)c);
+                                path_shard = g;
                             }
                         }
                     }
                     got = __shfl(got, 0);
                     pbase = __shfl(pbase, 0);
+                    path_shard = __shfl(path_shard, 0);
                     if (got == 0) paths_left = false;
                 }
                 bool take = false;
@@ -284,11 +316,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                             vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
                         o = ld3(CAM.position);
                         d = vnormalize(vsub(target, o));
-                        P.tx[j] = 1.0; P.ty[j] = 1.0; P.tz[j] = 1.0;
-                        P.lx[j] = 0.0; P.ly[j] = 0.0; P.lz[j] = 0.0;
+                        // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH)
                         P.key[j] = key;
-                        P.rn[j] = rn;
-                        P.depth[j] = P.max_depth;
                         P.pixel[j] = (int32_t)pixel;
                         take = true;
                         c_primary++;
@@ -297,21 +326,22 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 const uint64_t cm = __ballot(take);
                 if (take) {
                     const int r = __popcll(cm & lanes_below());
-                    pd.slot[r] = j;
+                    pd.slot[r] = sj == WF_FREE ? (j | (int)0x80000000) : j;  // sign bit: camera ray
                     pd.v[0 * 64 + r] = o.x; pd.v[1 * 64 + r] = o.y; pd.v[2 * 64 + r] = o.z;
                     pd.v[3 * 64 + r] = d.x; pd.v[4 * 64 + r] = d.y; pd.v[5 * 64 + r] = d.z;
                 }
                 wave_lds_sync();
                 pend_lo = 0;
                 pend_hi = __popcll(cm);
-                sc.win_next += 64;
+                sc.advance(P.state);
                 continue;
             }
             const int avail = pend_hi - pend_lo;
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
                 const int e = pend_lo + rank;
-                s = pd.slot[e];
+                s = pd.slot[e] & 0x7fffffff;
+                fresh = pd.slot[e] < 0;
                 trav_begin(T, S, dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            dv(pd.v[3 * 64 + e], pd.v[4 * 64 + e], pd.v[5 * 64 + e]), 99999999.);  // Integrators.fs:108
                 idle = false;
@@ -332,8 +362,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
                 P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
             }
-            P.hit_slot[s] = T.B.found ? (T.B.info & MFX_INFO_SHADE_MASK) : -1;
-            P.state[s] = WF_EXT_DONE;
+            if (T.B.found) P.hit_slot[s] = T.B.info & MFX_INFO_SHADE_MASK;
+            P.state[s] = (T.B.found ? WF_HIT : WF_MISS) | (fresh ? WF_FRESH : 0);
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
@@ -357,7 +387,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_shadow: shade EXT_DONE slots at fetch time, trace the vertex's shadow ray, retire or continue
+// k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, retire or continue
 // ------------------------------------------------------------------------------------------------
 template <bool STATS>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
@@ -371,9 +401,12 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
-    int* shl = (int*)(red + 16) + wave * 256;  // shade list: [0,128) path slots, [128,256) hit slots
-    Scanner sc{0, 0, 0, false};
-    int nshade = 0;  // wave-uniform: hits listed for shading
+    int* shl = (int*)(red + 16) + wave * 384;  // shade list: [0,128) path slots, [128,256) hit slots
+    int* rtl = shl + 256;                       // retire list: [0,128) path slots
+    Scanner sc{};
+    int nshade = 0;   // wave-uniform: hits listed for shading
+    int nretire = 0;  // wave-uniform: finished paths listed for retirement
+    bool fresh = false;  // the lane's vertex is its path's first (radiance 0 in registers only)
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
@@ -391,25 +424,37 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         uint64_t m = __ballot(idle);
         while (m != 0) {
             if (pend_lo == pend_hi) {
-                if (nshade < 64 && !sc.exhausted && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size)) {
+                if (nretire >= 64) {  // 64 finished paths: one round of atomics with all lanes
+                    retire_flush(P, rtl, 64);
+                    const int rest = nretire - 64;
+                    const int mv = lane < rest ? rtl[64 + lane] : 0;
+                    wave_lds_sync();
+                    if (lane < rest) rtl[lane] = mv;
+                    wave_lds_sync();
+                    nretire = rest;
+                }
+                if (nshade < 64 && !sc.exhausted && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
                     if (DG) dg.windows++;
-                    // scan a 64-slot window with the whole wave: retire every miss (TraceRay returns
-                    // black, Integrators.fs:137), append every hit to the wave's shade list
+                    // scan a 64-slot window with the whole wave: a camera ray's miss frees its slot
+                    // (TraceRay returns black, Integrators.fs:137, and nothing was gathered), a later
+                    // miss is listed for retirement, every hit is appended to the shade list
                     const int j = sc.win_next + lane;
-                    int hs = -1;
-                    if (j < sc.win_end && P.state[j] == WF_EXT_DONE) {
-                        hs = P.hit_slot[j];
-                        if (hs < 0) retire(P, j, P.lx[j], P.ly[j], P.lz[j]);
-                    }
-                    const uint64_t hm = __ballot(hs >= 0);
-                    if (hs >= 0) {
+                    const int sj = sc.word();
+                    const bool hit = (sj & ~WF_FRESH) == WF_HIT;
+                    const bool miss = sj == WF_MISS;
+                    if (sj == (WF_MISS | WF_FRESH)) P.state[j] = WF_FREE;
+                    const int hs = hit ? P.hit_slot[j] : -1;
+                    const uint64_t hm = __ballot(hit), mm = __ballot(miss);
+                    if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
-                        shl[r] = j;
+                        shl[r] = (sj & WF_FRESH) ? (j | (int)0x80000000) : j;  // sign bit: first vertex
                         shl[128 + r] = hs;
                     }
+                    if (miss) rtl[nretire + __popcll(mm & lanes_below())] = j;
                     wave_lds_sync();
                     nshade += __popcll(hm);
-                    sc.win_next += 64;
+                    nretire += __popcll(mm);
+                    sc.advance(P.state);
                     continue;
                 }
                 if (nshade == 0) break;  // every chunk scanned, every hit shaded, every ray handed out
@@ -417,7 +462,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
                 const int cnt = nshade < 64 ? nshade : 64;
                 if (lane < cnt) {
-                    const int j = shl[lane];
+                    const int j = shl[lane] & 0x7fffffff;
+                    const bool first = shl[lane] < 0;  // throughput 1, draws 2, depth max_depth implicit
                     const int slot = shl[128 + lane];
                     const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
@@ -425,7 +471,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
                     else nm = ld3(sh.n);
                     const uint64_t key = P.key[j];
-                    uint32_t rn = P.rn[j];
+                    uint32_t rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
                     // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
                     DV p = dv(20, 20, 20);
                     while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
@@ -460,9 +506,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                     const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
                     const double solid = fabs(cos_o) * LT.area / dist2;
                     const double cs = vdot(unit, nm);
-                    const double Tx = P.tx[j] * (TWOPI * (ei * (INVPI * a[0])));
-                    const double Ty = P.ty[j] * (TWOPI * (ei * (INVPI * a[1])));
-                    const double Tz = P.tz[j] * (TWOPI * (ei * (INVPI * a[2])));
+                    double Tx = 1.0, Ty = 1.0, Tz = 1.0;
+                    if (!first) { Tx = P.tx[j]; Ty = P.ty[j]; Tz = P.tz[j]; }
+                    Tx = Tx * (TWOPI * (ei * (INVPI * a[0])));
+                    Ty = Ty * (TWOPI * (ei * (INVPI * a[1])));
+                    Tz = Tz * (TWOPI * (ei * (INVPI * a[2])));
                     // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
                     double dx = 0.0, dy = 0.0, dz = 0.0;
                     if (cos_o < 0.) {
@@ -472,14 +520,14 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                     }
                     P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
                     P.rn[j] = rn;
-                    const int depth = P.depth[j] - 1;
+                    const int depth = (first ? P.max_depth : P.depth[j]) - 1;
                     P.depth[j] = depth;
                     // the depth -1 query's result is discarded (Integrators.fs:109): never traced
                     const bool cn = depth >= 0;
                     if (cn) { P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z; }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
                     pd.slot[lane] = j;
-                    pd.flag[lane] = cn ? 1 : 0;
+                    pd.flag[lane] = (cn ? 1 : 0) | (first ? 2 : 0);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
                     pd.v[4 * 64 + lane] = dx; pd.v[5 * 64 + lane] = dy; pd.v[6 * 64 + lane] = dz;
@@ -502,7 +550,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
             if (idle && rank < avail) {
                 const int e = pend_lo + rank;
                 s = pd.slot[e];
-                cont = pd.flag[e] != 0;
+                cont = (pd.flag[e] & 1) != 0;
+                fresh = (pd.flag[e] & 2) != 0;
                 scx = pd.v[4 * 64 + e]; scy = pd.v[5 * 64 + e]; scz = pd.v[6 * 64 + e];
                 // origin = the hit point k_extend stored (a cache hit: the scan just read it)
                 trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
@@ -527,22 +576,51 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         if (active) fin = trav_step<true, STATS>(T, S, stack, st, dg, DG);
 #endif
         DIAG_MARK(dg, leaf, DG);
+        bool to_retire = false;
         if (fin) {
-            double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
+            double lx = 0.0, ly = 0.0, lz = 0.0;  // a first vertex's radiance so far is 0
+            if (!fresh) { lx = P.lx[s]; ly = P.ly[s]; lz = P.lz[s]; }
             if (!T.B.found) {  // unoccluded: add this vertex's direct-light term
                 lx += scx;
                 ly += scy;
                 lz += scz;
             }
+            const bool store = !T.B.found || fresh;  // the radiance in HBM is stale
             if (cont) {
-                if (!T.B.found) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
+                if (store) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
                 P.state[s] = WF_NEED_EXT;
+            } else if (lx == 0.0 && ly == 0.0 && lz == 0.0) {
+                P.state[s] = WF_FREE;  // nothing to add
             } else {
-                retire(P, s, lx, ly, lz);
+                if (store) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
+                to_retire = true;
             }
             active = false;
         }
+        // list finished paths for retirement (flush first if the list could overflow)
+        const uint64_t rm = __ballot(to_retire);
+        if (rm) {
+            if (nretire >= 64) {
+                retire_flush(P, rtl, 64);
+                const int rest = nretire - 64;
+                const int mv = lane < rest ? rtl[64 + lane] : 0;
+                wave_lds_sync();
+                if (lane < rest) rtl[lane] = mv;
+                wave_lds_sync();
+                nretire = rest;
+            }
+            if (to_retire) rtl[nretire + __popcll(rm & lanes_below())] = s;
+            wave_lds_sync();
+            nretire += __popcll(rm);
+        }
         DIAG_MARK(dg, fin, DG);
+    }
+    // retire what is still listed
+    if (nretire > 64) {
+        retire_flush(P, rtl, 64);
+        retire_flush(P, rtl + 64, nretire - 64);
+    } else if (nretire > 0) {
+        retire_flush(P, rtl, nretire);
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
