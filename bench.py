@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Benchmark: Mrays/s (primary + secondary) of the path-tracing hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): scenes/spot.xml — spot (5,856 triangles)
+Workload (BASELINE.json configs[1]; --config C3/C4/C5 for the others):
+scenes/spot.xml — spot (5,856 triangles)
 on a floor quad under a quad light, 1920x1080, 64 samples per pixel per GPU, maxDepth 3.
 A step = one 64-spp-per-GPU frame: every rank traces its disjoint sample partition into an FP64
 accumulator, then (N > 1) one RCCL sum-reduce of that [3][w*h] buffer to rank 0. Per-GPU work is
@@ -11,10 +12,12 @@ Rays counted = primary + extension (closest-hit queries actually traced) + shado
 from the kernel's own counters. Inputs (scene, BVH) are resident in HBM before timing starts.
 
 Extra objects on the JSON line:
-  roofline      the dominant kernel — k_extend<false>, path start + closest-hit traversal of the
-                wavefront pipeline — algorithmic bytes per launch / its HIP-event duration vs HBM
-                8 TB/s; bytes per ray from the kernel's traversal counters; traffic =
-                PMC HBM bytes per launch (profiles/traffic_spot_1080p.json, scripts/profile_r01.sh)
+  roofline      the dominant kernel of the wavefront pipeline (k_extend<false>: path start +
+                closest-hit traversal; k_shadow<false>: shading + shadow-ray traversal; whichever
+                takes the larger share of the step, the other in `other_kernel`) — algorithmic
+                bytes per launch / its HIP-event duration vs HBM 8 TB/s; bytes per ray frozen in
+                profiles/bray_fixture.json; traffic = PMC HBM bytes per launch
+                (profiles/traffic_<scene>.json, scripts/profile_r01.sh)
   cpu_baseline  the CPU oracle (FP64 restatement of the reference algorithm) timed on this host
                 on a bounded random sample of the same workload's paths (rank 0, N = 1 only)
 """
@@ -33,6 +36,14 @@ sys.path.insert(0, ROOT)
 METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 SPOT_SCENE = os.path.join(ROOT, "scenes", "spot.xml")
+# BASELINE.json configs: scene, spp per GPU per step at N = 1, label. C4 and C5 are
+# 8-GPU configs; at N = 1 a step is one GPU's share of them (256/8 and 512/8 spp).
+CONFIGS = {
+    "C2": ("spot.xml", 64, "C2 spot (5856 tris) + floor/light stage"),
+    "C3": ("cube_cornell.xml", 1024, "C3 Cube (12 tris) in the synthetic Cornell box"),
+    "C4": ("renault.xml", 32, "C4 Renault12TL (36996 tris) + stage, per-GPU share of 256 spp over 8 GPUs"),
+    "C5": ("spot16.xml", 64, "C5 spot x16 flattened (93696 tris) + stage, per-GPU share of 512 spp over 8 GPUs"),
+}
 
 
 def parse():
@@ -40,8 +51,10 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--spp", type=int, default=64, help="samples per pixel per GPU per step")
-    ap.add_argument("--scene", default=SPOT_SCENE)
+    ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
+                    help="BASELINE.json workload (C2 default: the metric's configuration)")
+    ap.add_argument("--spp", type=int, default=None, help="samples per pixel per GPU per step (default: the config's)")
+    ap.add_argument("--scene", default=None, help="scene file (default: the config's)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU-baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the traversal-counter pass")
@@ -84,13 +97,18 @@ def cpu_baseline(arrays, spp, seed, budget_s):
         t_total += st[7]
     o.close()
     return {"value": round(rays / t_total / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
-            "sample": f"{int(paths)} random (pixel, sample) paths of the same 1920x1080x{spp} workload "
+            "sample": f"{int(paths)} random (pixel, sample) paths of the same {arrays.width}x{arrays.height}x{spp} workload "
                       f"({int(rays)} rays, {t_total:.1f} s), oracle/mfx_oracle.c strict FP64 restatement, "
                       f"OpenMP {nthreads} threads"}
 
 
 def main():
     args = parse()
+    cfg_scene, cfg_spp, cfg_label = CONFIGS[args.config]
+    if args.scene is None:
+        args.scene = os.path.join(ROOT, "scenes", cfg_scene)
+    if args.spp is None:
+        args.spp = cfg_spp
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(relaunch_distributed(args))
@@ -196,34 +214,54 @@ def main():
 
         roofline = None
         if stats is not None:
-            if args.megakernel:
-                kname, kms, krays, launches = "trace_kernel<false>", stage_ms["total_ms"], rays / args.steps, 1
-                bray = bytes_per_ray(stats["all"])
-                if fixture:
-                    fc, fs = fixture["closest"], fixture["shadow"]
-                    n_c, n_s = fixture["closest_rays"], fixture["shadow_rays"]
-                    bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
-            else:
-                kname, kms, krays = "k_extend<false>", stage_ms["extend_ms"], closest_rays / args.steps
-                launches = stage_ms["launches"]
-                bray = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
-            # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
-            achieved = krays * bray / (kms / 1e3) / 1e9
-            traffic = None
-            tf = os.path.join(ROOT, "profiles", "traffic_spot_1080p.json")
-            if os.path.exists(tf) and world == 1 and args.spp == 64 and args.scene == SPOT_SCENE:
-                with open(tf) as f:
-                    traffic = json.load(f).get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch")
-            roofline = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            tfile = os.path.join(ROOT, "profiles", f"traffic_{sname}.json")
+            if sname == "spot":
+                tfile = os.path.join(ROOT, "profiles", "traffic_spot_1080p.json")
+            tdata = None
+            if os.path.exists(tfile) and world == 1:
+                with open(tfile) as f:
+                    tdata = json.load(f)
+                if tdata.get("spp", args.spp) != args.spp:
+                    tdata = None  # profiled on another workload
+
+            def kernel_roofline(kname, kms, krays, launches, bray):
+                # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
+                achieved = krays * bray / (kms / 1e3) / 1e9
+                traffic = tdata.get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch") if tdata else None
+                return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                         "kernel": kname, "launches_per_step": launches,
                         "avg_launch_ms": round(kms / launches, 4),
                         "bytes_per_ray": round(bray, 1), "bytes_per_ray_source":
                             "profiles/bray_fixture.json (frozen)" if fixture else "live counters",
-                        "rays_per_launch": round(krays / launches, 1),
-                        "stage_ms": {k: round(v, 3) for k, v in stage_ms.items()},
-                        "counters": {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
-                                         else round(d, 4)) for g, d in stats.items()}}
+                        "rays_per_launch": round(krays / launches, 1)}
+
+            if args.megakernel:
+                bray = bytes_per_ray(stats["all"])
+                if fixture:
+                    fc, fs = fixture["closest"], fixture["shadow"]
+                    n_c, n_s = fixture["closest_rays"], fixture["shadow_rays"]
+                    bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
+                roofline = kernel_roofline("trace_kernel<false>", stage_ms["total_ms"], rays / args.steps, 1, bray)
+            else:
+                # the two wavefront kernels; the roofline object is the one with the larger share of
+                # the step (the dominant kernel), the other is reported beside it
+                launches = stage_ms["launches"]
+                bc = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
+                bs = fixture["shadow"]["B_ray"] if fixture else bytes_per_ray(stats["shadow"])
+                ext = kernel_roofline("k_extend<false>", stage_ms["extend_ms"], closest_rays / args.steps, launches, bc)
+                shd = kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"], (rays - closest_rays) / args.steps,
+                                      launches, bs)
+                dom, other = (shd, ext) if stage_ms["shadow_ms"] > stage_ms["extend_ms"] else (ext, shd)
+                roofline = dict(dom)
+                roofline["other_kernel"] = other
+                step_bytes = (closest_rays * bc + (rays - closest_rays) * bs) / args.steps
+                roofline["step"] = {"achieved": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9, 2),
+                                    "frac": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                                    "note": "both kernels' algorithmic bytes over the whole traced step"}
+            roofline["stage_ms"] = {k: round(v, 3) for k, v in stage_ms.items()}
+            roofline["counters"] = {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
+                                        else round(d, 4)) for g, d in stats.items()}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
@@ -233,8 +271,8 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"C2 spot ({len(arrays.prims) - 1} tris) + floor/light stage, {W}x{H}, "
-                                   f"{args.spp} spp per GPU per step",
+            "config": {"workload": f"{cfg_label}, {W}x{H}, {args.spp} spp per GPU per step",
+                       "baseline_config": args.config,
                        "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
                        "spp_per_gpu": args.spp, "global_spp_per_step": spp_step, "max_depth": 3,
                        "pipeline": "megakernel" if args.megakernel else "wavefront",

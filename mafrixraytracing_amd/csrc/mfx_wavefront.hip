@@ -84,8 +84,25 @@ __device__ __forceinline__ void block_add(unsigned long long* dst, uint32_t v, u
 // Slot windows: a wave takes chunks of P.chunk slots (its block's shard first, then the others)
 // and scans them 64 at a time.
 // ------------------------------------------------------------------------------------------------
+static_assert(WF_SHARDS == 64, "shard masks are one bit per lane of a wave");
+
+// Shards of a sharded counter set that are still open (counter below its capacity), one bit per
+// shard, from one vector load of all 64 counters (lane g reads shard g). Counters only grow, so a
+// stale value can only report a closed shard as open: the caller's atomic then fails and it asks
+// again. This replaces walking the shards with one returning atomic each, which cost every wave
+// up to 64 serialized round trips at the end of each kernel.
+__device__ __forceinline__ uint64_t open_shards(const unsigned long long* ctr, int64_t cap) {
+    const unsigned long long v = __hip_atomic_load(ctr + lane_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __ballot((int64_t)v < cap);
+}
+// the first open shard at or after `home` (cyclically); `open` must be non-zero
+__device__ __forceinline__ int next_open(uint64_t open, int home) {
+    const uint64_t r = home ? ((open >> home) | (open << (64 - home))) : open;
+    return (home + __builtin_ctzll(r)) & (WF_SHARDS - 1);
+}
+
 struct Scanner {
-    int win_next, win_end, shard_try;
+    int win_next, win_end, shard;
     bool exhausted;
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
@@ -93,25 +110,29 @@ struct Scanner {
     // through this wave, so the words stay current.
     int b[WF_LOOKAHEAD];
     int nbuf;
-    // Make [win_next, win_end) non-empty; false once every chunk has been taken.
+    // Make [win_next, win_end) non-empty; false once every chunk has been taken. A wave takes
+    // chunks from its block's home shard while it lasts, then from the next open shard.
     __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
                                            const int32_t* __restrict__ state) {
         if (win_next < win_end) return true;
-        while (shard_try < WF_SHARDS) {
-            const int g = (blockIdx.x + shard_try) & (WF_SHARDS - 1);
+        if (exhausted) return false;
+        while (true) {
             unsigned long long c = 0;
-            if (lane_id() == 0) c = atomicAdd(heads + g, (unsigned long long)chunk);
+            if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
             c = __shfl(c, 0);
             if ((int64_t)c < shard_size) {
-                win_next = g * shard_size + (int)c;
-                win_end = g * shard_size + min((int)c + chunk, shard_size);
+                win_next = shard * shard_size + (int)c;
+                win_end = shard * shard_size + min((int)c + chunk, shard_size);
                 fill(state);
                 return true;
             }
-            ++shard_try;
+            const uint64_t open = open_shards(heads, shard_size);
+            if (open == 0) {
+                exhausted = true;
+                return false;
+            }
+            shard = next_open(open, shard);
         }
-        exhausted = true;
-        return false;
     }
     __device__ __forceinline__ void fill(const int32_t* __restrict__ state) {
 #pragma unroll
@@ -238,8 +259,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
 
     Scanner sc{};
+    sc.shard = blockIdx.x & (WF_SHARDS - 1);
     bool paths_left = P.alloc != 0;  // wave-uniform: path indices remain in some shard
     int path_shard = (blockIdx.x * 4 + wave) & (WF_SHARDS - 1);
+    // path shard g (this lane's g = lane) owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices
+    const int64_t my_plo = P.total * lane / WF_SHARDS, my_pcap = P.total * (lane + 1) / WF_SHARDS - my_plo;
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
@@ -268,23 +292,24 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 int got = 0;
                 int64_t pbase = 0;
                 if (nf) {
-                    if (lane == 0) {
-                        // path shard g owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices; a
-                        // wave stays on the last shard that had paths
-                        for (int k = 0; k < WF_SHARDS && got == 0; ++k) {
-                            const int g = (path_shard + k) & (WF_SHARDS - 1);
-                            const int64_t lo = P.total * g / WF_SHARDS, hi = P.total * (g + 1) / WF_SHARDS;
-                            const unsigned long long c = atomicAdd(P.ctl + WF_CTL_PATH + g, (unsigned long long)nf);
-                            if ((int64_t)c < hi - lo) {
-                                pbase = lo + (int64_t)c;
-                                got = (int)min((int64_t)nf, hi - lo - (int64_t)c);
-                                path_shard = g;
-                            }
+                    // a wave stays on the last shard that had paths; when it runs dry, one vector
+                    // load of the 64 path counters names the next open shard
+                    while (true) {
+                        unsigned long long c = 0;
+                        if (lane == 0) c = atomicAdd(P.ctl + WF_CTL_PATH + path_shard, (unsigned long long)nf);
+                        c = __shfl(c, 0);
+                        const int64_t cap = __shfl(my_pcap, path_shard);
+                        if ((int64_t)c < cap) {
+                            pbase = __shfl(my_plo, path_shard) + (int64_t)c;
+                            got = (int)min((int64_t)nf, cap - (int64_t)c);
+                            break;
                         }
+                        const unsigned long long pc =
+                            __hip_atomic_load(P.ctl + WF_CTL_PATH + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t open = __ballot((int64_t)pc < my_pcap);
+                        if (open == 0) break;
+                        path_shard = next_open(open, path_shard);
                     }
-                    got = __shfl(got, 0);
-                    pbase = __shfl(pbase, 0);
-                    path_shard = __shfl(path_shard, 0);
                     if (got == 0) paths_left = false;
                 }
                 bool take = false;
@@ -404,6 +429,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     int* shl = (int*)(red + 16) + wave * 384;  // shade list: [0,128) path slots, [128,256) hit slots
     int* rtl = shl + 256;                       // retire list: [0,128) path slots
     Scanner sc{};
+    sc.shard = blockIdx.x & (WF_SHARDS - 1);
     int nshade = 0;   // wave-uniform: hits listed for shading
     int nretire = 0;  // wave-uniform: finished paths listed for retirement
     bool fresh = false;  // the lane's vertex is its path's first (radiance 0 in registers only)

@@ -17,4 +17,4 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats "$@" > $OUT/bench_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats "$@" > $OUT/bench_write.log 2>&1
-python3 $R/scripts/summarize_profile.py $OUT
+python3 $R/scripts/summarize_profile.py $OUT "$@"

@@ -28,7 +28,7 @@ def pmc(path, counter):
     return acc
 
 
-def main(d):
+def main(d, bench_args=()):
     stats = one(os.path.join(d, "trace", "**", "*kernel_stats.csv"))
     kern = {}
     if stats:
@@ -46,7 +46,14 @@ def main(d):
         wb = ws * 1024 / wn if wn else 0.0
         out[short] = {"launches_profiled": max(fn, wn), "fetch_bytes_per_launch": fb, "write_bytes_per_launch": wb,
                       "hbm_bytes_per_launch": fb + wb}
-    res = {"kernels": out, "trace": kern,
+    # the bench workload the passes ran (bench.py --config / --spp), so bench.py only pairs this
+    # traffic with the same workload
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from bench import CONFIGS
+    a = list(bench_args)
+    cfg = a[a.index("--config") + 1] if "--config" in a else "C2"
+    spp = int(a[a.index("--spp") + 1]) if "--spp" in a else CONFIGS[cfg][1]
+    res = {"config": cfg, "scene": CONFIGS[cfg][0], "spp": spp, "kernels": out, "trace": kern,
            "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, per launch, from separate --pmc passes"}
     with open(os.path.join(d, "traffic.json"), "w") as f:
         json.dump(res, f, indent=1)
@@ -54,4 +61,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2:])
