@@ -75,7 +75,11 @@ struct mfx_ctx {
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
-    int64_t wf_pool_max = 1 << 25;
+    // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
+    // slots, 17.5 GB) runs the frame as one generation: every iteration is one bounce of every
+    // live path, so no kernel ends with a partly filled pool (+11 % on C2 over 32 M slots). Capped
+    // at 2^28 slots (35 GB of the 288 GB) and at a quarter of the free HBM.
+    int64_t wf_pool_max = 1 << 28;
     int nsub = 1;
     unsigned long long* d_wfctl = nullptr;  // [MFX_MAX_SUB][WF_NCTL]
     unsigned long long* h_pin = nullptr;    // [MFX_MAX_SUB][WF_SHARDS] path counters read back
@@ -175,6 +179,13 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_counters, 16 * WF_SHARDS * sizeof(unsigned long long)));
     CK(hipMalloc((void**)&c->d_wfctl, MFX_MAX_SUB * WF_NCTL * sizeof(unsigned long long)));
     CK(hipHostMalloc((void**)&c->h_pin, MFX_MAX_SUB * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
+    {
+        size_t mfree = 0, mtotal = 0;
+        if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
+            const int64_t fit = (int64_t)(mfree / 4 / (WF_DOUBLES_PER_SLOT * 8 + WF_WORDS_PER_SLOT * 4));
+            c->wf_pool_max = std::max<int64_t>(1 << 20, std::min<int64_t>(c->wf_pool_max, fit));
+        }
+    }
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));

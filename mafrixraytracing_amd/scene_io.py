@@ -209,7 +209,7 @@ def save_npz_mesh(path: str, st: ObjState, mtl: list[tuple[str, tuple]]):
 
 
 def load_npz_mesh(path: str, manager: MaterialManager) -> ObjState:
-    z = np.load(path, allow_pickle=False)
+    z = dict(np.load(path, allow_pickle=False))  # read every member once (NpzFile re-reads per access)
     base = len(manager.materials)
     for ka in z["mtl_ka"]:
         manager.Add(ka)
@@ -218,11 +218,12 @@ def load_npz_mesh(path: str, manager: MaterialManager) -> ObjState:
     names = [str(s) for s in z["group_names"]]
     for g in names:
         st.groups.setdefault(g, [])
-    V = z["vertices"]
-    for f, gi, m in zip(z["faces"], z["face_group"], z["face_mtl"]):
+    V = z["vertices"].tolist()
+    has_mtl = len(z["mtl_ka"]) > 0
+    for f, gi, m in zip(z["faces"].tolist(), z["face_group"].tolist(), z["face_mtl"].tolist()):
         k = 3 if f[3] < 0 else 4
-        pts = tuple(tuple(float(c) for c in V[i]) for i in f[:k])
-        mat = base + int(m) if len(z["mtl_ka"]) else 0
+        pts = tuple(tuple(V[i]) for i in f[:k])
+        mat = base + int(m) if has_mtl else 0
         st.groups[names[gi]].append(Prim(MFX_PRIM_TRIANGLE if k == 3 else MFX_PRIM_RECT, pts, mat))
     return st
 
