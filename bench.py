@@ -178,7 +178,7 @@ def main():
         rays_all = rays
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
                 for k in ("total_ms", "logic_ms", "extend_ms", "shade_ms", "shadow_ms", "iterations", "launches",
-                          "subpools")}
+                          "generations")}
 
     result = None
     if rank == 0:

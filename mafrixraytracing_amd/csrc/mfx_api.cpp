@@ -42,7 +42,6 @@ hipError_t upload(T** dptr, const std::vector<T>& v) {
 }
 }  // namespace
 
-#define MFX_MAX_SUB 4
 
 struct mfx_ctx {
     int device = 0;
@@ -70,25 +69,20 @@ struct mfx_ctx {
     int64_t npix = 0;
     hipEvent_t ev0 = nullptr, ev1 = nullptr;
     bool ev_valid = false;
-    // wavefront pipeline: the slot pool is split into nsub sub-pools, each driven on its own
-    // stream so one sub-pool's traversal tail overlaps another's logic / shade kernels
+    // wavefront pipeline: a frame's paths run in generations of at most wf_pool_max paths
+    // (mfx_wavefront.h), every iteration one bounce of every live path
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
     // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
-    // slots, 17.5 GB) runs the frame as one generation: every iteration is one bounce of every
-    // live path, so no kernel ends with a partly filled pool (+11 % on C2 over 32 M slots). Capped
-    // at 2^28 slots (35 GB of the 288 GB) and at a quarter of the free HBM.
+    // slots, 15 GB) runs the frame as one generation: no kernel ends with a partly filled pool
+    // (+11 % on C2 over 32 M slots). Capped at 2^28 slots (31 GB of the 288 GB) and at a quarter
+    // of the free HBM.
     int64_t wf_pool_max = 1 << 28;
-    int nsub = 1;
-    unsigned long long* d_wfctl = nullptr;  // [MFX_MAX_SUB][WF_NCTL]
-    unsigned long long* h_pin = nullptr;    // [MFX_MAX_SUB][WF_SHARDS] path counters read back
-    hipStream_t sub_stream[MFX_MAX_SUB] = {};
-    hipEvent_t sub_ev[MFX_MAX_SUB][4] = {};  // iteration start, extend|shadow boundary, end, counters copied
-    hipEvent_t fork_ev = nullptr;
-    double stage_ms[4] = {0, 0, 0, 0};
-    int iterations = 0;  // iterations of the longest sub-pool
-    int launches = 0;    // launches per stage kernel, all sub-pools
+    unsigned long long* d_wfctl = nullptr;  // [WF_NCTL] chunk heads
+    std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
+    int it_recorded = 0;                    // iterations of the last trace with events in it_ev
+    int generations = 0;
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
@@ -102,13 +96,8 @@ static void free_ctx(mfx_ctx* c) {
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
-    if (c->h_pin) (void)hipHostFree(c->h_pin);
-    for (auto& evs : c->sub_ev)
-        for (hipEvent_t e : evs)
-            if (e) (void)hipEventDestroy(e);
-    if (c->fork_ev) (void)hipEventDestroy(c->fork_ev);
-    for (hipStream_t st : c->sub_stream)
-        if (st) (void)hipStreamDestroy(st);
+    for (hipEvent_t e : c->it_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -177,8 +166,7 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
     CK(hipMalloc((void**)&c->d_counters, 16 * WF_SHARDS * sizeof(unsigned long long)));
-    CK(hipMalloc((void**)&c->d_wfctl, MFX_MAX_SUB * WF_NCTL * sizeof(unsigned long long)));
-    CK(hipHostMalloc((void**)&c->h_pin, MFX_MAX_SUB * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
+    CK(hipMalloc((void**)&c->d_wfctl, WF_NCTL * sizeof(unsigned long long)));
     {
         size_t mfree = 0, mtotal = 0;
         if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
@@ -189,12 +177,6 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
-    if (const char* ns = getenv("MFX_SUBPOOLS")) c->nsub = std::max(1, std::min(MFX_MAX_SUB, atoi(ns)));
-    CK(hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming));
-    for (int k = 0; k < c->nsub; ++k) {
-        CK(hipStreamCreateWithFlags(&c->sub_stream[k], hipStreamNonBlocking));
-        for (hipEvent_t& e : c->sub_ev[k]) CK(hipEventCreate(&e));
-    }
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
     CK(hipMemset(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long)));
@@ -238,8 +220,6 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     c->wf.key = (uint64_t*)take(P * 8);
     c->wf.rn = (uint32_t*)take(P * 4);
     c->wf.depth = (int32_t*)take(P * 4);
-    c->wf.pixel = (int32_t*)take(P * 4);
-    c->wf.hit_slot = (int32_t*)take(P * 4);
     c->wf.state = (int32_t*)take(P * 4);
     c->wf_pool = pool;
     return MFX_OK;
@@ -256,132 +236,75 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.accum = c->d_accum;
 }
 
-// The wavefront pipeline: logic -> extend -> shade -> shadow per iteration, per sub-pool. Each
-// sub-pool owns a contiguous range of path indices, its control words and a stream; the host
-// feeds whichever sub-pool finished its last iteration (polling events), so the GPU always has
-// another sub-pool's kernels to run during a traversal kernel's tail. Once every path index of a
-// sub-pool has been handed out (its 8 shard counters, read back after each iteration),
-// max_depth more iterations finish and retire its last paths.
+// The wavefront pipeline. The frame's path indices (sample-major, 8x8 tiles) are cut into
+// generations of at most wf_pool_max paths; slot j of a generation holds path path_base + j. A
+// generation is max_depth + 1 iterations of (k_extend, k_shadow) — the primary ray and the
+// max_depth extension rays of PathIntegrator.TraceRay (Integrators.fs:107-137), one bounce of
+// every live path per iteration — then k_resolve adds its finished paths to their pixels. Every
+// launch count is known up front, so the whole call is enqueued without a host round trip.
 static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
-    const int nsub = (int)std::max<int64_t>(1, std::min<int64_t>(c->nsub, total / 65536 + 1));
-    const int64_t sub_max = std::min<int64_t>((total + nsub - 1) / nsub, c->wf_pool_max / c->nsub);
-    const int32_t sub_pool = (int32_t)((sub_max + 2047) / 2048 * 2048);
-    int rc = wf_ensure_pool(c, sub_pool * nsub);
+    const int64_t gen_max = std::min<int64_t>(total, c->wf_pool_max);
+    const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
+    int rc = wf_ensure_pool(c, pool);
     if (rc) return rc;
-    WfParams base = c->wf;
-    fill_scene_params(c, base);
-    base.counters = c->d_counters;
-    base.seed = c->seed;
-    base.sample_base = sample_base;
-    base.part_index = c->part_index;
-    base.part_count = c->part_count;
-    base.width = W;
-    base.height = H;
-    base.max_depth = c->host.max_depth;
-    base.stack_size = c->stack_size;
-    base.chunk = c->wf_chunk;
-    base.alloc = 1;
+    WfParams P = c->wf;
+    fill_scene_params(c, P);
+    P.ctl = c->d_wfctl;
+    P.counters = c->d_counters;
+    P.seed = c->seed;
+    P.sample_base = sample_base;
+    P.part_index = c->part_index;
+    P.part_count = c->part_count;
+    P.width = W;
+    P.height = H;
+    P.max_depth = c->host.max_depth;
+    P.stack_size = c->stack_size;
+    P.chunk = c->wf_chunk;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
-    struct Sub {
-        WfParams P;
-        hipStream_t st;
-        hipEvent_t* ev;
-        unsigned long long* pin;
-        int drain, iters;
-        bool done;
-    };
-    Sub sub[MFX_MAX_SUB];
-    HIPCHECK(hipEventRecord(c->ev0, c->stream));
-    HIPCHECK(hipEventRecord(c->fork_ev, c->stream));
-    for (int k = 0; k < nsub; ++k) {
-        Sub& u = sub[k];
-        u.P = mfx_wf_slice(base, k * sub_pool, sub_pool);
-        u.P.ctl = c->d_wfctl + k * WF_NCTL;
-        u.P.path_base = total * k / nsub;
-        u.P.total = total * (k + 1) / nsub - u.P.path_base;
-        u.st = c->sub_stream[k];
-        u.ev = c->sub_ev[k];
-        u.pin = c->h_pin + k * WF_SHARDS;
-        u.drain = -1;
-        u.iters = 0;
-        u.done = false;
-        HIPCHECK(hipStreamWaitEvent(u.st, c->fork_ev, 0));
-        HIPCHECK(hipMemsetAsync(u.P.state, 0, sizeof(int32_t) * (size_t)sub_pool, u.st));
-        HIPCHECK(hipMemsetAsync(u.P.ctl, 0, WF_NCTL * sizeof(unsigned long long), u.st));
+    const int64_t ngen = (total + gen_max - 1) / gen_max;
+    const int iters = (int)ngen * (P.max_depth + 1);
+    while ((int)c->it_ev.size() < 3 * iters) {
+        hipEvent_t e;
+        HIPCHECK(hipEventCreate(&e));
+        c->it_ev.push_back(e);
     }
-    auto enqueue = [&](Sub& u) -> int {
-        u.P.alloc = u.drain < 0 ? 1 : 0;  // draining: no path indices left, skip the allocation atomics
-        HIPCHECK(hipEventRecord(u.ev[0], u.st));
-        HIPCHECK(mfx_wf_iteration(u.P, c->wf_ext_grid, c->wf_shd_grid, stats, u.st, u.ev + 1));
-        HIPCHECK(hipEventRecord(u.ev[2], u.st));
-        if (u.drain < 0)
-            HIPCHECK(hipMemcpyAsync(u.pin, u.P.ctl + WF_CTL_PATH, WF_SHARDS * sizeof(unsigned long long),
-                                    hipMemcpyDeviceToHost, u.st));
-        HIPCHECK(hipEventRecord(u.ev[3], u.st));
-        ++u.iters;
-        return MFX_OK;
-    };
-    double stage_ms[4] = {0, 0, 0, 0};
-    int iters = 0;
-    for (int k = 0; k < nsub; ++k)
-        if ((rc = enqueue(sub[k]))) return rc;
-    int live = nsub;
-    while (live > 0) {
-        bool progressed = false;
-        for (int k = 0; k < nsub; ++k) {
-            Sub& u = sub[k];
-            if (u.done) continue;
-            const hipError_t q = hipEventQuery(u.ev[3]);
-            if (q == hipErrorNotReady) continue;
-            HIPCHECK(q);
-            progressed = true;
-            for (int s = 0; s < 2; ++s) {
-                float f = 0.f;
-                HIPCHECK(hipEventElapsedTime(&f, u.ev[s], u.ev[s + 1]));
-                stage_ms[1 + 2 * s] += f;  // [1] extend, [3] shade + shadow
-            }
+    HIPCHECK(hipEventRecord(c->ev0, c->stream));
+    int it = 0;
+    for (int64_t g = 0; g < ngen; ++g) {
+        P.path_base = g * gen_max;
+        P.total = std::min<int64_t>(gen_max, total - P.path_base);
+        P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
+        HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
+        for (int d = 0; d <= P.max_depth; ++d, ++it) {
+            P.start = d == 0 ? 1 : 0;
+            hipEvent_t* ev = c->it_ev.data() + 3 * it;
+            HIPCHECK(hipEventRecord(ev[0], c->stream));
+            HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, ev + 1));
+            HIPCHECK(hipEventRecord(ev[2], c->stream));
             if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
+                HIPCHECK(hipStreamSynchronize(c->stream));
                 unsigned long long h[16 * WF_SHARDS];
                 HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
                 double r[16] = {0};
-                for (int g = 0; g < WF_SHARDS; ++g)
-                    for (int q = 0; q < 16; ++q) r[q] += (double)h[16 * g + q];
+                for (int k = 0; k < WF_SHARDS; ++k)
+                    for (int q = 0; q < 16; ++q) r[q] += (double)h[16 * k + q];
                 float fe = 0.f, fs = 0.f;
-                HIPCHECK(hipEventElapsedTime(&fe, u.ev[0], u.ev[1]));
-                HIPCHECK(hipEventElapsedTime(&fs, u.ev[1], u.ev[2]));
-                fprintf(stderr, "iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
-                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g\n",
-                        u.iters, r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15]);
+                HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
+                HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
+                fprintf(stderr, "gen %lld iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
+                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g\n", (long long)g, d + 1,
+                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15]);
             }
-            if (u.drain < 0) {
-                bool all = true;
-                for (int g = 0; g < WF_SHARDS; ++g)
-                    if ((int64_t)u.pin[g] < u.P.total * (g + 1) / WF_SHARDS - u.P.total * g / WF_SHARDS) all = false;
-                if (all) u.drain = u.P.max_depth;  // no path of this sub-pool starts after this iteration
-            } else {
-                --u.drain;
-            }
-            if (u.drain == 0) {  // every path of this sub-pool has been retired
-                HIPCHECK(hipStreamWaitEvent(c->stream, u.ev[3], 0));
-                u.done = true;
-                --live;
-                iters = std::max(iters, u.iters);
-                continue;
-            }
-            if (u.iters > 10000000) return fail(MFX_E_STATE, "wavefront pipeline did not drain");
-            if ((rc = enqueue(u))) return rc;
         }
-        if (!progressed) std::this_thread::yield();
+        HIPCHECK(mfx_wf_resolve(P, c->stream));
     }
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
-    for (int k = 0; k < 4; ++k) c->stage_ms[k] = stage_ms[k];
-    c->iterations = iters;
-    c->launches = 0;
-    for (int k = 0; k < nsub; ++k) c->launches += sub[k].iters;
+    c->it_recorded = iters;
+    c->generations = (int)ngen;
     return MFX_OK;
 }
 
@@ -436,10 +359,19 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
         out[5] = 1;
         out[6] = 1;
     } else {
-        for (int k = 0; k < 4; ++k) out[1 + k] = c->stage_ms[k];
-        out[5] = c->iterations;
-        out[6] = c->launches;
-        out[7] = c->nsub;
+        // [2] k_extend, [4] k_shadow (+ memset), summed over iterations; [1], [3] unused (no
+        // separate logic / shade stages); the resolve launches make up the rest of [0]
+        for (int it = 0; it < c->it_recorded; ++it) {
+            const hipEvent_t* ev = c->it_ev.data() + 3 * it;
+            float fe = 0.f, fs = 0.f;
+            HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
+            HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
+            out[2] += fe;
+            out[4] += fs;
+        }
+        out[5] = c->it_recorded;
+        out[6] = c->it_recorded;
+        out[7] = c->generations;
     }
     return MFX_OK;
 }

@@ -1,13 +1,19 @@
 // mfx_wavefront.h — path-slot pool (SoA in HBM) of the wavefront pipeline.
 //
-// Each slot carries one path through a three-state machine; each kernel scans the pool for the
-// slots in its state, so no ray queue (and no hot queue-tail atomic) exists:
-//   FREE | NEED_EXT -(k_extend: camera ray or extension ray, closest hit)-> HIT | MISS (| FRESH)
-//   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, or FREE once the path is retired
-//   MISS -(k_shadow)-> FREE (retired; a FRESH miss adds nothing)
-// The only atomics are per-wave chunk fetches and path allocations, spread over WF_SHARDS
-// counters (a returning atomic on one word saturates near 88 per microsecond), and the FP64
-// adds of finished paths into the pixel accumulator.
+// A frame's paths run in generations of at most `pool` paths: slot j of a generation holds path
+// path_base + j for the generation's whole life, so no slot is recycled and nothing needs a path
+// counter. A generation is max_depth + 1 iterations of (k_extend, k_shadow) — one bounce of every
+// live path per iteration — and then k_resolve, which adds each pixel's finished paths into the
+// accumulator in sample order (no FP64 atomics; the image is run-to-run deterministic).
+//
+// Each slot carries its path through a state machine; each kernel scans the pool for the slots
+// in its state, so no ray queue (and no hot queue-tail atomic) exists:
+//   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
+//   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (radiance in lx..lz) or FREE (black)
+//   MISS -(k_shadow)-> DONE, or FREE for a camera ray's miss
+// A HIT state word also carries the hit's shade[] index, so the shading needs no extra lookup.
+// The only atomics are per-wave chunk fetches, spread over WF_SHARDS counters (a returning
+// atomic on one word saturates near 88 per microsecond).
 #ifndef MFX_WAVEFRONT_H
 #define MFX_WAVEFRONT_H
 
@@ -18,10 +24,13 @@
 
 #define WF_FREE 0
 #define WF_NEED_EXT 1
-#define WF_HIT 2    // k_extend found a hit: hit point (ox..oz) and hit_slot are written
+#define WF_HIT 2    // k_extend found a hit: hit point in ox..oz, shade index in the state word
 #define WF_MISS 3   // k_extend found no hit
 #define WF_FRESH 4  // flag on WF_HIT / WF_MISS: the path's camera ray. Its throughput (1), radiance
                     // (0), draw count (2) and depth (max_depth) are implicit: never stored
+#define WF_DONE 8   // finished with radiance in lx..lz: k_resolve adds it to its pixel
+#define WF_STATE_MASK 15
+#define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
 
 #ifndef WF_SHARDS
 #define WF_SHARDS 64  // returning atomics on one word serialize (~88 per us): 8 shards -> 64 is +13 % on C2
@@ -31,10 +40,9 @@
 #define WF_LOOKAHEAD 4  // windows whose state words a scan loads in one round
 #endif
 // control words (unsigned long long) in WfParams.ctl
-#define WF_CTL_PATH 0                 // [WF_SHARDS] path counters, shard g owns [g*T/S, (g+1)*T/S)
-#define WF_CTL_EXT (WF_SHARDS)        // [WF_SHARDS] k_extend slot-chunk heads
-#define WF_CTL_SHD (2 * WF_SHARDS)    // [WF_SHARDS] k_shadow slot-chunk heads
-#define WF_NCTL (3 * WF_SHARDS)
+#define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
+#define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
+#define WF_NCTL (2 * WF_SHARDS)
 
 struct WfParams {
     // scene
@@ -54,34 +62,31 @@ struct WfParams {
     uint64_t* key;         // RNG key of the path
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)
-    int32_t* pixel;        // x-major pixel index
-    int32_t* hit_slot;     // shade[] slot of the closest hit, -1 = miss
     int32_t* state;
     // control
     unsigned long long* ctl;              // [WF_NCTL]
     unsigned long long* counters;         // [WF_SHARDS][16] ray / traversal counters
-    int64_t total;                        // path indices of this sub-pool (incl. padding of edge tiles)
-    int64_t path_base;                    // first path index of this sub-pool
+    int64_t total;                        // paths of this generation (edge-tile padding included)
+    int64_t path_base;                    // first path index of this generation
     uint64_t seed;
     int64_t sample_base;
     int32_t part_index, part_count;
-    int32_t pool;
+    int32_t pool;                         // slots scanned (>= total, a multiple of 64)
     int32_t width, height, max_depth;
     int32_t stack_size;
     int32_t chunk;                        // slots per chunk fetch of the kernels
-    int32_t alloc;                        // 1 while path indices remain to be handed out
+    int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool
 #define WF_DOUBLES_PER_SLOT 13  // o, d, throughput, radiance (12) + key
-#define WF_WORDS_PER_SLOT 5     // rn, depth, pixel, hit_slot, state
-
-// P with every SoA slot array advanced by `first` slots (a sub-pool of `n` slots)
-WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n);
+#define WF_WORDS_PER_SLOT 3     // rn, depth, state
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);
+// after a generation's last iteration: add its finished paths' radiance to their pixels
+hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st);
 
 #endif

@@ -1,23 +1,25 @@
 // mfx_wavefront.hip — wavefront path tracing on gfx950: the integrator loop
 // (Integrators.fs:107-137, 161-172) as two persistent kernels per iteration over a pool of
-// path slots:
+// path slots, one bounce of every live path per iteration (mfx_wavefront.h):
 //
-//   k_extend   bvh.Hit(ray, 1e-6, 99999999.) (Integrators.fs:108) for NEED_EXT slots; FREE slots
-//              first take a new path index (PixelIntegrator.Sample + PinholeCamera.GetRay,
-//              Integrators.fs:161-169, Camera.fs:134-139). Writes the hit point and hit slot.
-//   k_shadow   one vertex of PathIntegrator.TraceRay for EXT_DONE slots: LambertianBrdf.SampleF,
+//   k_extend   bvh.Hit(ray, 1e-6, 99999999.) (Integrators.fs:108) for NEED_EXT slots; in a
+//              generation's first iteration every FREE slot j starts path path_base + j
+//              (PixelIntegrator.Sample + PinholeCamera.GetRay, Integrators.fs:161-169,
+//              Camera.fs:134-139). Writes the hit point and the hit's shade index.
+//   k_shadow   one vertex of PathIntegrator.TraceRay for HIT slots: LambertianBrdf.SampleF,
 //              NewAreaLight.Sample_Li and the throughput update (Integrators.fs:110-136), then
-//              the vertex's shadow ray (Integrators.fs:44) traced by the same lane; unoccluded ->
-//              L += direct term. Finished paths (miss, or depth exhausted) are retired here: an
-//              FP64 atomic add of L into the pixel sums, and the slot is FREE again.
+//              the vertex's shadow ray (Integrators.fs:44) traced by a lane of the same wave;
+//              unoccluded -> L += direct term. Finished paths keep their radiance in the slot.
+//   k_resolve  after a generation: each pixel's finished paths added to the accumulator in
+//              sample order (PixelIntegrator's `color <- color + ...`, Integrators.fs:169).
 //
-// Both kernels keep lanes busy: a lane that finishes its ray takes the next pending ray at the
-// next step (persistent while-while with dynamic fetch, Aila & Laine 2009). Pending rays come
-// from scanning 64-slot windows with the whole wave: lane j handles slot win+j (coalesced SoA
-// loads), does that slot's non-traversal work with all 64 lanes — the camera ray of a new path,
-// or the shading of a hit — and the rays to trace are compacted (ballot + popcount ranks) into a
-// 64-entry LDS list per wave, with their origin / direction / tmax / direct term, so a ray never
-// round-trips through HBM between its generation and its traversal. Path state lives in HBM as
+// Both trace kernels keep lanes busy: a lane that finishes its ray takes the next pending ray at
+// the next step (persistent while-while with dynamic fetch, Aila & Laine 2009). Pending rays come
+// from scanning 64-slot windows with the whole wave: only the state words are read (several
+// windows per memory round trip, WF_LOOKAHEAD), the slots to work on are compacted (ballot +
+// popcount ranks) into a per-wave LDS list, and the per-slot data is loaded by the lane that takes
+// the entry. k_shadow shades 64 listed hits at a time with all lanes and hands the shadow rays to
+// the traversal in LDS, so a shadow ray never round-trips through HBM. Path state lives in HBM as
 // SoA FP64; every arithmetic step is the same FP64 expression as the megakernel and the oracle.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -153,25 +155,6 @@ struct Scanner {
     }
 };
 
-// Per-wave LDS list of pending rays: slot index, (k_shadow) a flag word, and ND doubles per entry,
-// each field a 64-entry column (conflict-free). k_extend: origin + direction (6 doubles);
-// k_shadow: direction, tmax and the vertex's direct term (7).
-template <int ND, bool FLAG>
-struct PendT {
-    static constexpr int BYTES = 64 * (4 + (FLAG ? 4 : 0) + 8 * ND);
-    int* slot;
-    int* flag;
-    double* v;  // v[f * 64 + entry]
-    __device__ __forceinline__ PendT(uint8_t* base) {
-        slot = (int*)base;
-        flag = slot + 64;
-        v = (double*)(base + (FLAG ? 512 : 256));
-    }
-};
-using PendExt = PendT<6, false>;
-using PendShd = PendT<7, true>;
-constexpr int WF_SHADE_LIST_BYTES = 384 * 4;  // k_shadow per wave: shade list (128 path + 128 hit slots), retire list (128)
-
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
     DV o, d;
@@ -222,26 +205,39 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
     return false;
 }
 
-// Retire finished paths: FP64 atomic adds of their radiance into the pixel sums (the
-// PixelIntegrator's `color <- color + ...`, Integrators.fs:169); the slots become FREE. k_shadow
-// lists the slots to retire (radiance in HBM) and flushes 64 at a time with all lanes, so the
-// wait for the memory-side atomics is paid once per 64 paths instead of once per window.
-__device__ __forceinline__ void retire_flush(const WfParams& P, const int* rl, int cnt) {
-    const int lane = lane_id();
-    if (lane < cnt) {
-        const int s = rl[lane];
-        const int64_t pix = P.pixel[s];
-        const int64_t npix = (int64_t)P.width * P.height;
-        const double lx = P.lx[s], ly = P.ly[s], lz = P.lz[s];
-        if (lx != 0.0) unsafeAtomicAdd(P.accum + pix, lx);
-        if (ly != 0.0) unsafeAtomicAdd(P.accum + npix + pix, ly);
-        if (lz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pix, lz);
-        P.state[s] = WF_FREE;
-    }
+// Path index of this generation -> (sample, 8x8 pixel tile, pixel), sample-major and
+// tile-coherent. False for the padding indices of edge tiles (no path).
+__device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x, int& y, int64_t& smp) {
+    const int tiles_x = (P.width + 7) >> 3;
+    const int64_t per_sample = (int64_t)tiles_x * ((P.height + 7) >> 3) * 64;
+    smp = p / per_sample;
+    const int64_t q = p - smp * per_sample;
+    const int64_t tile = q >> 6;
+    const int within = (int)(q & 63);
+    x = (int)(tile % tiles_x) * 8 + (within & 7);
+    y = (int)(tile / tiles_x) * 8 + (within >> 3);
+    return x < P.width && y < P.height;
 }
 
+#define WF_EXT_PEND 128  // k_extend per-wave pending list: slot indices (sign bit: camera ray)
+#define WF_SHD_LIST 128  // k_shadow per-wave shade list entries
+
+// Per-wave LDS list of k_shadow's pending shadow rays: slot index, a flag word and 7 doubles
+// (direction, tmax, the vertex's direct term), each field a 64-entry column (conflict-free).
+struct PendShd {
+    static constexpr int BYTES = 64 * (4 + 4 + 8 * 7);
+    int* slot;
+    int* flag;
+    double* v;  // v[f * 64 + entry]
+    __device__ __forceinline__ PendShd(uint8_t* base) {
+        slot = (int*)base;
+        flag = slot + 64;
+        v = (double*)(base + 512);
+    }
+};
+
 // ------------------------------------------------------------------------------------------------
-// k_extend: closest hit for NEED_EXT slots; FREE slots start new paths
+// k_extend: closest hit for NEED_EXT slots; in a generation's first iteration FREE slots start paths
 // ------------------------------------------------------------------------------------------------
 template <bool STATS>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
@@ -249,21 +245,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
-    const PendExt pd(pend_base + wave * PendExt::BYTES);
-    uint32_t* red = (uint32_t*)(pend_base + 4 * PendExt::BYTES);
+    int* pend = lds + 4 * P.stack_size * 64 + wave * WF_EXT_PEND;
+    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_size * 64 + 4 * WF_EXT_PEND);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
-    const int W = P.width, H = P.height;
-    const int tiles_x = (W + 7) >> 3;
-    const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
 
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    bool paths_left = P.alloc != 0;  // wave-uniform: path indices remain in some shard
-    int path_shard = (blockIdx.x * 4 + wave) & (WF_SHARDS - 1);
-    // path shard g (this lane's g = lane) owns [g*T/S, (g+1)*T/S) of this sub-pool's path indices
-    const int64_t my_plo = P.total * lane / WF_SHARDS, my_pcap = P.total * (lane + 1) / WF_SHARDS - my_plo;
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
@@ -279,96 +267,62 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         // ---- dynamic fetch: idle lanes take pending rays by rank ----
         bool idle = !active;
         uint64_t m = __ballot(idle);
-        while (m != 0 && !sc.exhausted) {
+        while (m != 0) {
             if (pend_lo == pend_hi) {
-                if (!sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) break;
-                if (DG) dg.windows++;
-                // scan a 64-slot window with the whole wave; its FREE slots share one allocation
-                const int j = sc.win_next + lane;
-                const int sj = sc.word();
-                const bool fr = paths_left && sj == WF_FREE;
-                const uint64_t fm = __ballot(fr);
-                const int nf = __popcll(fm);
-                int got = 0;
-                int64_t pbase = 0;
-                if (nf) {
-                    // a wave stays on the last shard that had paths; when it runs dry, one vector
-                    // load of the 64 path counters names the next open shard
-                    while (true) {
-                        unsigned long long c = 0;
-                        if (lane == 0) c = atomicAdd(P.ctl + WF_CTL_PATH + path_shard, (unsigned long long)nf);
-                        c = __shfl(c, 0);
-                        const int64_t cap = __shfl(my_pcap, path_shard);
-                        if ((int64_t)c < cap) {
-                            pbase = __shfl(my_plo, path_shard) + (int64_t)c;
-                            got = (int)min((int64_t)nf, cap - (int64_t)c);
-                            break;
-                        }
-                        const unsigned long long pc =
-                            __hip_atomic_load(P.ctl + WF_CTL_PATH + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t open = __ballot((int64_t)pc < my_pcap);
-                        if (open == 0) break;
-                        path_shard = next_open(open, path_shard);
+                // list at least 64 slots to trace (or all that are left) from as many windows as it
+                // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
+                int n = 0;
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
+                    if (DG) dg.windows++;
+                    const int j = sc.win_next + lane;
+                    const int sj = sc.word();
+                    bool take = sj == WF_NEED_EXT;
+                    if (P.start && sj == WF_FREE && j < P.total) {
+                        int x, y;
+                        int64_t smp;
+                        take = path_pixel(P, P.path_base + j, x, y, smp);  // edge-tile padding: no path
                     }
-                    if (got == 0) paths_left = false;
-                }
-                bool take = false;
-                DV o = dv(0, 0, 0), d = dv(0, 0, 0);
-                if (sj == WF_NEED_EXT) {
-                    o = dv(P.ox[j], P.oy[j], P.oz[j]);
-                    d = dv(P.dx[j], P.dy[j], P.dz[j]);
-                    take = true;
-                    c_ext++;
-                } else if (fr && __popcll(fm & lanes_below()) < got) {
-                    // new path: index -> (sample, 8x8 tile, pixel), sample-major, tile-coherent
-                    const int64_t p = P.path_base + pbase + __popcll(fm & lanes_below());
-                    const int64_t smp = p / per_sample;
-                    const int64_t q = p - smp * per_sample;
-                    const int64_t tile = q >> 6;
-                    const int within = (int)(q & 63);
-                    const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-                    const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
-                    if (x < W && y < H) {  // edge-tile padding indices start no path
-                        const MfxCamera& CAM = P.cam;
-                        const int64_t pixel = (int64_t)x * H + y;  // Color[w,h] x-major
-                        const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
-                        const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
-                        uint32_t rn = 0;
-                        // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
-                        const double u = ((double)x + rng_next(key, rn)) / (double)W;
-                        const double v = ((double)y + rng_next(key, rn)) / (double)H;
-                        const DV target =
-                            vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
-                        o = ld3(CAM.position);
-                        d = vnormalize(vsub(target, o));
-                        // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH)
-                        P.key[j] = key;
-                        P.pixel[j] = (int32_t)pixel;
-                        take = true;
-                        c_primary++;
-                    }
-                }
-                const uint64_t cm = __ballot(take);
-                if (take) {
-                    const int r = __popcll(cm & lanes_below());
-                    pd.slot[r] = sj == WF_FREE ? (j | (int)0x80000000) : j;  // sign bit: camera ray
-                    pd.v[0 * 64 + r] = o.x; pd.v[1 * 64 + r] = o.y; pd.v[2 * 64 + r] = o.z;
-                    pd.v[3 * 64 + r] = d.x; pd.v[4 * 64 + r] = d.y; pd.v[5 * 64 + r] = d.z;
+                    const uint64_t tm = __ballot(take);
+                    if (take) pend[n + __popcll(tm & lanes_below())] = sj == WF_FREE ? (j | (int)0x80000000) : j;
+                    n += __popcll(tm);
+                    sc.advance(P.state);
                 }
                 wave_lds_sync();
                 pend_lo = 0;
-                pend_hi = __popcll(cm);
-                sc.advance(P.state);
-                continue;
+                pend_hi = n;
+                if (n == 0) break;  // every chunk scanned
             }
             const int avail = pend_hi - pend_lo;
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
-                const int e = pend_lo + rank;
-                s = pd.slot[e] & 0x7fffffff;
-                fresh = pd.slot[e] < 0;
-                trav_begin(T, S, dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
-                           dv(pd.v[3 * 64 + e], pd.v[4 * 64 + e], pd.v[5 * 64 + e]), 99999999.);  // Integrators.fs:108
+                const int e = pend[pend_lo + rank];
+                s = e & 0x7fffffff;
+                fresh = e < 0;
+                DV o, d;
+                if (fresh) {
+                    // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
+                    int x, y;
+                    int64_t smp;
+                    path_pixel(P, P.path_base + s, x, y, smp);
+                    const int64_t pixel = (int64_t)x * P.height + y;  // Color[w,h] x-major
+                    const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
+                    const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
+                    uint32_t rn = 0;
+                    const double u = ((double)x + rng_next(key, rn)) / (double)P.width;
+                    const double v = ((double)y + rng_next(key, rn)) / (double)P.height;
+                    const MfxCamera& CAM = P.cam;
+                    const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
+                    o = ld3(CAM.position);
+                    d = vnormalize(vsub(target, o));
+                    // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH)
+                    P.key[s] = key;
+                    c_primary++;
+                } else {
+                    o = dv(P.ox[s], P.oy[s], P.oz[s]);
+                    d = dv(P.dx[s], P.dy[s], P.dz[s]);
+                    c_ext++;
+                }
+                trav_begin(T, S, o, d, 99999999.);  // Integrators.fs:108
                 idle = false;
                 active = true;
             }
@@ -383,12 +337,14 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         if (active) fin = trav_step<false, STATS>(T, S, stack, st, dg, DG);
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
+            const int fl = fresh ? WF_FRESH : 0;
             if (T.B.found) {
                 const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
                 P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
+                P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
+            } else {
+                P.state[s] = WF_MISS | fl;
             }
-            if (T.B.found) P.hit_slot[s] = T.B.info & MFX_INFO_SHADE_MASK;
-            P.state[s] = (T.B.found ? WF_HIT : WF_MISS) | (fresh ? WF_FRESH : 0);
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
@@ -412,7 +368,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, retire or continue
+// k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
 template <bool STATS>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
@@ -426,12 +382,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
-    int* shl = (int*)(red + 16) + wave * 384;  // shade list: [0,128) path slots, [128,256) hit slots
-    int* rtl = shl + 256;                       // retire list: [0,128) path slots
+    int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    int nshade = 0;   // wave-uniform: hits listed for shading
-    int nretire = 0;  // wave-uniform: finished paths listed for retirement
+    int nshade = 0;      // wave-uniform: hits listed for shading
     bool fresh = false;  // the lane's vertex is its path's first (radiance 0 in registers only)
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
@@ -450,39 +404,27 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         uint64_t m = __ballot(idle);
         while (m != 0) {
             if (pend_lo == pend_hi) {
-                if (nretire >= 64) {  // 64 finished paths: one round of atomics with all lanes
-                    retire_flush(P, rtl, 64);
-                    const int rest = nretire - 64;
-                    const int mv = lane < rest ? rtl[64 + lane] : 0;
-                    wave_lds_sync();
-                    if (lane < rest) rtl[lane] = mv;
-                    wave_lds_sync();
-                    nretire = rest;
-                }
-                if (nshade < 64 && !sc.exhausted && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
+                // list hits from as many windows as it takes (state words only): a camera ray's miss
+                // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
+                // its path with the radiance already in the slot
+                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
                     if (DG) dg.windows++;
-                    // scan a 64-slot window with the whole wave: a camera ray's miss frees its slot
-                    // (TraceRay returns black, Integrators.fs:137, and nothing was gathered), a later
-                    // miss is listed for retirement, every hit is appended to the shade list
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
-                    const bool hit = (sj & ~WF_FRESH) == WF_HIT;
-                    const bool miss = sj == WF_MISS;
-                    if (sj == (WF_MISS | WF_FRESH)) P.state[j] = WF_FREE;
-                    const int hs = hit ? P.hit_slot[j] : -1;
-                    const uint64_t hm = __ballot(hit), mm = __ballot(miss);
+                    const int sv = sj & WF_STATE_MASK;
+                    const bool hit = (sv & ~WF_FRESH) == WF_HIT;
+                    if (sv == (WF_MISS | WF_FRESH)) P.state[j] = WF_FREE;
+                    else if (sv == WF_MISS) P.state[j] = WF_DONE;
+                    const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
-                        shl[r] = (sj & WF_FRESH) ? (j | (int)0x80000000) : j;  // sign bit: first vertex
-                        shl[128 + r] = hs;
+                        shl[r] = (sv & WF_FRESH) ? (j | (int)0x80000000) : j;  // sign bit: first vertex
+                        shl[WF_SHD_LIST + r] = (int)((unsigned)sj >> WF_SHADE_SHIFT);
                     }
-                    if (miss) rtl[nretire + __popcll(mm & lanes_below())] = j;
-                    wave_lds_sync();
                     nshade += __popcll(hm);
-                    nretire += __popcll(mm);
                     sc.advance(P.state);
-                    continue;
                 }
+                wave_lds_sync();
                 if (nshade == 0) break;  // every chunk scanned, every hit shaded, every ray handed out
                 // ---- shade up to 64 listed hits with all lanes: one vertex of PathIntegrator.TraceRay
                 //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
@@ -490,7 +432,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 if (lane < cnt) {
                     const int j = shl[lane] & 0x7fffffff;
                     const bool first = shl[lane] < 0;  // throughput 1, draws 2, depth max_depth implicit
-                    const int slot = shl[128 + lane];
+                    const int slot = shl[WF_SHD_LIST + lane];
                     const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
                     DV nm;
@@ -544,13 +486,15 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                         dy = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
                         dz = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
                     }
-                    P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
-                    P.rn[j] = rn;
                     const int depth = (first ? P.max_depth : P.depth[j]) - 1;
-                    P.depth[j] = depth;
                     // the depth -1 query's result is discarded (Integrators.fs:109): never traced
                     const bool cn = depth >= 0;
-                    if (cn) { P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z; }
+                    if (cn) {  // what the next vertex reads
+                        P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
+                        P.rn[j] = rn;
+                        P.depth[j] = depth;
+                        P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
+                    }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
                     pd.slot[lane] = j;
                     pd.flag[lane] = (cn ? 1 : 0) | (first ? 2 : 0);
@@ -562,9 +506,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 // the unshaded rest of the list moves to its front
                 const int rest = nshade - cnt;
                 int mv_j = 0, mv_s = 0;
-                if (lane < rest) { mv_j = shl[cnt + lane]; mv_s = shl[128 + cnt + lane]; }
+                if (lane < rest) { mv_j = shl[cnt + lane]; mv_s = shl[WF_SHD_LIST + cnt + lane]; }
                 wave_lds_sync();
-                if (lane < rest) { shl[lane] = mv_j; shl[128 + lane] = mv_s; }
+                if (lane < rest) { shl[lane] = mv_j; shl[WF_SHD_LIST + lane] = mv_s; }
                 wave_lds_sync();
                 nshade = rest;
                 pend_lo = 0;
@@ -579,7 +523,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 cont = (pd.flag[e] & 1) != 0;
                 fresh = (pd.flag[e] & 2) != 0;
                 scx = pd.v[4 * 64 + e]; scy = pd.v[5 * 64 + e]; scz = pd.v[6 * 64 + e];
-                // origin = the hit point k_extend stored (a cache hit: the scan just read it)
+                // origin = the hit point k_extend stored (a cache hit: the shading just read it)
                 trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            pd.v[3 * 64 + e]);
                 idle = false;
@@ -602,7 +546,6 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
         if (active) fin = trav_step<true, STATS>(T, S, stack, st, dg, DG);
 #endif
         DIAG_MARK(dg, leaf, DG);
-        bool to_retire = false;
         if (fin) {
             double lx = 0.0, ly = 0.0, lz = 0.0;  // a first vertex's radiance so far is 0
             if (!fresh) { lx = P.lx[s]; ly = P.ly[s]; lz = P.lz[s]; }
@@ -612,41 +555,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 lz += scz;
             }
             const bool store = !T.B.found || fresh;  // the radiance in HBM is stale
-            if (cont) {
-                if (store) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
-                P.state[s] = WF_NEED_EXT;
-            } else if (lx == 0.0 && ly == 0.0 && lz == 0.0) {
-                P.state[s] = WF_FREE;  // nothing to add
-            } else {
-                if (store) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
-                to_retire = true;
-            }
+            const bool black = lx == 0.0 && ly == 0.0 && lz == 0.0;
+            if (store && (cont || !black)) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
+            // continue; or finished: k_resolve adds the radiance (nothing to add: FREE)
+            P.state[s] = cont ? WF_NEED_EXT : (black ? WF_FREE : WF_DONE);
             active = false;
         }
-        // list finished paths for retirement (flush first if the list could overflow)
-        const uint64_t rm = __ballot(to_retire);
-        if (rm) {
-            if (nretire >= 64) {
-                retire_flush(P, rtl, 64);
-                const int rest = nretire - 64;
-                const int mv = lane < rest ? rtl[64 + lane] : 0;
-                wave_lds_sync();
-                if (lane < rest) rtl[lane] = mv;
-                wave_lds_sync();
-                nretire = rest;
-            }
-            if (to_retire) rtl[nretire + __popcll(rm & lanes_below())] = s;
-            wave_lds_sync();
-            nretire += __popcll(rm);
-        }
         DIAG_MARK(dg, fin, DG);
-    }
-    // retire what is still listed
-    if (nretire > 64) {
-        retire_flush(P, rtl, 64);
-        retire_flush(P, rtl + 64, nretire - 64);
-    } else if (nretire > 0) {
-        retire_flush(P, rtl, nretire);
     }
     unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
@@ -666,27 +581,48 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
 }
 
 // ------------------------------------------------------------------------------------------------
-// launchers
+// k_resolve: after a generation, every pixel adds its finished paths' radiance in sample order
+// (PixelIntegrator.Sample: color <- color + TraceRay(...), Integrators.fs:169). One thread per
+// tile-ordered pixel position q; for a fixed sample, consecutive q are consecutive slots, so the
+// loads are coalesced. No atomics: one thread owns each pixel, generations are stream-ordered.
 // ------------------------------------------------------------------------------------------------
-WfParams mfx_wf_slice(const WfParams& P, int32_t first, int32_t n) {
-    WfParams S = P;
-    double** dbl[] = {&S.ox, &S.oy, &S.oz, &S.dx, &S.dy, &S.dz, &S.tx, &S.ty, &S.tz, &S.lx, &S.ly, &S.lz};
-    static_assert(sizeof(dbl) / sizeof(dbl[0]) == WF_DOUBLES_PER_SLOT - 1, "slot arrays");
-    for (double** d : dbl) *d += first;
-    S.key += first;
-    S.rn += first;
-    S.depth += first;
-    S.pixel += first;
-    S.hit_slot += first;
-    S.state += first;
-    S.pool = n;
-    return S;
+__global__ void __launch_bounds__(256) k_resolve(WfParams P) {
+    const int tiles_x = (P.width + 7) >> 3;
+    const int64_t per_sample = (int64_t)tiles_x * ((P.height + 7) >> 3) * 64;
+    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (q >= per_sample) return;
+    const int64_t tile = q >> 6;
+    const int within = (int)(q & 63);
+    const int x = (int)(tile % tiles_x) * 8 + (within & 7);
+    const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
+    if (x >= P.width || y >= P.height) return;
+    const int64_t npix = (int64_t)P.width * P.height;
+    const int64_t pixel = (int64_t)x * P.height + y;
+    const int64_t end = P.path_base + P.total;
+    double ax = P.accum[pixel], ay = P.accum[npix + pixel], az = P.accum[2 * npix + pixel];
+    for (int64_t smp = P.path_base / per_sample; smp * per_sample < end; ++smp) {
+        const int64_t p = smp * per_sample + q;
+        if (p < P.path_base || p >= end) continue;
+        const int64_t j = p - P.path_base;
+        if ((P.state[j] & WF_STATE_MASK) == WF_DONE) {
+            ax += P.lx[j];
+            ay += P.ly[j];
+            az += P.lz[j];
+        }
+    }
+    P.accum[pixel] = ax;
+    P.accum[npix + pixel] = ay;
+    P.accum[2 * npix + pixel] = az;
 }
 
+// ------------------------------------------------------------------------------------------------
+// launchers
+// ------------------------------------------------------------------------------------------------
 // stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
 static size_t wf_lds_bytes(int stack_size, bool shadow) {
     const size_t stacks = (size_t)4 * stack_size * 64 * sizeof(int);
-    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * WF_SHADE_LIST_BYTES : stacks + 4 * PendExt::BYTES + 64;
+    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
+                  : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
 hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
@@ -700,7 +636,7 @@ hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blo
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
     const size_t lds_e = wf_lds_bytes(P.stack_size, false), lds_s = wf_lds_bytes(P.stack_size, true);
-    hipError_t e = hipMemsetAsync(P.ctl + WF_CTL_EXT, 0, 2 * WF_SHARDS * sizeof(unsigned long long), st);
+    hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     if (stats)
         hipLaunchKernelGGL(k_extend<true>, dim3(ext_grid), dim3(256), lds_e, st, P);
@@ -711,5 +647,11 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
         hipLaunchKernelGGL(k_shadow<true>, dim3(shd_grid), dim3(256), lds_s, st, P);
     else
         hipLaunchKernelGGL(k_shadow<false>, dim3(shd_grid), dim3(256), lds_s, st, P);
+    return hipGetLastError();
+}
+
+hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st) {
+    const int64_t per_sample = (int64_t)((P.width + 7) >> 3) * ((P.height + 7) >> 3) * 64;
+    hipLaunchKernelGGL(k_resolve, dim3((unsigned)((per_sample + 255) / 256)), dim3(256), 0, st, P);
     return hipGetLastError();
 }
