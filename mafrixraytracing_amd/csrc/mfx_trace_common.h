@@ -83,7 +83,8 @@ __device__ __forceinline__ bool aabb_hit64(const double* lo, const double* hi, D
     return tmin < tMax && tmax > tMin;
 }
 
-// Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148)
+// Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148); fields
+// loaded where used (the rare whole-reference-leaf evaluation)
 __device__ __forceinline__ bool tri_hit64(const MfxSlot& s, DV o, DV d, double tMin, double& t) {
     DV e1 = ld3(s.b), e2 = ld3(s.c);
     DV s1 = vcross(d, e2);
@@ -198,6 +199,63 @@ __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV
     return true;
 }
 
+#ifndef MFX_LEAF_PRELOAD
+#define MFX_LEAF_PRELOAD 2  // 0: fields loaded where used; 1: a slot's 80-B test prefix in one round; 2: + its box (+5 % on C2)
+#endif
+
+// A traversal slot's test prefix (bytes 0..79: geometry, `first`, `info`) in registers, loaded
+// as five independent 16-B loads in one round before any test arithmetic. Loading fields where
+// they are used puts two dependent memory round trips into every triangle test (e1/e2 first, v0
+// only after the divisor cull), which the compiler may not hoist above the branch.
+struct SlotR {
+    DV a, b, c;
+    int first, info;
+};
+__device__ __forceinline__ double i2d(int lo, int hi) { return __hiloint2double(hi, lo); }
+__device__ __forceinline__ SlotR load_slot(const MfxSlot* __restrict__ p) {
+    const int4* __restrict__ q = (const int4*)p;
+    const int4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    SlotR s;
+    s.a = dv(i2d(r0.x, r0.y), i2d(r0.z, r0.w), i2d(r1.x, r1.y));
+    s.b = dv(i2d(r1.z, r1.w), i2d(r2.x, r2.y), i2d(r2.z, r2.w));
+    s.c = dv(i2d(r3.x, r3.y), i2d(r3.z, r3.w), i2d(r4.x, r4.y));
+    s.first = r4.z;
+    s.info = r4.w;
+    return s;
+}
+// Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148)
+__device__ __forceinline__ bool tri_hit64(const SlotR& s, DV o, DV d, double tMin, double& t) {
+    DV s1 = vcross(d, s.c);
+    double divisor = vdot(s1, s.b);
+    if (fabs(divisor) < 1e-6) return false;
+    double inv = 1. / divisor;
+    DV dd = vsub(o, s.a);
+    double b1 = vdot(dd, s1) * inv;
+    if (b1 < 0. || b1 > 1.) return false;
+    DV s2 = vcross(dd, s.b);
+    double b2 = vdot(d, s2) * inv;
+    if (b2 < 0. || (b1 + b2) >= 1.) return false;
+    t = vdot(s.c, s2) * inv;
+    return t > tMin;
+}
+// Sphere.Hit — Sphere.fs:21-43
+__device__ __forceinline__ bool sphere_hit64(const SlotR& s, DV o, DV d, double tMin, double tMax, double& t) {
+    DV oc = vsub(o, s.a);
+    double a = 1.;
+    double b = 2.0 * vdot(oc, d);
+    double c = vdot(oc, oc) - s.b.x * s.b.x;
+    double disc = b * b - 4.0 * a * c;
+    if (disc > 0) {
+        double rd = sqrt(disc);
+        double q = (b < 0.) ? -0.5 * (b - rd) : -0.5 * (b + rd);
+        double t0 = q, t1 = c / q;
+        double tmn = t0 < t1 ? t0 : t1, tmx = t0 > t1 ? t0 : t1;
+        if (tmn >= tMin && tmn < tMax) { t = tmn; return true; }
+        if (tmx > tMin && tmx < tMax) { t = tmx; return true; }
+    }
+    return false;
+}
+
 // One traversal leaf (1..4 primitives of possibly different reference leaves; child code = first
 // slot << 3 | slots - 1). Each primitive hit is a candidate for its reference leaf's result: with
 // t < tMax the reference leaf's minBy result is a hit of t no larger (the leaf's other primitives
@@ -216,6 +274,36 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     if (STATS) st.clusters++;
     bool improved = false;
     for (int k = 0; k < n; ++k) {
+#if MFX_LEAF_PRELOAD
+        SlotR r = load_slot(sl + k);
+#if MFX_LEAF_PRELOAD == 2
+        // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)
+        const double2 bx0 = *(const double2*)sl[k].lo, bx1 = *(const double2*)(sl[k].lo + 2),
+                      bx2 = *(const double2*)(sl[k].hi + 1);
+#endif
+        int info = r.info;
+        const int kind = (info >> MFX_INFO_KIND_SHIFT) & 3;
+        if (STATS) st.prims++;
+        double t = 0.0;
+        int hs = k;
+        int first = r.first;
+        bool hit;
+        if (kind == MFX_KIND_SPHERE) {
+            hit = sphere_hit64(r, o, d, tMin, tMax, t);
+        } else {
+            hit = tri_hit64(r, o, d, tMin, t);
+            if (kind == MFX_KIND_RECT) {
+                ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
+                if (!hit) {
+                    hs = k;
+                    r = load_slot(sl + k);
+                    hit = tri_hit64(r, o, d, tMin, t);
+                    info = r.info;
+                    first = r.first;
+                }
+            }
+        }
+#else
         int info = sl[k].info;
         const int kind = (info >> MFX_INFO_KIND_SHIFT) & 3;
         if (STATS) st.prims++;
@@ -223,18 +311,20 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         int hs = k;
         bool hit;
         if (kind == MFX_KIND_SPHERE) {
-            hit = sphere_hit64(sl[k], o, d, tMin, tMax, t);
+            hit = sphere_hit64(load_slot(sl + k), o, d, tMin, tMax, t);
         } else {
-            hit = tri_hit64(sl[k], o, d, tMin, t);
+            hit = tri_hit64(load_slot(sl + k), o, d, tMin, t);
             if (kind == MFX_KIND_RECT) {
-                ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
+                ++k;
                 if (!hit) {
                     hs = k;
-                    hit = tri_hit64(sl[k], o, d, tMin, t);
+                    hit = tri_hit64(load_slot(sl + k), o, d, tMin, t);
                     info = sl[k].info;
                 }
             }
         }
+        const int first = sl[hs].first;
+#endif
         if (!hit) continue;
         if (t >= tMax) {
             double t2;
@@ -249,9 +339,13 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
             continue;
         }
         if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
-        const int first = sl[hs].first;
         if (!SHADOW && !beats(B, t, first, info)) continue;
+#if MFX_LEAF_PRELOAD == 2
+        const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
+        if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
+#else
         if (!aabb_hit64(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
+#endif
         if (SHADOW) return true;
         B = Best{t, info, first, true};
         improved = true;

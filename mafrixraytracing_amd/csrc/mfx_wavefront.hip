@@ -29,7 +29,7 @@
 #include "mfx_wavefront.h"
 
 #ifndef MFX_TRAV_WAVES
-#define MFX_TRAV_WAVES 1  // min waves per SIMD requested from the register allocator
+#define MFX_TRAV_WAVES 4  // min waves per SIMD requested from the register allocator (128 VGPRs; a few spills)
 #endif
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
