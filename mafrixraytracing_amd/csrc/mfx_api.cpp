@@ -263,6 +263,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
     P.chunk = c->wf_chunk;
+    P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
@@ -275,6 +276,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     int it = 0;
     for (int64_t g = 0; g < ngen; ++g) {
         P.path_base = g * gen_max;
+        P.base_smp = P.path_base / per_sample;
+        P.base_q = P.path_base % per_sample;
         P.total = std::min<int64_t>(gen_max, total - P.path_base);
         P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));

@@ -202,6 +202,9 @@ __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV
 #ifndef MFX_LEAF_PRELOAD
 #define MFX_LEAF_PRELOAD 2  // 0: fields loaded where used; 1: a slot's 80-B test prefix in one round; 2: + its box (+5 % on C2)
 #endif
+#ifndef MFX_SHADOW_PRELOAD
+#define MFX_SHADOW_PRELOAD MFX_LEAF_PRELOAD  // the same for shadow queries (a hit ends them: the box is rarely needed)
+#endif
 
 // A traversal slot's test prefix (bytes 0..79: geometry, `first`, `info`) in registers, loaded
 // as five independent 16-B loads in one round before any test arithmetic. Loading fields where
@@ -273,14 +276,17 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     const MfxSlot* __restrict__ sl = S.slots + s0;
     if (STATS) st.clusters++;
     bool improved = false;
+    constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
     for (int k = 0; k < n; ++k) {
 #if MFX_LEAF_PRELOAD
         SlotR r = load_slot(sl + k);
-#if MFX_LEAF_PRELOAD == 2
         // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)
-        const double2 bx0 = *(const double2*)sl[k].lo, bx1 = *(const double2*)(sl[k].lo + 2),
-                      bx2 = *(const double2*)(sl[k].hi + 1);
-#endif
+        double2 bx0 = make_double2(0, 0), bx1 = bx0, bx2 = bx0;
+        if (PRE == 2) {
+            bx0 = *(const double2*)sl[k].lo;
+            bx1 = *(const double2*)(sl[k].lo + 2);
+            bx2 = *(const double2*)(sl[k].hi + 1);
+        }
         int info = r.info;
         const int kind = (info >> MFX_INFO_KIND_SHIFT) & 3;
         if (STATS) st.prims++;
@@ -340,12 +346,12 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         }
         if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
         if (!SHADOW && !beats(B, t, first, info)) continue;
-#if MFX_LEAF_PRELOAD == 2
-        const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
-        if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
-#else
-        if (!aabb_hit64(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
-#endif
+        if (PRE == 2) {
+            const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
+            if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
+        } else {
+            if (!aabb_hit64(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
+        }
         if (SHADOW) return true;
         B = Best{t, info, first, true};
         improved = true;

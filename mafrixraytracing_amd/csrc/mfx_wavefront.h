@@ -76,6 +76,8 @@ struct WfParams {
     int32_t stack_size;
     int32_t chunk;                        // slots per chunk fetch of the kernels
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
+    int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
+    int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool

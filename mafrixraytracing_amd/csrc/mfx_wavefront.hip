@@ -208,14 +208,18 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
 // Path index of this generation -> (sample, 8x8 pixel tile, pixel), sample-major and
 // tile-coherent. False for the padding indices of edge tiles (no path).
 __device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x, int& y, int64_t& smp) {
-    const int tiles_x = (P.width + 7) >> 3;
-    const int64_t per_sample = (int64_t)tiles_x * ((P.height + 7) >> 3) * 64;
-    smp = p / per_sample;
-    const int64_t q = p - smp * per_sample;
-    const int64_t tile = q >> 6;
-    const int within = (int)(q & 63);
-    x = (int)(tile % tiles_x) * 8 + (within & 7);
-    y = (int)(tile / tiles_x) * 8 + (within >> 3);
+    // p = path_base + s: the 64-bit split of path_base is done once per generation on the host
+    // (base_smp, base_q), so only 32-bit divisions remain here (base_q + s < 2^32)
+    const unsigned tiles_x = (unsigned)(P.width + 7) >> 3;
+    const unsigned per_sample = tiles_x * (((unsigned)P.height + 7) >> 3) * 64;  // < 2^31 (film limit)
+    const unsigned qs = (unsigned)P.base_q + (unsigned)(p - P.path_base);
+    const unsigned ds = qs / per_sample;
+    smp = P.base_smp + ds;
+    const unsigned q = qs - ds * per_sample;
+    const unsigned tile = q >> 6, within = q & 63;
+    const unsigned ty = tile / tiles_x;
+    x = (int)((tile - ty * tiles_x) * 8 + (within & 7));
+    y = (int)(ty * 8 + (within >> 3));
     return x < P.width && y < P.height;
 }
 
@@ -280,7 +284,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     if (P.start && sj == WF_FREE && j < P.total) {
                         int x, y;
                         int64_t smp;
-                        take = path_pixel(P, P.path_base + j, x, y, smp);  // edge-tile padding: no path
+                        // edge-tile padding starts no path (none when 8 divides the film size)
+                        take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
                     }
                     const uint64_t tm = __ballot(take);
                     if (take) pend[n + __popcll(tm & lanes_below())] = sj == WF_FREE ? (j | (int)0x80000000) : j;
