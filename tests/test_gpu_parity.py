@@ -2,9 +2,9 @@
 
 Bar: discrete results (hit/miss, primitive, occlusion, ray counts, reference-leaf
 grouping, RGBA8 bytes) must be identical; FP64 hit distances and normals bit-identical; images
-within 1e-12 absolute per channel (the GPU sums a path's bounces forward and the pixel's samples
-in atomic order, the oracle recursively and in sample order — FP64 rounding only), far inside
-north_star's 1e-4 per-channel RMSE gate, which is asserted too.
+within 1e-12 absolute per channel (the GPU sums a path's bounces forward, the oracle recursively;
+the wavefront adds a pixel's samples in sample order like the oracle, the megakernel with atomics —
+FP64 rounding only), far inside north_star's 1e-4 per-channel RMSE gate, which is asserted too.
 """
 import numpy as np
 import pytest
@@ -188,6 +188,18 @@ def test_wavefront_small_pool_many_iterations(gpu, oracle, pool, monkeypatch):
         tm = ctx.trace_timing()
     assert tm["iterations"] > 5
     assert np.abs(img[:, :3] - ref[:, :3]).max() <= 1e-12
+
+
+def test_wavefront_image_is_deterministic(gpu):
+    """k_resolve adds each pixel's paths in sample order (no atomics): two runs are bit-identical,
+    also across generations (a small pool forces several)."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 64, 36)
+    with NativeContext(a, seed=SEED) as ctx:
+        f1 = ctx.sample(8)
+    with NativeContext(a, seed=SEED) as ctx:
+        f2 = ctx.sample(8)
+    assert np.array_equal(f1, f2)
 
 
 def test_megakernel_and_wavefront_counters_agree(gpu):
