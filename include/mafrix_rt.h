@@ -103,6 +103,7 @@ typedef struct mfx_options {
 #define MFX_F_NONE 0
 #define MFX_F_COUNT_STATS 1 /* count traversal node/leaf/prim visits (slower; for the roofline model) */
 #define MFX_F_MEGAKERNEL 2  /* one persistent megakernel instead of the wavefront pipeline */
+#define MFX_F_HOST_BVH 4    /* build the traversal BVH on the host CPU (default: on the GPU; the same tree) */
 
 typedef struct mfx_ctx mfx_ctx;
 
@@ -196,6 +197,14 @@ int mfx_ref_leaves(mfx_ctx* ctx, int32_t* indices_out, int32_t* leaf_first_out,
  * may be NULL.                                                                                */
 int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t* leaf_first_out,
                      int32_t* leaf_count_out, int32_t* nleaves_out, int32_t info_out[4]);
+
+/* How mfx_create built the scene (Scene ctor, Scene.fs:298-313; Bvh.Build, BvhNode.fs:24-61):
+ * out[0] = ms for the reference leaf grouping (host), out[1] = ms for the traversal BVH2
+ * (GPU incl. transfers, or host), out[2] = ms for the whole scene preparation, out[3] = 1 if the
+ * BVH2 was built on the GPU, out[4] = BVH4 nodes, out[5] = traversal slots, out[6] = BVH2
+ * internal nodes, out[7] = BVH2 build levels. digest (may be NULL) = FNV-1a of the device
+ * images (nodes, slots, slot_ref, ref_blob, shade): equal digests mean identical traversal.    */
+int mfx_build_info(mfx_ctx* ctx, double out[8], uint64_t* digest);
 
 /* Device FP64 self-test: computes a/b, sqrt(a) on the GPU for n pairs (bit-exactness check
  * of the device math the numerics contract relies on).                                      */

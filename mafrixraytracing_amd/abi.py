@@ -19,6 +19,7 @@ MFX_PRIM_SPHERE = 2
 MFX_F_NONE = 0
 MFX_F_COUNT_STATS = 1
 MFX_F_MEGAKERNEL = 2
+MFX_F_HOST_BVH = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -122,6 +123,7 @@ def _bind(lib):
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
         "mfx_fp64_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _dp, _dp]),
         "mfx_build_leaves": (C.c_int, [_P(MfxSceneDesc), _ip, _ip, _ip, _ip, _ip]),
+        "mfx_build_info": (C.c_int, [C.c_void_p, _dp, _P(C.c_uint64)]),
         "mfx_last_error": (C.c_char_p, []),
         "mfx_abi_version": (C.c_int, []),
         "mfx_device_count": (C.c_int, []),
@@ -137,7 +139,7 @@ EXPORTED_SYMBOLS = [
     "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_reset", "mfx_film_mean",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
-    "mfx_fp64_selftest", "mfx_build_leaves", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+    "mfx_fp64_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 
 _lib = None

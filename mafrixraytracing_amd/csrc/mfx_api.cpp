@@ -123,11 +123,15 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     int ndev = 0;
     HIPCHECK(hipGetDeviceCount(&ndev));
     if (opt->device < 0 || opt->device >= ndev) return fail(MFX_E_DEVICE, "mfx_create: no such HIP device");
+    HIPCHECK(hipSetDevice(opt->device));
     mfx_ctx* c = new mfx_ctx();
     std::string err;
-    if (!mfx_build_scene(scene, c->host, err)) {
+    // the traversal BVH is built on this device unless the caller asks for the host build (the
+    // same tree either way: tests/test_gpu_build.py)
+    if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0)) {
         delete c;
-        return fail(MFX_E_INVALID, "mfx_create: " + err);
+        const bool dev = err.rfind("GPU BVH build", 0) == 0;
+        return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
     }
     c->device = opt->device;
     c->seed = opt->seed;
@@ -567,6 +571,35 @@ int mfx_ref_leaves(mfx_ctx* c, int32_t* indices_out, int32_t* leaf_first_out, in
     std::copy(c->host.leaf_first.begin(), c->host.leaf_first.end(), leaf_first_out);
     std::copy(c->host.leaf_count.begin(), c->host.leaf_count.end(), leaf_count_out);
     *nleaves_out = (int32_t)c->host.leaf_first.size();
+    return MFX_OK;
+}
+
+int mfx_build_info(mfx_ctx* c, double out[8], uint64_t* digest) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    const MfxHostScene& h = c->host;
+    if (out) {
+        out[0] = h.ms_ref_bvh;
+        out[1] = h.ms_bvh;
+        out[2] = h.ms_total;
+        out[3] = h.bvh_gpu ? 1.0 : 0.0;
+        out[4] = (double)h.nodes.size();
+        out[5] = (double)h.slots.size();
+        out[6] = h.nodes2;
+        out[7] = h.bvh_levels;
+    }
+    if (digest) {  // FNV-1a over the device images
+        uint64_t x = 1469598103934665603ULL;
+        auto mix = [&](const void* p, size_t n) {
+            const uint8_t* b = (const uint8_t*)p;
+            for (size_t i = 0; i < n; ++i) x = (x ^ b[i]) * 1099511628211ULL;
+        };
+        mix(h.nodes.data(), h.nodes.size() * sizeof(MfxNode));
+        mix(h.slots.data(), h.slots.size() * sizeof(MfxSlot));
+        mix(h.slot_ref.data(), h.slot_ref.size() * sizeof(int32_t));
+        mix(h.ref_blob.data(), h.ref_blob.size());
+        mix(h.shade.data(), h.shade.size() * sizeof(MfxShade));
+        *digest = x;
+    }
     return MFX_OK;
 }
 

@@ -12,6 +12,10 @@
 //    so the reference's leaf semantics are applied exactly per candidate hit.
 #include "mfx_scene.h"
 
+#include <chrono>
+
+#include "mfx_build.h"
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -308,7 +312,8 @@ struct SahBuilder {
             mid = (b + e) / 2;  // all centroids coincide: split by position
         } else {
             const float lo = cbox.lo[best_axis], ext = cbox.hi[best_axis] - cbox.lo[best_axis];
-            auto it = std::partition(ids.begin() + b, ids.begin() + e, [&](int id) {
+            // stable: the GPU build (mfx_build.hip) partitions the same way, so both builds agree
+            auto it = std::stable_partition(ids.begin() + b, ids.begin() + e, [&](int id) {
                 int k = (int)((cent[3 * id + best_axis] - lo) / ext * NB);
                 k = std::min(NB - 1, std::max(0, k));
                 return k <= best_split;
@@ -410,7 +415,12 @@ inline float round_up(double x) {
 
 }  // namespace
 
-bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err) {
+bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err, bool gpu_bvh) {
+    using clock = std::chrono::steady_clock;
+    const auto t_start = clock::now();
+    auto ms_since = [](clock::time_point t0) {
+        return std::chrono::duration<double, std::milli>(clock::now() - t0).count();
+    };
     if (!d || !d->prims || d->nprims < 1) {
         err = "scene has no primitives (Bvh.Build on an empty array throws, BvhNode.fs:26)";
         return false;
@@ -494,9 +504,11 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
     s.leaf_first.clear();
     s.leaf_count.clear();
     {
+        const auto t0 = clock::now();
         RefBvh rb{pb, s.ref_indices, s.leaf_first, s.leaf_count, std::vector<double>(n), std::vector<int32_t>(n)};
         Box root = rb.bound(0, n);
         rb.subdivide(0, n, root);
+        s.ms_ref_bvh = ms_since(t0);
     }
     const int nc = (int)s.leaf_first.size();
     std::vector<MfxLeaf> leaves(nc);
@@ -588,7 +600,47 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
         sb.ids[i] = i;
     }
     FBox rootbox;
-    const int root2 = sb.build(0, n, 0, rootbox);
+    int root2 = 0;
+    const auto t_bvh = clock::now();
+    s.bvh_gpu = gpu_bvh;
+    if (gpu_bvh) {  // the same tree, built breadth-first on the current HIP device (mfx_build.hip)
+        std::vector<float> pbox(6 * (size_t)n);
+        for (int i = 0; i < n; ++i)
+            for (int a = 0; a < 3; ++a) {
+                pbox[6 * (size_t)i + a] = sb.cb[i].lo[a];
+                pbox[6 * (size_t)i + 3 + a] = sb.cb[i].hi[a];
+            }
+        MfxBvh2 g;
+        const hipError_t he = mfx_gpu_sah_build(pbox.data(), sb.cent.data(), nslot_of.data(), n, sb.max_leaf,
+                                                sb.c_isect, g);
+        if (he != hipSuccess) {
+            err = std::string("GPU BVH build: ") + hipGetErrorString(he);
+            return false;
+        }
+        nodes2.resize(g.child.size() / 2);
+        for (size_t i = 0; i < nodes2.size(); ++i)
+            for (int k = 0; k < 2; ++k) {
+                nodes2[i].child[k] = g.child[2 * i + k];
+                for (int a = 0; a < 3; ++a) {
+                    nodes2[i].box[k].lo[a] = g.box[(2 * i + k) * 6 + a];
+                    nodes2[i].box[k].hi[a] = g.box[(2 * i + k) * 6 + 3 + a];
+                }
+            }
+        sb.leaves.clear();
+        for (size_t l = 0; l < g.leaf_b.size(); ++l) sb.leaves.emplace_back(g.leaf_b[l], g.leaf_e[l]);
+        sb.ids = g.ids;
+        root2 = g.root;
+        for (int a = 0; a < 3; ++a) {
+            rootbox.lo[a] = g.root_box[a];
+            rootbox.hi[a] = g.root_box[3 + a];
+        }
+        s.bvh_levels = g.levels;
+    } else {
+        root2 = sb.build(0, n, 0, rootbox);
+        s.bvh_levels = sb.max_depth + 1;
+    }
+    s.ms_bvh = ms_since(t_bvh);
+    s.nodes2 = (int32_t)nodes2.size();
     s.nodes.clear();
     Collapse4 c4{nodes2, s.nodes};
     const int root = c4.run(root2, 0, 0, &rootbox);  // always an internal node (a lone leaf gets a parent)
@@ -693,5 +745,6 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err)
     s.ref_blob.resize(s.ref_blob.size() + 3 * sizeof(MfxSlot), 0);
     s.nclusters = nc;
     s.ntleaves = nl;
+    s.ms_total = ms_since(t_start);
     return true;
 }

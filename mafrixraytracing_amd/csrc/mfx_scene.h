@@ -27,9 +27,15 @@ struct MfxHostScene {
     int32_t bvh_depth = 0;     // longest root-to-leaf path in nodes[]
     int32_t stack_entries = 1; // traversal stack bound: pushes along any root-to-node path
     float eps = 0.f;           // conservative box widening
+    // build record (mfx_build_info)
+    bool bvh_gpu = false;      // traversal BVH2 built on the GPU (mfx_build.hip)
+    int32_t bvh_levels = 0;    // its breadth-first levels (GPU) / depth + 1 (host)
+    int32_t nodes2 = 0;        // its internal nodes
+    double ms_ref_bvh = 0, ms_bvh = 0, ms_total = 0;
 };
 
 // Builds everything from the C-ABI scene description; returns false with `err` set on bad input.
-bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err);
+// gpu_bvh: build the traversal BVH2 on the current HIP device (the same tree as the host build).
+bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err, bool gpu_bvh = false);
 
 #endif

@@ -130,6 +130,15 @@ class NativeContext:
         check(self.lib.mfx_any_hit(self._h, len(rays), dptr(rays), tmin, dptr(tmax), iptr(occ)), "mfx_any_hit")
         return occ
 
+    def build_info(self) -> dict:
+        """How the scene was prepared (mfx_build_info): timings, BVH sizes, image digest."""
+        out = np.zeros(8)
+        dig = C.c_uint64()
+        check(self.lib.mfx_build_info(self._h, dptr(out), C.byref(dig)), "mfx_build_info")
+        return {"ref_bvh_ms": out[0], "bvh_ms": out[1], "scene_ms": out[2], "gpu_bvh": bool(out[3]),
+                "nodes4": int(out[4]), "slots": int(out[5]), "nodes2": int(out[6]), "levels": int(out[7]),
+                "digest": dig.value}
+
     def ref_leaves(self):
         n = len(self.arrays.prims)
         idx = np.zeros(n, dtype=np.int32)
