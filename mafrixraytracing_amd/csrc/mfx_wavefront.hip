@@ -34,6 +34,10 @@
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
+#ifndef MFX_HEMI_FP32_SCREEN
+#define MFX_HEMI_FP32_SCREEN 1  // rejection trials decided in FP32 away from the boundary (exact)
+#endif
+
 #ifndef MFX_NODE_LANES_MIN
 #define MFX_NODE_LANES_MIN 12  // node-loop early exit: fewer lanes than this still stepping
 #endif
@@ -446,6 +450,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                     const uint64_t key = P.key[j];
                     uint32_t rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
                     // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
+#if MFX_HEMI_FP32_SCREEN
+                    const DV p = hemisphere_ball(nm, key, rn);
+#else
                     DV p = dv(20, 20, 20);
                     while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
                         const double rx = rng_next(key, rn);
@@ -453,6 +460,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                         const double rz = rng_next(key, rn);
                         p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
                     }
+#endif
                     const DV wi = vnormalize(p);
                     const double ei = vdot(nm, wi);
                     const double* a = sh.albedo;
