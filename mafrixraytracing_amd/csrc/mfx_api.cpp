@@ -86,6 +86,8 @@ struct mfx_ctx {
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
+    int wf_stack_lds = 1;            // traversal stack entries per lane in LDS (the rest spill)
+    int32_t* d_spill = nullptr;      // deep traversal-stack entries
     bool diag_iter = false;
 };
 
@@ -93,7 +95,7 @@ static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->it_ev)
@@ -190,14 +192,37 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     CK(mfx_trace_occupancy(c->stack_size, &bpc));
     bpc = std::max(1, std::min(bpc, 8));
     c->grid = prop.multiProcessorCount * bpc;
+    // Traversal stacks: the whole bound in LDS unless that costs resident blocks. Measured (C2 / C4
+    // / C5): with a deep BVH (C4's bound is 44 entries: k_extend 3 and k_shadow 2 blocks per CU) the
+    // first WF_STACK_LDS entries in LDS and the rest spilled (the kernels' SPILL instances) is
+    // +14 %; when the full stacks already allow k_extend its 4 blocks and k_shadow 3 (C2, C5), the
+    // spilling instances' extra stack arithmetic costs more than k_shadow's fourth block gains.
     int ebpc = 0, sbpc = 0;
-    CK(mfx_wf_occupancy(c->stack_size, &ebpc, &sbpc));
+    CK(mfx_wf_occupancy(c->stack_size, false, &ebpc, &sbpc));
+    c->wf_stack_lds = c->stack_size;
+    if (c->stack_size > WF_STACK_LDS) {
+        int e2 = 0, s2 = 0;
+        CK(mfx_wf_occupancy(WF_STACK_LDS, true, &e2, &s2));
+        if (e2 > ebpc || (sbpc < 3 && s2 > sbpc)) {
+            c->wf_stack_lds = WF_STACK_LDS;
+            ebpc = e2;
+            sbpc = s2;
+        }
+    }
+    if (const char* e = getenv("MFX_STACK_LDS")) {
+        c->wf_stack_lds = std::max(1, std::min(c->stack_size, atoi(e)));
+        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, &ebpc, &sbpc));
+    }
     if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
         ebpc = std::min(ebpc, std::max(1, atoi(b)));
         sbpc = std::min(sbpc, std::max(1, atoi(b)));
     }
     c->wf_ext_grid = prop.multiProcessorCount * std::max(1, std::min(ebpc, 8));
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
+    {  // deep traversal-stack entries of every lane of the larger grid
+        const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
+        CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, c->stack_size - c->wf_stack_lds)));
+    }
 #undef CK
     *out = c;
     return MFX_OK;
@@ -266,6 +291,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.height = H;
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
+    P.stack_lds = c->wf_stack_lds;
+    P.spill = c->d_spill;
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;

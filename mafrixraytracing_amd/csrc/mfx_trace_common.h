@@ -412,6 +412,26 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
 
+// A lane's traversal stack. LdsStack: the whole bound in an LDS column (stride 64 dwords:
+// conflict-free). SpillStack: the first `nlds` entries in LDS and deeper ones in a global column
+// (stride `gstride`), so the LDS a wave needs — which caps the resident waves — no longer grows
+// with the BVH's depth; pushes that deep are rare.
+struct LdsStack {
+    int* lds;
+    __device__ __forceinline__ int get(int i) const { return lds[i * 64]; }
+    __device__ __forceinline__ void put(int i, int v) const { lds[i * 64] = v; }
+};
+struct SpillStack {
+    int* lds;
+    int* spill;
+    int nlds, gstride;
+    __device__ __forceinline__ int get(int i) const { return i < nlds ? lds[i * 64] : spill[(i - nlds) * gstride]; }
+    __device__ __forceinline__ void put(int i, int v) const {
+        if (i < nlds) lds[i * 64] = v;
+        else spill[(i - nlds) * gstride] = v;
+    }
+};
+
 // One internal-node step of the BVH4, branch-free: four child slab tests, the hit children sorted
 // near to far (5-comparator network over (entry distance, child), misses sorted last at +inf),
 // then descend into the nearest, push the others far-first, or pop. The pop candidate (top of stack) is read before the node's boxes arrive, so
@@ -426,9 +446,10 @@ __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
     db = s ? t : db;
     cb = s ? u : cb;
 }
+template <typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         int* __restrict__ stack, int& sp) {
-    const int top = stack[(sp > 0 ? sp - 1 : 0) * 64];
+                                         const ST& stack, int& sp) {
+    const int top = stack.get(sp > 0 ? sp - 1 : 0);
     const float4* __restrict__ q = (const float4*)(nodes + node);
     const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     int4 ch = *(const int4*)(q + 6);
@@ -464,9 +485,9 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     cswap(d[1], c[1], d[2], c[2]);
     // far-first pushes: stack[sp + j] = c[nh - 1 - j] for j < nh - 1 (exec-masked stores, so the
     // stack never holds more than the pushes themselves: mfx_scene.cpp's Collapse4 bound)
-    if (nh >= 2) stack[sp * 64] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
-    if (nh >= 3) stack[(sp + 1) * 64] = nh == 4 ? c[2] : c[1];
-    if (nh >= 4) stack[(sp + 2) * 64] = c[1];
+    if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]));
+    if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1]);
+    if (nh >= 4) stack.put(sp + 2, c[1]);
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
@@ -489,7 +510,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            node = node_step(S.nodes, node, rf, tlim, stack, sp);
+            node = node_step(S.nodes, node, rf, tlim, LdsStack{stack}, sp);
         }
         if (node == MFX_TRAV_EXIT) return B.found;
         // ---- leaf ----

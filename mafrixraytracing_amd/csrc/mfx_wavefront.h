@@ -73,7 +73,9 @@ struct WfParams {
     int32_t part_index, part_count;
     int32_t pool;                         // slots scanned (>= total, a multiple of 64)
     int32_t width, height, max_depth;
-    int32_t stack_size;
+    int32_t stack_size;                   // traversal stack bound (entries per lane)
+    int32_t stack_lds;                    // of which in LDS; the rest in `spill`
+    int32_t* spill;                       // [stack_size - stack_lds][grid * 256] deep stack entries
     int32_t chunk;                        // slots per chunk fetch of the kernels
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
@@ -84,7 +86,11 @@ struct WfParams {
 #define WF_DOUBLES_PER_SLOT 13  // o, d, throughput, radiance (12) + key
 #define WF_WORDS_PER_SLOT 3     // rn, depth, state
 
-hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu);
+#ifndef WF_STACK_LDS
+#define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)
+#endif
+// resident blocks per CU of each kernel with `stack_lds` stack entries per lane in LDS
+hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int* ext_blocks_per_cu, int* shd_blocks_per_cu);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 #include "mfx_device.h"
 #include "mfx_trace_common.h"
 #include "mfx_wavefront.h"
@@ -159,6 +161,16 @@ struct Scanner {
     }
 };
 
+// the lane's stack: all of it in LDS, or the first P.stack_lds entries (the rest in P.spill)
+template <bool SPILL>
+__device__ __forceinline__ typename std::conditional<SPILL, SpillStack, LdsStack>::type make_stack(int* lds,
+                                                                                                  const WfParams& P) {
+    if constexpr (SPILL)
+        return SpillStack{lds, P.spill + blockIdx.x * 256 + threadIdx.x, P.stack_lds, (int)gridDim.x * 256};
+    else
+        return LdsStack{lds};
+}
+
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
     DV o, d;
@@ -183,8 +195,8 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
-template <bool SHADOW, bool STATS>
-__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __restrict__ stack, Stats& st,
+template <bool SHADOW, bool STATS, typename ST>
+__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, Stats& st,
                                           DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
@@ -205,7 +217,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, int* __re
         T.tlim = f_round_up(T.B.t);
     }
     if (T.sp == 0) return true;
-    T.node = stack[(--T.sp) * 64];
+    T.node = stack.get(--T.sp);
     return false;
 }
 
@@ -247,14 +259,15 @@ struct PendShd {
 // ------------------------------------------------------------------------------------------------
 // k_extend: closest hit for NEED_EXT slots; in a generation's first iteration FREE slots start paths
 // ------------------------------------------------------------------------------------------------
-template <bool STATS>
+template <bool STATS, bool SPILL>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    int* stack = lds + wave * P.stack_size * 64 + lane;
-    int* pend = lds + 4 * P.stack_size * 64 + wave * WF_EXT_PEND;
-    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_size * 64 + 4 * WF_EXT_PEND);
+    using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
+    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds * 64 + lane, P);
+    int* pend = lds + 4 * P.stack_lds * 64 + wave * WF_EXT_PEND;
+    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds * 64 + 4 * WF_EXT_PEND);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
     const int shard_size = P.pool / WF_SHARDS;
 
@@ -379,13 +392,14 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
-template <bool STATS>
+template <bool STATS, bool SPILL>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
     extern __shared__ int lds[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    int* stack = lds + wave * P.stack_size * 64 + lane;
-    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_size * 64);
+    using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
+    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds * 64 + lane, P);
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
@@ -638,28 +652,38 @@ static size_t wf_lds_bytes(int stack_size, bool shadow) {
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
-hipError_t mfx_wf_occupancy(int stack_size, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, k_extend<false>, 256,
-                                                                 wf_lds_bytes(stack_size, false));
+hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        ext_blocks_per_cu, spill ? k_extend<false, true> : k_extend<false, false>, 256, wf_lds_bytes(stack_lds, false));
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, k_shadow<false>, 256,
-                                                        wf_lds_bytes(stack_size, true));
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        shd_blocks_per_cu, spill ? k_shadow<false, true> : k_shadow<false, false>, 256, wf_lds_bytes(stack_lds, true));
+}
+
+template <bool SPILL>
+static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
+                             hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
+    if (stats)
+        hipLaunchKernelGGL((k_extend<true, SPILL>), dim3(ext_grid), dim3(256), lds_e, st, P);
+    else
+        hipLaunchKernelGGL((k_extend<false, SPILL>), dim3(ext_grid), dim3(256), lds_e, st, P);
+    if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return;
+    if (stats)
+        hipLaunchKernelGGL((k_shadow<true, SPILL>), dim3(shd_grid), dim3(256), lds_s, st, P);
+    else
+        hipLaunchKernelGGL((k_shadow<false, SPILL>), dim3(shd_grid), dim3(256), lds_s, st, P);
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
-    const size_t lds_e = wf_lds_bytes(P.stack_size, false), lds_s = wf_lds_bytes(P.stack_size, true);
+    const size_t lds_e = wf_lds_bytes(P.stack_lds, false), lds_s = wf_lds_bytes(P.stack_lds, true);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    if (stats)
-        hipLaunchKernelGGL(k_extend<true>, dim3(ext_grid), dim3(256), lds_e, st, P);
+    if (P.stack_lds < P.stack_size)
+        launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
     else
-        hipLaunchKernelGGL(k_extend<false>, dim3(ext_grid), dim3(256), lds_e, st, P);
-    if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return e;
-    if (stats)
-        hipLaunchKernelGGL(k_shadow<true>, dim3(shd_grid), dim3(256), lds_s, st, P);
-    else
-        hipLaunchKernelGGL(k_shadow<false>, dim3(shd_grid), dim3(256), lds_s, st, P);
+        launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    if (e != hipSuccess) return e;
     return hipGetLastError();
 }
 
