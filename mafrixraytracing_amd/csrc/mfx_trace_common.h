@@ -416,18 +416,25 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 // conflict-free). SpillStack: the first `nlds` entries in LDS and deeper ones in a global column
 // (stride `gstride`), so the LDS a wave needs — which caps the resident waves — no longer grows
 // with the BVH's depth; pushes that deep are rare.
+// `deep` is wave-uniform: false when no lane of the wave touches an entry past nlds, so the common
+// case runs plain LDS accesses behind one scalar branch.
 struct LdsStack {
     int* lds;
-    __device__ __forceinline__ int get(int i) const { return lds[i * 64]; }
-    __device__ __forceinline__ void put(int i, int v) const { lds[i * 64] = v; }
+    __device__ __forceinline__ bool deep(int) const { return false; }
+    __device__ __forceinline__ int get(int i, bool) const { return lds[i * 64]; }
+    __device__ __forceinline__ void put(int i, int v, bool) const { lds[i * 64] = v; }
 };
 struct SpillStack {
     int* lds;
     int* spill;
     int nlds, gstride;
-    __device__ __forceinline__ int get(int i) const { return i < nlds ? lds[i * 64] : spill[(i - nlds) * gstride]; }
-    __device__ __forceinline__ void put(int i, int v) const {
-        if (i < nlds) lds[i * 64] = v;
+    __device__ __forceinline__ bool deep(int top) const { return __ballot(top > nlds) != 0; }  // top: highest index + 1
+    __device__ __forceinline__ int get(int i, bool dp) const {
+        if (!dp) return lds[i * 64];
+        return i < nlds ? lds[i * 64] : spill[(i - nlds) * gstride];
+    }
+    __device__ __forceinline__ void put(int i, int v, bool dp) const {
+        if (!dp || i < nlds) lds[i * 64] = v;
         else spill[(i - nlds) * gstride] = v;
     }
 };
@@ -449,7 +456,8 @@ __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
 template <typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp) {
-    const int top = stack.get(sp > 0 ? sp - 1 : 0);
+    const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
+    const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
     const float4* __restrict__ q = (const float4*)(nodes + node);
     const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     int4 ch = *(const int4*)(q + 6);
@@ -485,9 +493,9 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     cswap(d[1], c[1], d[2], c[2]);
     // far-first pushes: stack[sp + j] = c[nh - 1 - j] for j < nh - 1 (exec-masked stores, so the
     // stack never holds more than the pushes themselves: mfx_scene.cpp's Collapse4 bound)
-    if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]));
-    if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1]);
-    if (nh >= 4) stack.put(sp + 2, c[1]);
+    if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]), dp);
+    if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1], dp);
+    if (nh >= 4) stack.put(sp + 2, c[1], dp);
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);

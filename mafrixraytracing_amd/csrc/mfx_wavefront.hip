@@ -217,7 +217,8 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         T.tlim = f_round_up(T.B.t);
     }
     if (T.sp == 0) return true;
-    T.node = stack.get(--T.sp);
+    T.node = stack.get(T.sp - 1, stack.deep(T.sp));
+    --T.sp;
     return false;
 }
 
