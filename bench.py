@@ -227,7 +227,12 @@ def main():
             def kernel_roofline(kname, kms, krays, launches, bray):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
                 achieved = krays * bray / (kms / 1e3) / 1e9
-                traffic = tdata.get("kernels", {}).get(kname, {}).get("hbm_bytes_per_launch") if tdata else None
+                traffic = None
+                if tdata:  # rocprof names the instance: k_shadow<false> or k_shadow<false, SPILL>
+                    base = kname.split(">")[0]
+                    for kk, kv in tdata.get("kernels", {}).items():
+                        if kk == kname or kk.startswith(base + ","):
+                            traffic = kv.get("hbm_bytes_per_launch")
                 return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                         "kernel": kname, "launches_per_step": launches,
