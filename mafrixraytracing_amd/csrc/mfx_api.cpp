@@ -87,6 +87,7 @@ struct mfx_ctx {
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     int wf_stack_lds = 1;            // traversal stack entries per lane in LDS (the rest spill)
+    int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     bool diag_iter = false;
 };
@@ -198,11 +199,11 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     // +14 %; when the full stacks already allow k_extend its 4 blocks and k_shadow 3 (C2, C5), the
     // spilling instances' extra stack arithmetic costs more than k_shadow's fourth block gains.
     int ebpc = 0, sbpc = 0;
-    CK(mfx_wf_occupancy(c->stack_size, false, &ebpc, &sbpc));
+    CK(mfx_wf_occupancy(c->stack_size, false, 0, 0, &ebpc, &sbpc));
     c->wf_stack_lds = c->stack_size;
     if (c->stack_size > WF_STACK_LDS) {
         int e2 = 0, s2 = 0;
-        CK(mfx_wf_occupancy(WF_STACK_LDS, true, &e2, &s2));
+        CK(mfx_wf_occupancy(WF_STACK_LDS, true, 0, 0, &e2, &s2));
         if (e2 > ebpc || (sbpc < 3 && s2 > sbpc)) {
             c->wf_stack_lds = WF_STACK_LDS;
             ebpc = e2;
@@ -211,7 +212,27 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     }
     if (const char* e = getenv("MFX_STACK_LDS")) {
         c->wf_stack_lds = std::max(1, std::min(c->stack_size, atoi(e)));
-        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, &ebpc, &sbpc));
+        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, 0, 0, &ebpc, &sbpc));
+    }
+    {  // top BVH nodes in LDS: as many as fit in the LDS the resident blocks leave over
+        const bool spill = c->wf_stack_lds < c->stack_size;
+        int cap = std::min((int)c->host.nodes.size(), WF_NTOP_MAX);
+        if (const char* e = getenv("MFX_NTOP")) cap = std::max(0, std::min(cap, atoi(e)));
+        for (int k = 0; k < 2; ++k) {
+            const int want = k == 0 ? ebpc : sbpc;
+            int lo = 0, hi = cap;  // resident blocks do not grow with ntop: bisect the largest that keeps them
+            while (lo < hi) {
+                const int mid = (lo + hi + 1) / 2, ne = k == 0 ? mid : 0, ns = k == 0 ? 0 : mid;
+                int e3 = 0, s3 = 0;
+                CK(mfx_wf_occupancy(c->wf_stack_lds, spill, ne, ns, &e3, &s3));
+                if ((k == 0 ? e3 : s3) >= want) lo = mid;
+                else hi = mid - 1;
+            }
+            (k == 0 ? c->wf_ntop_ext : c->wf_ntop_shd) = lo;
+        }
+        if (c->diag_iter)
+            fprintf(stderr, "wavefront: stack %d/%d in LDS, blocks/CU extend %d shadow %d, top nodes in LDS %d / %d\n",
+                    c->wf_stack_lds, c->stack_size, ebpc, sbpc, c->wf_ntop_ext, c->wf_ntop_shd);
     }
     if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
         ebpc = std::min(ebpc, std::max(1, atoi(b)));
@@ -292,6 +313,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
     P.stack_lds = c->wf_stack_lds;
+    P.ntop_ext = c->wf_ntop_ext;
+    P.ntop_shd = c->wf_ntop_shd;
     P.spill = c->d_spill;
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;

@@ -33,6 +33,9 @@ struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache l
     int32_t pad[4];
 };
 #define MFX_CHILD_EMPTY (-0x7fffffff - 1)
+// nodes[0 .. MFX_TOP_NODES) are the BVH's top levels in breadth-first order (the trace kernels
+// keep a prefix of them in LDS); the rest follow in preorder
+#define MFX_TOP_NODES 128
 
 // reference leaf header (ref_blob[]); copies of its primitives' slots follow
 struct alignas(16) MfxLeaf {

@@ -724,6 +724,29 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
         for (int k = 0; k < 4; ++k)
             if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~code_of[~nd.child[k]];
 
+    // ---- renumber: the first MFX_TOP_NODES nodes breadth-first from the root, then the rest in
+    //      preorder (mfx_layout.h) -----------------------------------------------------------------
+    {
+        const int nn = (int)s.nodes.size();
+        std::vector<int> bfs{root};
+        for (size_t h = 0; h < bfs.size() && (int)bfs.size() < MFX_TOP_NODES; ++h)
+            for (int k = 0; k < 4 && (int)bfs.size() < MFX_TOP_NODES; ++k)
+                if (s.nodes[bfs[h]].child[k] >= 0) bfs.push_back(s.nodes[bfs[h]].child[k]);
+        std::vector<int> idx(nn, -1);
+        int next = 0;
+        for (int v : bfs) idx[v] = next++;
+        for (int v = 0; v < nn; ++v)
+            if (idx[v] < 0) idx[v] = next++;
+        std::vector<MfxNode> renum(nn);
+        for (int v = 0; v < nn; ++v) {
+            MfxNode nd = s.nodes[v];
+            for (int k = 0; k < 4; ++k)
+                if (nd.child[k] >= 0) nd.child[k] = idx[nd.child[k]];
+            renum[idx[v]] = nd;
+        }
+        s.nodes.swap(renum);
+    }
+
     // ---- reference leaves (heap order): FP64 box header + slot copies ----------------------
     s.ref_blob.clear();
     for (int c = 0; c < nc; ++c) {

@@ -453,14 +453,48 @@ __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
     db = s ? t : db;
     cb = s ? u : cb;
 }
-template <typename ST>
+// LDS copy of the first `ntop` nodes (the BVH's top levels: mfx_scene.cpp numbers them first, in
+// breadth-first order). Node n's 16-B column c sits at float4 n * 8 + (c ^ ((n >> 1) & 7)), so
+// lanes reading the same column of different nodes spread over the LDS banks.
+struct TopNodes {
+    const float4* lds;
+    int ntop;
+};
+__device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
+// block-wide copy at kernel start (all threads; ends with a barrier)
+__device__ __forceinline__ void load_top_nodes(float4* lds, const MfxNode* __restrict__ nodes, int ntop) {
+    const float4* __restrict__ g = (const float4*)nodes;
+    for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
+    __syncthreads();
+}
+
+template <bool TOP = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp) {
+                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
+    float4 lx, hx, ly, hy, lz, hz;
+    int4 ch;
+#ifdef MFX_TOP_DIVERGENT
+    if (TOP && node < tn.ntop) {  // a top-level node: from LDS
+#else
+    // wave-uniform: from LDS when every stepping lane is at a top-level node (a divergent split would
+    // serialize the two paths: the LDS and global loads write the same registers)
+    if (TOP && __ballot(node >= tn.ntop) == 0) {
+#endif
+        const int sw = (node >> 1) & 7;
+        const float4* t = tn.lds + node * 8;
+        lx = t[0 ^ sw]; hx = t[1 ^ sw]; ly = t[2 ^ sw]; hy = t[3 ^ sw]; lz = t[4 ^ sw]; hz = t[5 ^ sw];
+        const float4 c4 = t[6 ^ sw];
+        ch = make_int4(__float_as_int(c4.x), __float_as_int(c4.y), __float_as_int(c4.z), __float_as_int(c4.w));
+    } else {
+        const float4* __restrict__ q = (const float4*)(nodes + node);
+        lx = q[0]; hx = q[1]; ly = q[2]; hy = q[3]; lz = q[4]; hz = q[5];
+        ch = *(const int4*)(q + 6);
+    }
+#ifdef MFX_DIAG_EXTRA_NODE_LOADS
     const float4* __restrict__ q = (const float4*)(nodes + node);
-    const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
-    int4 ch = *(const int4*)(q + 6);
+#endif
 #ifdef MFX_DIAG_EXTRA_NODE_LOADS  // timing experiment: MFX_DIAG_EXTRA_NODE_LOADS more 16-B loads per step
 #pragma unroll
     for (int k = 0; k < MFX_DIAG_EXTRA_NODE_LOADS; ++k) {

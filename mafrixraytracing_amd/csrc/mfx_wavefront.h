@@ -80,6 +80,7 @@ struct WfParams {
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
+    int32_t ntop_ext, ntop_shd;           // top BVH nodes each trace kernel keeps in LDS (<= nodes)
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool
@@ -89,8 +90,13 @@ struct WfParams {
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)
 #endif
-// resident blocks per CU of each kernel with `stack_lds` stack entries per lane in LDS
-hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int* ext_blocks_per_cu, int* shd_blocks_per_cu);
+#ifndef WF_NTOP_MAX
+#define WF_NTOP_MAX MFX_TOP_NODES  // top BVH nodes a trace kernel may keep in LDS (mfx_scene.cpp numbers them first)
+#endif
+// resident blocks per CU of each kernel with `stack_lds` stack entries per lane and ntop_* top
+// BVH nodes in LDS
+hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
+                            int* shd_blocks_per_cu);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

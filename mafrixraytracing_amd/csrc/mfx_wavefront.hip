@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "mfx_device.h"
@@ -196,12 +197,12 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
 template <bool SHADOW, bool STATS, typename ST>
-__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, Stats& st,
+__device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
                                           DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = node_step(S.nodes, T.node, T.rf, T.tlim, stack, T.sp);
+        T.node = node_step<true>(S.nodes, T.node, T.rf, T.tlim, stack, T.sp, tn);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
         if (__popcll(__ballot(T.node >= 0)) < MFX_NODE_LANES_MIN) break;
@@ -262,7 +263,10 @@ struct PendShd {
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool SPILL>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
-    extern __shared__ int lds[];
+    extern __shared__ int lds_all[];
+    const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
+    int* lds = lds_all + P.ntop_ext * 32;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -357,7 +361,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
-        if (active) fin = trav_step<false, STATS>(T, S, stack, st, dg, DG);
+        if (active) fin = trav_step<false, STATS>(T, S, stack, tn, st, dg, DG);
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
             const int fl = fresh ? WF_FRESH : 0;
@@ -395,7 +399,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool SPILL>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
-    extern __shared__ int lds[];
+    extern __shared__ int lds_all[];
+    const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
+    int* lds = lds_all + P.ntop_shd * 32;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -571,7 +578,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
             fin = true;
         }
 #else
-        if (active) fin = trav_step<true, STATS>(T, S, stack, st, dg, DG);
+        if (active) fin = trav_step<true, STATS>(T, S, stack, tn, st, dg, DG);
 #endif
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
@@ -646,19 +653,33 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-// stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
-static size_t wf_lds_bytes(int stack_size, bool shadow) {
-    const size_t stacks = (size_t)4 * stack_size * 64 * sizeof(int);
+// top nodes, stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
+static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop) {
+    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
-hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int* ext_blocks_per_cu, int* shd_blocks_per_cu) {
+// Blocks per CU the LDS allows. gfx950 allocates LDS in 1,280-byte granules out of 160 KB per CU;
+// hipOccupancyMaxActiveBlocksPerMultiprocessor counts finer granules, so near a boundary it
+// reports one block more than fits (measured: k_shadow at 53,952 B per block runs 2 blocks per CU
+// where the API says 3, a 10 % loss).
+static int wf_lds_blocks(size_t bytes) {
+    const size_t g = 1280, per_cu = 160 * 1024;
+    return (int)(per_cu / ((bytes + g - 1) / g * g));
+}
+
+hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
+                            int* shd_blocks_per_cu) {
+    const size_t le = wf_lds_bytes(stack_lds, false, ntop_ext), ls = wf_lds_bytes(stack_lds, true, ntop_shd);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        ext_blocks_per_cu, spill ? k_extend<false, true> : k_extend<false, false>, 256, wf_lds_bytes(stack_lds, false));
+        ext_blocks_per_cu, spill ? k_extend<false, true> : k_extend<false, false>, 256, le);
     if (e != hipSuccess) return e;
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        shd_blocks_per_cu, spill ? k_shadow<false, true> : k_shadow<false, false>, 256, wf_lds_bytes(stack_lds, true));
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu,
+                                                     spill ? k_shadow<false, true> : k_shadow<false, false>, 256, ls);
+    *ext_blocks_per_cu = std::min(*ext_blocks_per_cu, wf_lds_blocks(le));
+    *shd_blocks_per_cu = std::min(*shd_blocks_per_cu, wf_lds_blocks(ls));
+    return e;
 }
 
 template <bool SPILL>
@@ -677,7 +698,8 @@ static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
-    const size_t lds_e = wf_lds_bytes(P.stack_lds, false), lds_s = wf_lds_bytes(P.stack_lds, true);
+    const size_t lds_e = wf_lds_bytes(P.stack_lds, false, P.ntop_ext);
+    const size_t lds_s = wf_lds_bytes(P.stack_lds, true, P.ntop_shd);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     if (P.stack_lds < P.stack_size)
