@@ -472,7 +472,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                     const uint64_t key = P.key[j];
                     uint32_t rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
                     // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
-#if MFX_HEMI_FP32_SCREEN
+#if defined(MFX_DIAG_ONE_TRIAL)  // timing experiment only: the first trial, mirrored into the hemisphere
+                    DV p = dv(rng_next(key, rn) * 2.0 - 1.0, rng_next(key, rn) * 2.0 - 1.0, rng_next(key, rn) * 2.0 - 1.0);
+                    if (vdot(nm, p) <= 0.) p = vmul(p, -1.0);
+#elif MFX_HEMI_FP32_SCREEN
                     const DV p = hemisphere_ball(nm, key, rn);
 #else
                     DV p = dv(20, 20, 20);
