@@ -441,9 +441,15 @@ struct SpillStack {
 
 // One internal-node step of the BVH4, branch-free: four child slab tests, the hit children sorted
 // near to far (5-comparator network over (entry distance, child), misses sorted last at +inf),
-// then descend into the nearest, push the others far-first, or pop. The pop candidate (top of stack) is read before the node's boxes arrive, so
-// the LDS read overlaps the L2 load. Returns the next node: >= 0 internal, < 0 a leaf (~offset),
-// or MFX_TRAV_EXIT when nothing is left. An empty child (box at FLT_MAX) never hits.
+// then descend into the nearest, push the others far-first, or pop. The pop candidate (top of
+// stack) is read before the node's boxes arrive, so the LDS read overlaps the L2 load. Returns the
+// next node: >= 0 internal, < 0 a leaf (~offset), or MFX_TRAV_EXIT when nothing is left. An empty
+// child (box at FLT_MAX) never hits.
+// FAR (shadow rays): the children are visited far to near by exit distance. Whether a shadow ray
+// is occluded does not depend on the order (the any-hit test keeps tMax fixed, and a leaf that
+// reports a hit under a shrunken tMax also does under the original one), and the occluder of a
+// ray leaving a surface is seldom near its origin. Near-first walked every node around the origin
+// first: C2 shadow rays 7.26 -> 5.58 node and 2.32 -> 1.57 leaf visits, +12 % on the frame.
 __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
     const bool s = db < da;
     const float t = da;
@@ -468,7 +474,7 @@ __device__ __forceinline__ void load_top_nodes(float4* lds, const MfxNode* __res
     __syncthreads();
 }
 
-template <bool TOP = false, typename ST>
+template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
@@ -515,7 +521,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = n <= f;
-        d[k] = h ? n : __builtin_inff();
+        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
         nh += h ? 1 : 0;
     }
     cswap(d[0], c[0], d[1], c[1]);
@@ -550,7 +556,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            node = node_step(S.nodes, node, rf, tlim, LdsStack{stack}, sp);
+            node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, LdsStack{stack}, sp);
         }
         if (node == MFX_TRAV_EXIT) return B.found;
         // ---- leaf ----

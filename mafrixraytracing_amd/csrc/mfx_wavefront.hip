@@ -41,6 +41,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define MFX_HEMI_FP32_SCREEN 1  // rejection trials decided in FP32 away from the boundary (exact)
 #endif
 
+#ifndef MFX_SHADOW_ORDER
+#define MFX_SHADOW_ORDER 1  // shadow rays' child order: 0 near-first, 1 far-first (by exit distance)
+#endif
+
 #ifndef MFX_NODE_LANES_MIN
 #define MFX_NODE_LANES_MIN 12  // node-loop early exit: fewer lanes than this still stepping
 #endif
@@ -174,6 +178,9 @@ __device__ __forceinline__ typename std::conditional<SPILL, SpillStack, LdsStack
 
 // Traversal state of one lane (one ray) across outer-loop iterations
 struct Trav {
+#ifdef MFX_DIAG_OCCLUSION
+    uint32_t n0, l0;  // the lane's node / cluster counts when this ray started
+#endif
     DV o, d;
     double tmax64;
     Best B;
@@ -202,7 +209,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     while (T.node >= 0) {
         if (STATS) st.nodes++;
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = node_step<true>(S.nodes, T.node, T.rf, T.tlim, stack, T.sp, tn);
+        T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, T.rf, T.tlim, stack, T.sp, tn);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
         if (__popcll(__ballot(T.node >= 0)) < MFX_NODE_LANES_MIN) break;
@@ -426,6 +433,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     bool cont = false;                        // the path continues after this vertex
     uint32_t c_shadow = 0;
     Stats st{0, 0, 0};
+#ifdef MFX_DIAG_OCCLUSION
+    uint32_t dg_occ = 0, dg_occ_nodes = 0, dg_occ_leaves = 0;
+#endif
     constexpr bool DG = MFX_DIAG_STAMPS == 2;
     DiagAcc dg{0, 0, 0, 0, 0, 0, 0, 0};
     if (DG) dg.last = stamp();
@@ -564,6 +574,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
                 // origin = the hit point k_extend stored (a cache hit: the shading just read it)
                 trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            pd.v[3 * 64 + e]);
+#ifdef MFX_DIAG_OCCLUSION
+                T.n0 = st.nodes;
+                T.l0 = st.clusters;
+#endif
                 idle = false;
                 active = true;
             }
@@ -585,6 +599,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
 #endif
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
+#ifdef MFX_DIAG_OCCLUSION  // STATS build: occluded shadow rays and their node / cluster visits
+            if (STATS && T.B.found) {
+                dg_occ++;
+                dg_occ_nodes += st.nodes - T.n0;
+                dg_occ_leaves += st.clusters - T.l0;
+            }
+#endif
             double lx = 0.0, ly = 0.0, lz = 0.0;  // a first vertex's radiance so far is 0
             if (!fresh) { lx = P.lx[s]; ly = P.ly[s]; lz = P.lz[s]; }
             if (!T.B.found) {  // unoccluded: add this vertex's direct-light term
@@ -613,6 +634,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) 
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);
+#ifdef MFX_DIAG_OCCLUSION
+        block_add<4>(cnt + 10, dg_occ, red);
+        block_add<4>(cnt + 11, dg_occ_nodes, red);
+        block_add<4>(cnt + 12, dg_occ_leaves, red);
+#endif
         block_add<4>(cnt + 8, st.clusters, red);
         block_add<4>(cnt + 9, st.prims, red);
     }

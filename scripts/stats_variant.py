@@ -33,3 +33,7 @@ if __name__ == "__main__":
               f"{c[4] / max(rc, 1):.2f} leaves {c[5] / max(rc, 1):.2f} prims {c[6] / max(rc, 1):.2f} | per shadow "
               f"ray: nodes {c[7] / max(rs, 1):.2f} leaves {c[8] / max(rs, 1):.2f} prims {c[9] / max(rs, 1):.2f}",
               flush=True)
+        if c[10] > 0:  # MFX_DIAG_OCCLUSION builds: occluded shadow rays
+            print(f"  occluded shadow rays {c[10] / max(rs, 1):.3f}: nodes {c[11] / c[10]:.2f} leaves "
+                  f"{c[12] / c[10]:.2f} per occluded ray; unoccluded: nodes {(c[7] - c[11]) / max(rs - c[10], 1):.2f} "
+                  f"leaves {(c[8] - c[12]) / max(rs - c[10], 1):.2f}", flush=True)
