@@ -156,6 +156,9 @@ struct SceneView {
 
 struct Stats {
     uint32_t nodes, clusters, prims;  // internal-node visits, leaf visits, primitive tests
+#ifdef MFX_DIAG_OCCLUSION
+    uint32_t after_nodes, after_leaves;  // closest-hit visits made after the ray's first hit
+#endif
 };
 
 // The best hit so far under the reference's order: smallest t; equal t -> the later reference

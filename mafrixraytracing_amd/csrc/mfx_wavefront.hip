@@ -208,6 +208,9 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
                                           DiagAcc& dg, bool diag) {
     while (T.node >= 0) {
         if (STATS) st.nodes++;
+#ifdef MFX_DIAG_OCCLUSION
+        if (STATS && !SHADOW && T.B.found) st.after_nodes++;
+#endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
         T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, T.rf, T.tlim, stack, T.sp, tn);
         // leave the node loop once few lanes still step: the rest resume next round, after the
@@ -217,6 +220,9 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     DIAG_MARK(dg, node, diag);
     if (T.node >= 0) return false;
     if (T.node == MFX_TRAV_EXIT) return true;
+#ifdef MFX_DIAG_OCCLUSION
+    if (STATS && !SHADOW && T.B.found) st.after_leaves++;
+#endif
     if (leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st)) {
         if (SHADOW) {
             T.B.found = true;
@@ -398,6 +404,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         block_add<4>(cnt + 4, st.nodes, red);
         block_add<4>(cnt + 5, st.clusters, red);
         block_add<4>(cnt + 6, st.prims, red);
+#ifdef MFX_DIAG_OCCLUSION
+        block_add<4>(cnt + 13, st.after_nodes, red);
+        block_add<4>(cnt + 14, st.after_leaves, red);
+#endif
     }
 }
 

@@ -36,4 +36,5 @@ if __name__ == "__main__":
         if c[10] > 0:  # MFX_DIAG_OCCLUSION builds: occluded shadow rays
             print(f"  occluded shadow rays {c[10] / max(rs, 1):.3f}: nodes {c[11] / c[10]:.2f} leaves "
                   f"{c[12] / c[10]:.2f} per occluded ray; unoccluded: nodes {(c[7] - c[11]) / max(rs - c[10], 1):.2f} "
-                  f"leaves {(c[8] - c[12]) / max(rs - c[10], 1):.2f}", flush=True)
+                  f"leaves {(c[8] - c[12]) / max(rs - c[10], 1):.2f}; closest rays after their first hit: "
+                  f"nodes {c[13] / max(rc, 1):.2f} leaves {c[14] / max(rc, 1):.2f} per ray", flush=True)
