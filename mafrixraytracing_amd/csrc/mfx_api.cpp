@@ -88,6 +88,7 @@ struct mfx_ctx {
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     int wf_stack_lds = 1;            // traversal stack entries per lane in LDS (the rest spill)
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
+    int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     bool diag_iter = false;
 };
@@ -230,9 +231,16 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
             }
             (k == 0 ? c->wf_ntop_ext : c->wf_ntop_shd) = lo;
         }
+        // k_shadow with at most 3 resident blocks per CU (its LDS) runs the instance compiled for 3
+        // waves per SIMD: more registers, no spills (C2 / C5 +2 %); with 4 it keeps the 4-wave one
+        c->wf_shadow_waves = sbpc <= 3 ? 3 : 4;
+        if (const char* e = getenv("MFX_SHADOW_WAVES")) c->wf_shadow_waves = atoi(e) == 3 ? 3 : 4;
+        if (c->wf_shadow_waves == 3) sbpc = std::min(sbpc, 3);
         if (c->diag_iter)
-            fprintf(stderr, "wavefront: stack %d/%d in LDS, blocks/CU extend %d shadow %d, top nodes in LDS %d / %d\n",
-                    c->wf_stack_lds, c->stack_size, ebpc, sbpc, c->wf_ntop_ext, c->wf_ntop_shd);
+            fprintf(stderr,
+                    "wavefront: stack %d/%d in LDS, blocks/CU extend %d shadow %d (%d-wave build), top nodes in LDS "
+                    "%d / %d\n",
+                    c->wf_stack_lds, c->stack_size, ebpc, sbpc, c->wf_shadow_waves, c->wf_ntop_ext, c->wf_ntop_shd);
     }
     if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
         ebpc = std::min(ebpc, std::max(1, atoi(b)));
@@ -315,6 +323,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.stack_lds = c->wf_stack_lds;
     P.ntop_ext = c->wf_ntop_ext;
     P.ntop_shd = c->wf_ntop_shd;
+    P.shadow_waves = c->wf_shadow_waves;
     P.spill = c->d_spill;
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;

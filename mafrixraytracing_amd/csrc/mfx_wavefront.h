@@ -81,6 +81,7 @@ struct WfParams {
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
     int32_t ntop_ext, ntop_shd;           // top BVH nodes each trace kernel keeps in LDS (<= nodes)
+    int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool

@@ -414,8 +414,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool SPILL>
-__global__ void __launch_bounds__(256, MFX_TRAV_WAVES > 4 ? MFX_TRAV_WAVES : 4) k_shadow(WfParams P) {
+template <bool STATS, bool SPILL, int WAVES>
+__global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
@@ -715,13 +715,13 @@ hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_sh
         ext_blocks_per_cu, spill ? k_extend<false, true> : k_extend<false, false>, 256, le);
     if (e != hipSuccess) return e;
     e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu,
-                                                     spill ? k_shadow<false, true> : k_shadow<false, false>, 256, ls);
+                                                     spill ? k_shadow<false, true, 4> : k_shadow<false, false, 4>, 256, ls);
     *ext_blocks_per_cu = std::min(*ext_blocks_per_cu, wf_lds_blocks(le));
     *shd_blocks_per_cu = std::min(*shd_blocks_per_cu, wf_lds_blocks(ls));
     return e;
 }
 
-template <bool SPILL>
+template <bool SPILL, int WAVES>
 static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                              hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
     if (stats)
@@ -730,9 +730,9 @@ static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool
         hipLaunchKernelGGL((k_extend<false, SPILL>), dim3(ext_grid), dim3(256), lds_e, st, P);
     if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return;
     if (stats)
-        hipLaunchKernelGGL((k_shadow<true, SPILL>), dim3(shd_grid), dim3(256), lds_s, st, P);
+        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES>), dim3(shd_grid), dim3(256), lds_s, st, P);
     else
-        hipLaunchKernelGGL((k_shadow<false, SPILL>), dim3(shd_grid), dim3(256), lds_s, st, P);
+        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES>), dim3(shd_grid), dim3(256), lds_s, st, P);
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
@@ -741,10 +741,13 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     const size_t lds_s = wf_lds_bytes(P.stack_lds, true, P.ntop_shd);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    if (P.stack_lds < P.stack_size)
-        launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else
-        launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    // k_shadow compiled for 3 waves per SIMD (up to 168 VGPRs, no spills) when its LDS allows no
+    // more blocks anyway, else for 4 (128 VGPRs, a few spills)
+    const bool spill = P.stack_lds < P.stack_size, w3 = P.shadow_waves == 3;
+    if (spill && w3) launch_iteration<true, 3>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else if (spill) launch_iteration<true, 4>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else if (w3) launch_iteration<false, 3>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else launch_iteration<false, 4>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
