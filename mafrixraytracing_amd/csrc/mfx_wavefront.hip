@@ -46,7 +46,10 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #endif
 
 #ifndef MFX_NODE_LANES_MIN
-#define MFX_NODE_LANES_MIN 12  // node-loop early exit: fewer lanes than this still stepping
+#define MFX_NODE_LANES_MIN 16  // node-loop early exit: fewer lanes than this still stepping
+#endif
+#ifndef MFX_NODE_LANES_MIN_SHD
+#define MFX_NODE_LANES_MIN_SHD 12  // the same for shadow rays
 #endif
 
 #ifndef MFX_DIAG_STAMPS
@@ -215,7 +218,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, rf, tlim, stack, T.sp, tn);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
-        if (__popcll(__ballot(T.node >= 0)) < MFX_NODE_LANES_MIN) break;
+        if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
     }
     DIAG_MARK(dg, node, diag);
     if (T.node >= 0) return false;
