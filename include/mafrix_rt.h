@@ -130,6 +130,9 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * rgba may be NULL (accumulate only).                                                      */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
+/* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */
+int mfx_accumulate_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
+
 /* == Film.Reset (Film.fs:26-30): zero the film accumulator and its frame count. */
 int mfx_reset(mfx_ctx* ctx);
 
@@ -174,6 +177,12 @@ int mfx_trace_timing(mfx_ctx* ctx, double out[8]);
  * MFX_F_COUNT_STATS: out[4..6] = internal-node visits, cluster (reference leaf) visits and
  * primitive tests of the closest-hit queries, out[7..9] the same for the shadow queries.     */
 int mfx_ray_counts(mfx_ctx* ctx, double out[16]);
+
+/* SURVEY.md §8(b)'s stats call, for the Mrays/s metric (§8(d)): rays = primary + extension +
+ * shadow rays traced by the last mfx_sample / mfx_render_rgba8 / mfx_trace_accumulate call (the
+ * sum of mfx_ray_counts out[0..2]), seconds = its device time (mfx_last_trace_ms / 1000; waits
+ * for the call's kernels). Either pointer may be NULL.                                        */
+int mfx_stats(mfx_ctx* ctx, double* rays, double* seconds);
 
 /* ---- query entry points (parity tests of the BVH/intersection layer) ----------------- */
 

@@ -106,6 +106,8 @@ def _bind(lib):
         "mfx_destroy": (None, [C.c_void_p]),
         "mfx_sample": (C.c_int, [C.c_void_p, C.c_int32, _dp]),
         "mfx_render_rgba8": (C.c_int, [C.c_void_p, C.c_int32, _P(C.c_uint8)]),
+        "mfx_accumulate_render_rgba8": (C.c_int, [C.c_void_p, C.c_int32, _P(C.c_uint8)]),
+        "mfx_stats": (C.c_int, [C.c_void_p, _dp, _dp]),
         "mfx_reset": (C.c_int, [C.c_void_p]),
         "mfx_film_mean": (C.c_int, [C.c_void_p, _dp]),
         "mfx_trace_accumulate": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
@@ -136,7 +138,8 @@ def _bind(lib):
 
 
 EXPORTED_SYMBOLS = [
-    "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_reset", "mfx_film_mean",
+    "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
+    "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
     "mfx_fp64_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",

@@ -546,6 +546,25 @@ int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     return MFX_OK;
 }
 
+int mfx_accumulate_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) { return mfx_render_rgba8(c, spp, rgba); }
+
+int mfx_stats(mfx_ctx* c, double* rays, double* seconds) {
+    if (!c) return fail(MFX_E_INVALID, "null context");
+    if (seconds) {
+        double ms = 0;
+        int rc = mfx_last_trace_ms(c, &ms);
+        if (rc) return rc;
+        *seconds = ms * 1e-3;
+    }
+    if (rays) {
+        double n[16];
+        int rc = mfx_ray_counts(c, n);
+        if (rc) return rc;
+        *rays = n[0] + n[1] + n[2];
+    }
+    return MFX_OK;
+}
+
 int mfx_reset(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
     HIPCHECK(hipSetDevice(c->device));

@@ -102,6 +102,12 @@ class NativeContext:
         check(self.lib.mfx_ray_counts(self._h, dptr(out)), "mfx_ray_counts")
         return out
 
+    def stats(self) -> tuple[float, float]:
+        """(rays traced, device seconds) of the last trace call (mfx_stats)."""
+        rays, sec = C.c_double(), C.c_double()
+        check(self.lib.mfx_stats(self._h, C.byref(rays), C.byref(sec)), "mfx_stats")
+        return rays.value, sec.value
+
     def last_trace_ms(self) -> float:
         ms = C.c_double()
         check(self.lib.mfx_last_trace_ms(self._h, C.byref(ms)), "mfx_last_trace_ms")

@@ -215,3 +215,23 @@ def test_megakernel_and_wavefront_counters_agree(gpu):
     assert np.array_equal(cw[:4], cm[:4])
     # identical traversal algorithm per ray -> identical visit counts
     assert np.array_equal(cw[4:10], cm[4:10])
+
+
+@pytest.mark.gpu
+def test_survey_named_entry_points(gpu):
+    """mfx_accumulate_render_rgba8 (SURVEY §8(b)'s name) == mfx_render_rgba8 on a twin context, and
+    mfx_stats reports the last call's rays (primary + extension + shadow) and device time."""
+    import ctypes as C
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("two_spheres_plane", 40, 30)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED) as c2:
+        for _ in range(2):
+            r1 = c1.render_rgba8(2)
+            r2 = np.empty(40 * 30 * 4, dtype=np.uint8)
+            rc = c2.lib.mfx_accumulate_render_rgba8(c2._h, 2, r2.ctypes.data_as(C.POINTER(C.c_uint8)))
+            assert rc == 0
+            assert np.array_equal(r1, r2)
+        rays, sec = c2.stats()
+        n = c2.ray_counts()
+        assert rays == n[0] + n[1] + n[2] and rays > 0
+        assert 0 < sec < 10 and abs(sec * 1e3 - c2.last_trace_ms()) < 1e-9
