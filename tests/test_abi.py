@@ -48,6 +48,9 @@ def test_version_errors_and_no_cpu_fallback():
     opt = MfxOptions(seed=1, device=0, flags=0, part_index=0, part_count=1)
     assert lib.mfx_create(None, C.byref(opt), C.byref(h)) == -1
     assert b"null" in lib.mfx_last_error()
+    rays, sec = C.c_double(), C.c_double()
+    assert lib.mfx_stats(None, C.byref(rays), C.byref(sec)) == -1
+    assert lib.mfx_accumulate_render_rgba8(None, 1, None) == -1
     opt.part_count = 0
     from conftest import scene
     d = scene("cornell", 4, 4).desc()
