@@ -30,7 +30,8 @@
 extern "C" {
 #endif
 
-#define MFX_ABI_VERSION 1
+#define MFX_ABI_VERSION 2
+#define MFX_MAX_DEVICES 64
 
 /* error codes */
 #define MFX_OK 0
@@ -91,14 +92,24 @@ typedef struct mfx_scene_desc {
     mfx_pinhole camera;
 } mfx_scene_desc;
 
-/* Context options. */
+/* Context options.
+ * Devices: with ndevices == 0 the context runs on `device`. With ndevices > 0 it drives
+ * devices[0..ndevices) from this one process (the reference's in-process fan-out,
+ * Integrators.fs:164, across GPUs): device g renders sample sub-partition
+ * part_index + g*part_count of part_count*ndevices on its own stream, and one RCCL reduce
+ * (a communicator the library owns, ncclCommInitAll over the list) sums the FP64 accumulators
+ * into devices[0], where film and post run. A list that repeats a device (e.g. {0,0}) adds the
+ * accumulators in device order instead (RCCL needs distinct devices).                        */
 typedef struct mfx_options {
     uint64_t seed;      /* counter-RNG seed; the reference uses unseeded System.Random */
-    int32_t device;     /* HIP device ordinal for this context */
+    int32_t device;     /* HIP device ordinal when ndevices == 0 */
     int32_t flags;      /* MFX_F_* */
     int32_t part_index; /* this context renders sample partition part_index of part_count */
-    int32_t part_count; /* (multi-GPU: one context per rank; partitions are disjoint sample sets) */
-} mfx_options;
+    int32_t part_count; /* (multi-process: one context per rank; partitions are disjoint sample sets) */
+    int32_t ndevices;   /* 0: one device (`device`); 1..MFX_MAX_DEVICES: the device list below */
+    int32_t reserved;
+    const int32_t* devices; /* [ndevices] HIP device ordinals; devices[0] is the primary */
+} mfx_options; /* 40 bytes */
 
 #define MFX_F_NONE 0
 #define MFX_F_COUNT_STATS 1 /* count traversal node/leaf/prim visits (slower; for the roofline model) */
@@ -143,17 +154,24 @@ int mfx_film_mean(mfx_ctx* ctx, double* frame_xmajor_rgba);
 
 /* Adds, for global samples [sample_base, sample_base + spp) of this context's partition,
  * the per-pixel radiance sums into the context's device accumulator (FP64, 3 planes of w*h,
- * plane-major, x-major pixels). Does not synchronise; mfx_sync() does.                      */
+ * plane-major, x-major pixels); on a multi-device context each device into its own.
+ * Does not synchronise; mfx_sync() does.                                                     */
 int mfx_trace_accumulate(mfx_ctx* ctx, int32_t spp, int64_t sample_base);
+/* Multi-device context: sum every device's accumulator into the primary's (RCCL reduce, root
+ * devices[0]), ordered after each device's trace. No-op on a single-device context.
+ * mfx_sample / mfx_render_rgba8 call it themselves.                                          */
+int mfx_accum_reduce(mfx_ctx* ctx);
 int mfx_accum_clear(mfx_ctx* ctx);
-/* Device pointer + byte size of the FP64 accumulator (for an RCCL reduce across ranks).    */
+/* Device pointer + byte size of the (primary device's) FP64 accumulator (for an RCCL reduce
+ * across ranks).                                                                             */
 int mfx_accum_device_ptr(mfx_ctx* ctx, void** dptr, int64_t* nbytes);
 /* Use caller-owned device memory (>= the size above, on this context's device) as the
  * accumulator — e.g. a buffer an RCCL reduce then works on in place; NULL restores the
  * context's own buffer. The caller keeps it alive until detached or mfx_destroy.            */
 int mfx_accum_attach(mfx_ctx* ctx, void* dptr, int64_t nbytes);
-/* Copy accumulator / inv_count to host as x-major RGBA doubles (alpha = 1).                */
-int mfx_accum_read_mean(mfx_ctx* ctx, double inv_count, double* frame_xmajor_rgba);
+/* Copy accumulator / count to host as x-major RGBA doubles (alpha = 1): the division by the
+ * sample count itself, as `color / float n` (Integrators.fs:171). count must be > 0.         */
+int mfx_accum_read_mean(mfx_ctx* ctx, double count, double* frame_xmajor_rgba);
 int mfx_sync(mfx_ctx* ctx);
 /* The HIP stream (hipStream_t) the context launches on, for event timing by the caller.   */
 int mfx_stream(mfx_ctx* ctx, void** stream);

@@ -20,6 +20,8 @@ MFX_F_NONE = 0
 MFX_F_COUNT_STATS = 1
 MFX_F_MEGAKERNEL = 2
 MFX_F_HOST_BVH = 4
+MFX_MAX_DEVICES = 64
+MFX_ABI_VERSION = 2
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -49,7 +51,8 @@ class MfxSceneDesc(C.Structure):
 
 class MfxOptions(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("flags", C.c_int32),
-                ("part_index", C.c_int32), ("part_count", C.c_int32)]
+                ("part_index", C.c_int32), ("part_count", C.c_int32),
+                ("ndevices", C.c_int32), ("reserved", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
 assert C.sizeof(MfxPrim) == 104
@@ -112,6 +115,7 @@ def _bind(lib):
         "mfx_film_mean": (C.c_int, [C.c_void_p, _dp]),
         "mfx_trace_accumulate": (C.c_int, [C.c_void_p, C.c_int32, C.c_int64]),
         "mfx_accum_clear": (C.c_int, [C.c_void_p]),
+        "mfx_accum_reduce": (C.c_int, [C.c_void_p]),
         "mfx_accum_device_ptr": (C.c_int, [C.c_void_p, _P(C.c_void_p), _P(C.c_int64)]),
         "mfx_accum_read_mean": (C.c_int, [C.c_void_p, C.c_double, _dp]),
         "mfx_accum_attach": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int64]),
@@ -140,7 +144,7 @@ def _bind(lib):
 EXPORTED_SYMBOLS = [
     "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
     "mfx_film_mean", "mfx_stats",
-    "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
+    "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
     "mfx_fp64_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]

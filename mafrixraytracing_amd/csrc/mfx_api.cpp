@@ -1,9 +1,15 @@
 // mfx_api.cpp — the extern "C" boundary (include/mafrix_rt.h).
 //
-// One mfx_ctx = one `Scene` on one GPU: the scene images live in HBM from mfx_create until
-// mfx_destroy; every render call is a single persistent-kernel launch plus a small film/post
-// kernel, all on the context's own HIP stream. No call falls back to a CPU path.
+// One mfx_ctx = one `Scene` on one or more GPUs. Per device the scene images live in HBM from
+// mfx_create until mfx_destroy, and every render call is the wavefront pipeline's launches on
+// that device's own HIP stream. A context over G devices (mfx_options.devices) is a primary
+// device context plus G - 1 peers built from the same host scene; each device renders its own
+// sample partition, and one RCCL reduce (a communicator the library owns, ncclCommInitAll over
+// the device list) sums the FP64 accumulators into the primary's, where film and post run. No
+// call falls back to a CPU path.
+#include <dlfcn.h>
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 
 #include <algorithm>
 #include <cstdio>
@@ -12,6 +18,7 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <set>
 
 #include "../../include/mafrix_rt.h"
 #include "mfx_device.h"
@@ -31,6 +38,36 @@ int fail(int code, const std::string& msg) {
         hipError_t _e = (expr);                                                                      \
         if (_e != hipSuccess) return fail(MFX_E_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
     } while (0)
+
+// RCCL is opened when the first multi-device context is created, not linked: a process that
+// already holds an RCCL (PyTorch loads its own librccl.so, soname librccl.so.1) gets that same
+// instance back from dlopen by soname, so one process never maps two RCCLs; a process that
+// never creates a multi-device context never loads it at all.
+struct Rccl {
+    decltype(&ncclCommInitAll) commInitAll = nullptr;
+    decltype(&ncclCommDestroy) commDestroy = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclGroupStart) groupStart = nullptr;
+    decltype(&ncclGroupEnd) groupEnd = nullptr;
+    decltype(&ncclGetErrorString) errorString = nullptr;
+};
+const Rccl* rccl() {
+    static Rccl r;
+    static bool tried = false, ok = false;
+    if (tried) return ok ? &r : nullptr;
+    tried = true;
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return nullptr;
+    r.commInitAll = (decltype(r.commInitAll))dlsym(h, "ncclCommInitAll");
+    r.commDestroy = (decltype(r.commDestroy))dlsym(h, "ncclCommDestroy");
+    r.reduce = (decltype(r.reduce))dlsym(h, "ncclReduce");
+    r.groupStart = (decltype(r.groupStart))dlsym(h, "ncclGroupStart");
+    r.groupEnd = (decltype(r.groupEnd))dlsym(h, "ncclGroupEnd");
+    r.errorString = (decltype(r.errorString))dlsym(h, "ncclGetErrorString");
+    ok = r.commInitAll && r.commDestroy && r.reduce && r.groupStart && r.groupEnd && r.errorString;
+    return ok ? &r : nullptr;
+}
 
 template <typename T>
 hipError_t upload(T** dptr, const std::vector<T>& v) {
@@ -91,11 +128,32 @@ struct mfx_ctx {
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     bool diag_iter = false;
+    // ---- multi-device (primary context only) ----
+    int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
+    std::vector<mfx_ctx*> peers;         // devices[1..G) of the device list, same host scene
+    std::vector<ncclComm_t> comms;       // [G] one RCCL communicator per device, rank g = device g
+    double* d_reduce_stage = nullptr;    // repeated-device list: a peer's accumulator copied here
+    std::vector<hipEvent_t> peer_done;   // repeated-device list: per peer, its trace has finished
 };
+
+// the devices of a context, primary first
+static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
+    std::vector<mfx_ctx*> v{c};
+    v.insert(v.end(), c->peers.begin(), c->peers.end());
+    return v;
+}
 
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
+    for (ncclComm_t cm : c->comms)
+        if (cm) (void)rccl()->commDestroy(cm);
+    c->comms.clear();
+    for (mfx_ctx* p : c->peers) free_ctx(p);
+    c->peers.clear();
     (void)hipSetDevice(c->device);
+    for (hipEvent_t e : c->peer_done)
+        if (e) (void)hipEventDestroy(e);
+    if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill};
     for (void* b : bufs)
@@ -119,41 +177,18 @@ int mfx_device_count(void) {
     return n;
 }
 
-int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out) {
-    if (!scene || !opt || !out) return fail(MFX_E_INVALID, "mfx_create: null argument");
-    *out = nullptr;
-    if (opt->part_count < 1 || opt->part_index < 0 || opt->part_index >= opt->part_count)
-        return fail(MFX_E_INVALID, "mfx_create: bad sample partition");
-    int ndev = 0;
-    HIPCHECK(hipGetDeviceCount(&ndev));
-    if (opt->device < 0 || opt->device >= ndev) return fail(MFX_E_DEVICE, "mfx_create: no such HIP device");
-    HIPCHECK(hipSetDevice(opt->device));
-    mfx_ctx* c = new mfx_ctx();
-    std::string err;
-    // the traversal BVH is built on this device unless the caller asks for the host build (the
-    // same tree either way: tests/test_gpu_build.py)
-    if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0)) {
-        delete c;
-        const bool dev = err.rfind("GPU BVH build", 0) == 0;
-        return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
-    }
-    c->device = opt->device;
-    c->seed = opt->seed;
-    c->flags = opt->flags;
-    c->part_index = opt->part_index;
-    c->part_count = opt->part_count;
+// Device resources of a context whose host scene, device, seed, flags and partition are set:
+// stream, events, the scene images in HBM, accumulators, occupancy-derived launch shapes. On
+// failure the caller frees the context (free_ctx releases whatever was allocated).
+static int ctx_setup(mfx_ctx* c) {
     c->npix = (int64_t)c->host.width * c->host.height;
     c->stack_size = std::max(1, c->host.stack_entries);
-    if (c->stack_size > 96) {
-        free_ctx(c);
-        return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
-    }
+    if (c->stack_size > 96) return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
 #define CK(expr)                                                                               \
     do {                                                                                       \
         hipError_t _e = (expr);                                                                \
         if (_e != hipSuccess) {                                                                \
             std::string m = std::string(#expr) + ": " + hipGetErrorString(_e);                 \
-            free_ctx(c);                                                                       \
             return fail(_e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE, m);            \
         }                                                                                      \
     } while (0)
@@ -253,6 +288,105 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
         CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, c->stack_size - c->wf_stack_lds)));
     }
 #undef CK
+    return MFX_OK;
+}
+
+int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out) {
+    if (!scene || !opt || !out) return fail(MFX_E_INVALID, "mfx_create: null argument");
+    *out = nullptr;
+    if (opt->part_count < 1 || opt->part_index < 0 || opt->part_index >= opt->part_count)
+        return fail(MFX_E_INVALID, "mfx_create: bad sample partition");
+    if (opt->ndevices < 0 || opt->ndevices > MFX_MAX_DEVICES || (opt->ndevices > 0 && !opt->devices))
+        return fail(MFX_E_INVALID, "mfx_create: bad device list");
+    int ndev = 0;
+    HIPCHECK(hipGetDeviceCount(&ndev));
+    std::vector<int> devlist;
+    if (opt->ndevices == 0) devlist.push_back(opt->device);
+    else devlist.assign(opt->devices, opt->devices + opt->ndevices);
+    for (int d : devlist)
+        if (d < 0 || d >= ndev) return fail(MFX_E_DEVICE, "mfx_create: no such HIP device");
+    const int G = (int)devlist.size();
+    HIPCHECK(hipSetDevice(devlist[0]));
+    mfx_ctx* c = new mfx_ctx();
+    std::string err;
+    // the traversal BVH is built on the first device unless the caller asks for the host build
+    // (the same tree either way: tests/test_gpu_build.py); the other devices get copies
+    if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0)) {
+        delete c;
+        const bool dev = err.rfind("GPU BVH build", 0) == 0;
+        return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
+    }
+    // device g of G renders sub-partition part_index + g * part_count of part_count * G: the union
+    // over the devices is exactly the caller's partition (global samples s = part_index mod part_count)
+    auto init = [&](mfx_ctx* d, int g) {
+        d->device = devlist[g];
+        d->seed = opt->seed;
+        d->flags = opt->flags;
+        d->part_index = opt->part_index + g * opt->part_count;
+        d->part_count = opt->part_count * G;
+        d->api_part_count = opt->part_count;
+    };
+    init(c, 0);
+    int rc = ctx_setup(c);
+    if (rc) {
+        free_ctx(c);
+        return rc;
+    }
+    if (G > 1) {  // peers: one host thread each (HIP context creation and uploads run concurrently)
+        c->peers.assign(G - 1, nullptr);
+        std::vector<int> prc(G - 1, MFX_OK);
+        std::vector<std::string> perr(G - 1);
+        std::vector<std::thread> th;
+        for (int g = 1; g < G; ++g) {
+            mfx_ctx* p = new mfx_ctx();
+            p->host = c->host;
+            init(p, g);
+            c->peers[g - 1] = p;
+            th.emplace_back([p, g, &prc, &perr] {
+                prc[g - 1] = ctx_setup(p);
+                if (prc[g - 1]) perr[g - 1] = g_err;
+            });
+        }
+        for (auto& t : th) t.join();
+        for (int g = 1; g < G; ++g)
+            if (prc[g - 1]) {
+                free_ctx(c);
+                return fail(prc[g - 1], "device " + std::to_string(devlist[g]) + ": " + perr[g - 1]);
+            }
+    }
+    if (opt->ndevices > 0) {
+        // The device reduce. Distinct devices: one RCCL communicator per device, owned by the
+        // library (ncclCommInitAll, single process). A list that repeats a device cannot form a
+        // communicator: its accumulators are added into the primary's in device order instead.
+        const bool distinct = std::set<int>(devlist.begin(), devlist.end()).size() == devlist.size();
+        if (distinct) {
+            const Rccl* R = rccl();
+            if (!R) {
+                free_ctx(c);
+                return fail(MFX_E_DEVICE, "mfx_create: RCCL (librccl.so.1) could not be loaded");
+            }
+            c->comms.assign(G, nullptr);
+            const ncclResult_t r = R->commInitAll(c->comms.data(), G, devlist.data());
+            if (r != ncclSuccess) {
+                c->comms.clear();
+                free_ctx(c);
+                return fail(MFX_E_DEVICE, std::string("mfx_create: ncclCommInitAll: ") + R->errorString(r));
+            }
+        } else {
+            hipError_t e = hipSetDevice(c->device);
+            if (e == hipSuccess) e = hipMalloc((void**)&c->d_reduce_stage, 3 * sizeof(double) * (size_t)c->npix);
+            for (size_t k = 0; k < c->peers.size() && e == hipSuccess; ++k) {
+                hipEvent_t ev = nullptr;
+                e = hipSetDevice(c->peers[k]->device);
+                if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+                if (e == hipSuccess) c->peer_done.push_back(ev);
+            }
+            if (e != hipSuccess) {
+                free_ctx(c);
+                return fail(MFX_E_DEVICE, std::string("mfx_create: device reduce setup: ") + hipGetErrorString(e));
+            }
+        }
+    }
     *out = c;
     return MFX_OK;
 }
@@ -374,15 +508,21 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     return MFX_OK;
 }
 
-int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
-    if (!c) return fail(MFX_E_STATE, "null context");
-    if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
+// one device's share of mfx_trace_accumulate (its sample partition), enqueued on its stream
+static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(hipSetDevice(c->device));
     const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
     HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
     HIPCHECK(hipMemsetAsync(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long), c->stream));
     c->mega_last = (c->flags & MFX_F_MEGAKERNEL) != 0;
-    if (ns == 0) return MFX_OK;
+    if (ns == 0) {  // this partition has no sample in the call: zero rays in zero device time
+        HIPCHECK(hipEventRecord(c->ev0, c->stream));
+        HIPCHECK(hipEventRecord(c->ev1, c->stream));
+        c->ev_valid = true;
+        c->it_recorded = 0;
+        c->generations = 0;
+        return MFX_OK;
+    }
     if (!c->mega_last) return wf_trace(c, ns, sample_base);
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
@@ -410,6 +550,49 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(mfx_launch_trace(P, (c->flags & MFX_F_COUNT_STATS) != 0, c->grid, c->stream));
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
+    return MFX_OK;
+}
+
+// Every device enqueues its partition on its own stream; nothing here waits for a device, so the
+// G devices render concurrently.
+int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
+    for (mfx_ctx* d : devs_of(c)) {
+        const int rc = dev_trace_accumulate(d, spp, sample_base);
+        if (rc) return rc;
+    }
+    return MFX_OK;
+}
+
+// Sum every device's accumulator into the primary's, stream-ordered after each device's trace.
+int mfx_accum_reduce(mfx_ctx* c) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    if (!c->comms.empty()) {  // RCCL: rank g sends device g's buffer, the root reduces in place
+        const Rccl* R = rccl();  // loaded: the communicators exist
+        const size_t count = 3 * (size_t)c->npix;
+        const std::vector<mfx_ctx*> ds = devs_of(c);
+        ncclResult_t r = R->groupStart();
+        for (size_t g = 0; g < ds.size() && r == ncclSuccess; ++g) {
+            HIPCHECK(hipSetDevice(ds[g]->device));
+            r = R->reduce(ds[g]->d_accum, ds[g]->d_accum, count, ncclFloat64, ncclSum, 0, c->comms[g], ds[g]->stream);
+        }
+        const ncclResult_t r2 = R->groupEnd();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) return fail(MFX_E_DEVICE, std::string("mfx_accum_reduce: ") + R->errorString(r));
+        return MFX_OK;
+    }
+    // a repeated-device list: add the peers' accumulators in device order (a0 + a1) + a2 ...
+    const size_t bytes = 3 * sizeof(double) * (size_t)c->npix;
+    for (size_t k = 0; k < c->peers.size(); ++k) {
+        mfx_ctx* p = c->peers[k];
+        HIPCHECK(hipSetDevice(p->device));
+        HIPCHECK(hipEventRecord(c->peer_done[k], p->stream));
+        HIPCHECK(hipSetDevice(c->device));
+        HIPCHECK(hipStreamWaitEvent(c->stream, c->peer_done[k], 0));
+        HIPCHECK(hipMemcpyAsync(c->d_reduce_stage, p->d_accum, bytes, hipMemcpyDefault, c->stream));
+        HIPCHECK(mfx_launch_accum_add(c->d_accum, c->d_reduce_stage, 3 * c->npix, c->stream));
+    }
     return MFX_OK;
 }
 
@@ -444,19 +627,25 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
 
 int mfx_last_trace_ms(mfx_ctx* c, double* ms) {
     if (!c || !ms) return fail(MFX_E_INVALID, "null argument");
-    if (!c->ev_valid) return fail(MFX_E_STATE, "no trace launch recorded yet");
-    HIPCHECK(hipSetDevice(c->device));
-    HIPCHECK(hipEventSynchronize(c->ev1));
-    float f = 0.f;
-    HIPCHECK(hipEventElapsedTime(&f, c->ev0, c->ev1));
-    *ms = (double)f;
+    double worst = 0.0;  // the devices run concurrently: the slowest one's time
+    for (mfx_ctx* d : devs_of(c)) {
+        if (!d->ev_valid) return fail(MFX_E_STATE, "no trace launch recorded yet");
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipEventSynchronize(d->ev1));
+        float f = 0.f;
+        HIPCHECK(hipEventElapsedTime(&f, d->ev0, d->ev1));
+        worst = std::max(worst, (double)f);
+    }
+    *ms = worst;
     return MFX_OK;
 }
 
 int mfx_accum_clear(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
-    HIPCHECK(hipSetDevice(c->device));
-    HIPCHECK(hipMemsetAsync(c->d_accum, 0, 3 * sizeof(double) * (size_t)c->npix, c->stream));
+    for (mfx_ctx* d : devs_of(c)) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipMemsetAsync(d->d_accum, 0, 3 * sizeof(double) * (size_t)d->npix, d->stream));
+    }
     return MFX_OK;
 }
 
@@ -478,11 +667,12 @@ int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
     return MFX_OK;
 }
 
-int mfx_accum_read_mean(mfx_ctx* c, double inv_count, double* frame) {
+int mfx_accum_read_mean(mfx_ctx* c, double count, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
+    if (!(count > 0.0)) return fail(MFX_E_INVALID, "mfx_accum_read_mean: count must be > 0");
     HIPCHECK(hipSetDevice(c->device));
-    // texture[i,j] <- color / float n (Integrators.fs:171): divide by n = 1 / inv_count
-    HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, 1.0 / inv_count, c->d_frame, c->stream));
+    // texture[i,j] <- color / float n (Integrators.fs:171): divided by the count itself
+    HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, count, c->d_frame, c->stream));
     HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     return MFX_OK;
@@ -490,8 +680,10 @@ int mfx_accum_read_mean(mfx_ctx* c, double inv_count, double* frame) {
 
 int mfx_sync(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
-    HIPCHECK(hipSetDevice(c->device));
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (mfx_ctx* d : devs_of(c)) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipStreamSynchronize(d->stream));
+    }
     return MFX_OK;
 }
 
@@ -503,14 +695,17 @@ int mfx_stream(mfx_ctx* c, void** stream) {
 
 int mfx_ray_counts(mfx_ctx* c, double out[16]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
-    HIPCHECK(hipSetDevice(c->device));
-    unsigned long long h[16 * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
-    HIPCHECK(hipMemcpyAsync(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    for (int k = 0; k < 16; ++k) {
-        double v = 0;
-        for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[16 * g + k];
-        out[k] = v;
+    for (int k = 0; k < 16; ++k) out[k] = 0.0;
+    for (mfx_ctx* d : devs_of(c)) {  // summed over the context's devices
+        HIPCHECK(hipSetDevice(d->device));
+        unsigned long long h[16 * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
+        HIPCHECK(hipMemcpyAsync(h, d->d_counters, sizeof(h), hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipStreamSynchronize(d->stream));
+        for (int k = 0; k < 16; ++k) {
+            double v = 0;
+            for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[16 * g + k];
+            out[k] += v;
+        }
     }
     out[3] = out[0];  // paths == primary rays
     return MFX_OK;
@@ -518,7 +713,7 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
 
 int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
-    if (c->part_count != 1)
+    if (c->api_part_count != 1)
         return fail(MFX_E_STATE, "mfx_sample needs the whole sample set (part_count == 1); "
                                  "partitioned contexts compose with mfx_trace_accumulate + a reduce");
     int rc = mfx_accum_clear(c);
@@ -526,24 +721,34 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
     c->next_sample += spp;
-    return mfx_accum_read_mean(c, 1.0 / (double)spp, frame);
+    if (!c->peers.empty() || !c->comms.empty()) {
+        rc = mfx_accum_reduce(c);
+        if (rc) return rc;
+    }
+    rc = mfx_accum_read_mean(c, (double)spp, frame);
+    if (rc) return rc;
+    return mfx_sync(c);
 }
 
 int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     if (!c) return fail(MFX_E_INVALID, "null context");
-    if (c->part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
+    if (c->api_part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
     int rc = mfx_accum_clear(c);
     if (rc) return rc;
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
     c->next_sample += spp;
+    if (!c->peers.empty() || !c->comms.empty()) {
+        rc = mfx_accum_reduce(c);
+        if (rc) return rc;
+    }
     c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
     HIPCHECK(mfx_launch_film_post(c->d_accum, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
                                   rgba ? c->d_rgba : nullptr, c->stream));
     if (rgba)
         HIPCHECK(hipMemcpyAsync(rgba, c->d_rgba, 4 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
-    return MFX_OK;
+    return mfx_sync(c);
 }
 
 int mfx_accumulate_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) { return mfx_render_rgba8(c, spp, rgba); }

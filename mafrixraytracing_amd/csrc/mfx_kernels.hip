@@ -318,6 +318,13 @@ __global__ void film_mean_kernel(const double* __restrict__ film, int64_t npix, 
     out[4 * q + 3] = 1.0;
 }
 
+// dst += src, element-wise: one device's accumulator added into another's (the in-order device
+// reduce of a context whose device list repeats a device, where RCCL cannot form a communicator)
+__global__ void accum_add_kernel(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) dst[k] = dst[k] + src[k];
+}
+
 __global__ void fp64_selftest_kernel(const double* a, const double* b, int64_t n, double* dv_out, double* sq_out) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n) return;
@@ -373,5 +380,10 @@ hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_c
 
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo, hipStream_t st) {
     hipLaunchKernelGGL(fp64_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, a, b, n, dvo, sqo);
+    return hipGetLastError();
+}
+
+hipError_t mfx_launch_accum_add(double* dst, const double* src, int64_t n, hipStream_t st) {
+    hipLaunchKernelGGL(accum_add_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, dst, src, n);
     return hipGetLastError();
 }

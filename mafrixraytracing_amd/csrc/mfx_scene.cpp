@@ -433,6 +433,18 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
         err = "invalid film size or empty material table";
         return false;
     }
+    // one sample of the film is ceil(w/8) * ceil(h/8) 8x8 tiles of path slots, indexed in 32-bit
+    // arithmetic by the kernels (path_pixel, k_resolve): reject films whose count reaches 2^31
+    if ((int64_t)((d->width + 7) / 8) * ((d->height + 7) / 8) * 64 >= ((int64_t)1 << 31)) {
+        err = "film too large: padded paths per sample must stay below 2^31";
+        return false;
+    }
+    // PathIntegrator(bvh, maxDepth, light) with maxDepth < 0 still traces the camera ray and
+    // returns black (Integrators.fs:108-109); the reference only ever passes 3 (Scene.fs:304)
+    if (d->max_depth < 0) {
+        err = "max_depth must be >= 0";
+        return false;
+    }
     const int n = (int)d->nprims;
     s.width = d->width;
     s.height = d->height;

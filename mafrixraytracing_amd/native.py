@@ -19,18 +19,24 @@ class NativeContext:
     """One mfx_ctx: a scene resident in HBM on one GPU."""
 
     def __init__(self, arrays: SceneArrays, seed: int = DEFAULT_SEED, device: int = 0, flags: int = MFX_F_NONE,
-                 part_index: int = 0, part_count: int = 1):
+                 part_index: int = 0, part_count: int = 1, devices: list[int] | None = None):
+        """devices: drive this list of HIP devices from one context (mfx_options.devices; the
+        library's own RCCL reduce sums them into devices[0]); None: the single `device`."""
         self.lib = load_library()
         self.arrays = arrays
         self.w, self.h = arrays.width, arrays.height
         self._desc = arrays.desc()
-        opt = MfxOptions(seed=seed, device=device, flags=flags, part_index=part_index, part_count=part_count)
+        self.devices = list(devices) if devices else [device]
+        self._devs = (C.c_int32 * len(self.devices))(*self.devices)
+        opt = MfxOptions(seed=seed, device=device, flags=flags, part_index=part_index, part_count=part_count,
+                         ndevices=len(devices) if devices else 0,
+                         devices=C.cast(self._devs, C.POINTER(C.c_int32)) if devices else None)
         h = C.c_void_p()
         check(self.lib.mfx_create(C.byref(self._desc), C.byref(opt), C.byref(h)), "mfx_create")
         self._h = h
 
     def close(self):
-        if getattr(self, "h", None):
+        if getattr(self, "_h", None):
             self.lib.mfx_destroy(self._h)
             self._h = None
 
@@ -72,6 +78,10 @@ class NativeContext:
     def trace_accumulate(self, spp: int, sample_base: int):
         check(self.lib.mfx_trace_accumulate(self._h, spp, sample_base), "mfx_trace_accumulate")
 
+    def accum_reduce(self):
+        """Multi-device context: sum the devices' accumulators into devices[0] (mfx_accum_reduce)."""
+        check(self.lib.mfx_accum_reduce(self._h), "mfx_accum_reduce")
+
     def accum_clear(self):
         check(self.lib.mfx_accum_clear(self._h), "mfx_accum_clear")
 
@@ -86,7 +96,7 @@ class NativeContext:
 
     def accum_read_mean(self, count: float) -> np.ndarray:
         frame = np.empty((self.w * self.h, 4), dtype=np.float64)
-        check(self.lib.mfx_accum_read_mean(self._h, 1.0 / count, dptr(frame)), "mfx_accum_read_mean")
+        check(self.lib.mfx_accum_read_mean(self._h, float(count), dptr(frame)), "mfx_accum_read_mean")
         return frame
 
     def sync(self):

@@ -18,7 +18,7 @@ OBJ inputs produce the same primitive list, in the same order, with the same mat
 Documented extensions: `vt`/`vn`/`o`/`s` lines are accepted and ignored
 (an `o` name may contain dots, which FindModel's `model.group` split rejects), trailing whitespace/CR is trimmed from group names (the
 FParsec grammar as shipped rejects the bundled meshes — SURVEY.md §0.4); a `.npz` mesh
-(converted OBJ, scripts/convert_assets.py) may stand in for an `.obj`; and
+(converted OBJ, scripts/make_scenes.py) may stand in for an `.obj`; and
 <Shape type="sphere"> adds a Sphere (the reference's scene graph has spheres, Scene.fs:159,
 but no loader produces one).
 """
@@ -179,7 +179,7 @@ def load_obj(path: str, manager: MaterialManager) -> ObjState:
 
 
 def save_npz_mesh(path: str, st: ObjState, mtl: list[tuple[str, tuple]]):
-    """Binary form of an ObjState + its MTL (scripts/convert_assets.py)."""
+    """Binary form of an ObjState + its MTL (scripts/make_scenes.py)."""
     names = list(st.groups.keys())
     faces, fgroup, fmat = [], [], []
     verts, vidx = [], {}
@@ -276,8 +276,25 @@ def _find_model(ref: str, models: dict):
     return groups[nm[1]]
 
 
-def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager | None = None) -> SceneState:
-    """InitSceneState (Scene.fs:265-271): parse XML *text*, version must be 0.1."""
+# The light Scene.fs:194 builds when the light group's first primitive is not a Rect: there the
+# reference asserts false, which a Release build compiles out, and returns this quad.
+RELEASE_FALLBACK_LIGHT = {
+    "p": ((-0.24, 1.98, 0.16), (-0.24, 1.98, -0.22), (0.23, 1.98, -0.22), (0.23, 1.98, 0.16)),
+    "normal": (0.0, -1.0, 0.0),
+    "intensity": (20.0, 20.0, 20.0),
+}
+
+
+def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager | None = None,
+                   light_fallback: str = "debug") -> SceneState:
+    """InitSceneState (Scene.fs:265-271): parse XML *text*, version must be 0.1.
+
+    light_fallback: what a light group whose first primitive is not a Rect does. "debug" (the
+    default) raises SceneError, as the reference's Debug build does at `assert(false)`
+    (Scene.fs:194); "release" returns the hard-coded NewAreaLight of the same line (I = 20,
+    normal (0,-1,0)), as its Release build does, where the assert compiles out."""
+    if light_fallback not in ("debug", "release"):
+        raise ValueError("light_fallback must be 'debug' or 'release'")
     mgr = manager or MaterialManager.GetManager()
     root = ET.fromstring(xml_text)
     if root.get("version") != "0.1":
@@ -331,10 +348,15 @@ def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager 
         else:
             raise SceneError(f"unknown light argument {a.get('name')!r}")
     grp = _find_model(ref, models)
-    if not grp or grp[0].kind != MFX_PRIM_RECT:
-        raise SceneError("the light's first primitive must be a quad (Rect)")
-    q = grp[0].pts
-    light = {"p": (q[0], q[1], q[2], q[3]), "normal": tri_normal(q[0], q[1], q[2]), "intensity": inten}
+    if not grp:  # FindModel(...).ToArray()[0] on an empty group throws in either build
+        raise SceneError("the light's group has no primitive")
+    if grp[0].kind != MFX_PRIM_RECT:
+        if light_fallback == "debug":
+            raise SceneError("the light's first primitive must be a quad (Rect)")
+        light = dict(RELEASE_FALLBACK_LIGHT)
+    else:
+        q = grp[0].pts
+        light = {"p": (q[0], q[1], q[2], q[3]), "normal": tri_normal(q[0], q[1], q[2]), "intensity": inten}
     # Film (Scene.fs:201-211)
     w, h = 800, 800
     fn = nodes.get("Film")
@@ -397,11 +419,12 @@ def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager 
     return SceneState(cam, light, w, h, prims, mgr)
 
 
-def load_scene_file(path: str, fresh_manager: bool = True, **kw) -> SceneArrays:
+def load_scene_file(path: str, fresh_manager: bool = True, light_fallback: str = "debug", **kw) -> SceneArrays:
     """Convenience: XML file -> SceneArrays, with a fresh MaterialManager (the reference's
     manager is process-global; a fresh one gives the index space of a first load)."""
     with open(path, "r", encoding="utf-8") as f:
         text = f.read()
     mgr = MaterialManager() if fresh_manager else None
-    st = InitSceneState(text, base_dir=os.path.dirname(os.path.abspath(path)), manager=mgr)
+    st = InitSceneState(text, base_dir=os.path.dirname(os.path.abspath(path)), manager=mgr,
+                        light_fallback=light_fallback)
     return st.arrays(**kw)

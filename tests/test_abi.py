@@ -28,21 +28,41 @@ def test_library_exports_every_declared_symbol():
     assert exported == names  # nothing undeclared leaks out
 
 
-def test_struct_layouts_match_header():
+def header_layouts(tmp_path):
+    """sizeof and every field offset of the header's structs, as gcc lays them out."""
+    from mafrixraytracing_amd import abi
+    structs = {"mfx_prim": abi.MfxPrim, "mfx_quad_light": abi.MfxQuadLight, "mfx_pinhole": abi.MfxPinhole,
+               "mfx_scene_desc": abi.MfxSceneDesc, "mfx_options": abi.MfxOptions}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
+    for cname, py in structs.items():
+        lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
+        for f in py._fields_:
+            lines.append(f'printf("{cname} {f[0]} %zu\\n", offsetof({cname}, {f[0]}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(src)], check=True)
+    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout
+    return structs, {tuple(l.split()[:2]): int(l.split()[2]) for l in out.splitlines()}
+
+
+def test_struct_layouts_match_header(tmp_path):
+    """The ctypes mirror (and so the F# shim, whose fields follow it) has the C header's layout."""
     import ctypes as C
-    from mafrixraytracing_amd.abi import MfxOptions, MfxPinhole, MfxPrim, MfxQuadLight, MfxSceneDesc
-    assert C.sizeof(MfxPrim) == 104
-    assert C.sizeof(MfxQuadLight) == 18 * 8
-    assert C.sizeof(MfxPinhole) == 17 * 8 + 8
-    assert C.sizeof(MfxOptions) == 24
-    assert C.sizeof(MfxSceneDesc) == 8 + 8 + 8 + 4 * 4 + C.sizeof(MfxQuadLight) + C.sizeof(MfxPinhole)
+    structs, lay = header_layouts(tmp_path)
+    for cname, py in structs.items():
+        assert lay[(cname, "size")] == C.sizeof(py), cname
+        for f in py._fields_:
+            assert lay[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
+    assert lay[("mfx_prim", "size")] == 104 and lay[("mfx_options", "size")] == 40
 
 
 def test_version_errors_and_no_cpu_fallback():
     import ctypes as C
     from mafrixraytracing_amd.abi import MfxOptions, load_library
     lib = load_library()
-    assert lib.mfx_abi_version() == 1
+    assert lib.mfx_abi_version() == 2
     assert lib.mfx_device_count() >= 0
     h = C.c_void_p()
     opt = MfxOptions(seed=1, device=0, flags=0, part_index=0, part_count=1)
@@ -59,6 +79,14 @@ def test_version_errors_and_no_cpu_fallback():
         # without a GPU, creating a context fails loudly (MFX_E_DEVICE) instead of falling back
         opt.part_count = 1
         assert lib.mfx_create(C.byref(d), C.byref(opt), C.byref(h)) == -2
+    # a device list needs its array, and at most MFX_MAX_DEVICES entries
+    opt.part_count = 1
+    opt.ndevices = 2
+    opt.devices = None
+    assert lib.mfx_create(C.byref(d), C.byref(opt), C.byref(h)) == -1
+    opt.ndevices = 65
+    assert lib.mfx_create(C.byref(d), C.byref(opt), C.byref(h)) == -1
+    assert lib.mfx_accum_reduce(None) == -4
 
 
 def test_empty_scene_rejected():

@@ -1,0 +1,105 @@
+"""Multi-device contexts through the C ABI (mfx_options.devices).
+
+One context drives a device list from one process: device g renders sample sub-partition g of G
+on its own stream, and the library's own reduce sums the FP64 accumulators into devices[0]:
+- a list of distinct devices reduces with RCCL (a communicator the library creates with
+  ncclCommInitAll); devices=[0] runs that code path on the 1-GPU box (a 1-rank reduce);
+- a list that repeats a device (devices=[0,0]) adds the peers' accumulators in device order.
+The 8-GPU case is the driver's; every bit of bookkeeping it uses is exercised here with G = 1-3.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+from conftest import SEED, scene
+
+pytestmark = pytest.mark.gpu
+
+
+def test_single_device_list_is_bit_identical(gpu):
+    """devices=[0] (RCCL communicator of one rank + its reduce) == the plain single-device context."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 64, 36)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, devices=[0]) as c2:
+        for _ in range(2):
+            assert np.array_equal(c1.sample(3), c2.sample(3))
+            assert np.array_equal(c1.render_rgba8(2), c2.render_rgba8(2))
+        assert np.array_equal(c1.film_mean(), c2.film_mean())
+        assert np.array_equal(c1.ray_counts(), c2.ray_counts())
+
+
+@pytest.mark.parametrize("G", [2, 3])
+def test_repeated_device_list_sums_partitions_in_device_order(gpu, oracle, G):
+    """devices=[0]*G: device g renders partition g of G; the primary's accumulator is
+    (a_0 + a_1) + a_2 ..., bit for bit the partitioned single-device contexts summed in that order;
+    ray counts equal the whole sample set's; the image matches the oracle."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("cube_cornell", 48, 27)
+    spp = 7
+    parts = []
+    for g in range(G):
+        with NativeContext(a, seed=SEED, part_index=g, part_count=G) as ctx:
+            ctx.accum_clear()
+            ctx.trace_accumulate(spp, 0)
+            parts.append(ctx.accum_read_mean(1.0))
+    want = parts[0].copy()
+    for p in parts[1:]:
+        want[:, :3] = want[:, :3] + p[:, :3]
+    with NativeContext(a, seed=SEED, devices=[0] * G) as m:
+        m.accum_clear()
+        m.trace_accumulate(spp, 0)
+        m.accum_reduce()
+        got = m.accum_read_mean(1.0)
+        counts = m.ray_counts()
+        img = m.sample(spp)  # the same frame through mfx_sample (trace_accumulate does not advance it)
+    assert np.array_equal(got, want)
+    with NativeContext(a, seed=SEED) as s:
+        s.sample(spp)
+        assert np.array_equal(counts[:4], s.ray_counts()[:4])
+    ref = oracle.OracleScene(a).sample(spp, SEED, sample_base=0)
+    diff = np.abs(img[:, :3] - ref[:, :3])
+    assert np.sqrt((diff ** 2).mean(axis=0)).max() <= 1e-4 and diff.max() <= 1e-12
+
+
+def test_repeated_device_render_and_stats(gpu, oracle):
+    """Scene.Render on a 2-device context: the film on devices[0] holds the reduced frames;
+    mfx_stats sums rays over the devices."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("two_spheres_plane", 40, 30)
+    with NativeContext(a, seed=SEED, devices=[0, 0]) as m, NativeContext(a, seed=SEED) as s:
+        for _ in range(3):
+            m.render_rgba8(2)
+            s.render_rgba8(2)
+        assert np.abs(m.film_mean() - s.film_mean()).max() <= 1e-12
+        rays, sec = m.stats()
+        n = s.ray_counts()
+        assert rays == n[0] + n[1] + n[2] and sec > 0
+
+
+def test_sample_mean_divides_by_the_count(gpu):
+    """mfx_sample(49) divides by 49 itself (Integrators.fs:171): 1/(1/49) != 49 in FP64, so a
+    reciprocal round trip would be 1 ulp off here."""
+    from mafrixraytracing_amd.native import NativeContext
+    assert 1.0 / (1.0 / 49.0) != 49.0
+    a = scene("cornell", 16, 16)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED) as c2:
+        img = c1.sample(49)
+        c2.accum_clear()
+        c2.trace_accumulate(49, 0)
+        acc = c2.accum_read_mean(1.0)
+        assert np.array_equal(c2.accum_read_mean(49.0), img)
+    assert np.array_equal(img[:, :3], acc[:, :3] / 49.0)
+
+
+def test_bad_device_lists_fail_loudly(gpu):
+    from mafrixraytracing_amd.abi import MfxError
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("cornell", 8, 8)
+    n = gpu.mfx_device_count()
+    with pytest.raises(MfxError):
+        NativeContext(a, seed=SEED, devices=[0, n])  # no such device
+    with pytest.raises(MfxError):  # partitioned contexts compose through trace_accumulate, not Sample
+        with NativeContext(a, seed=SEED, devices=[0, 0], part_index=0, part_count=2) as m:
+            m.sample(1)
+    _ = C

@@ -105,3 +105,18 @@ def test_sphere_extension():
     sph = a.prims[a.prims["kind"] == 2]
     assert len(sph) == 2 and sph["p"][:, 1, 0].tolist() == [0.5, 0.5]
     assert np.allclose(sph["p"][:, 0, :], [[-0.6, 0.5, -1.0], [0.6, 0.5, -1.0]])
+
+
+def test_release_light_fallback(tmp_path):
+    """Scene.fs:194: a non-Rect light group asserts in Debug builds (the default here) and
+    returns the hard-coded I=20 quad with normal (0,-1,0) in Release builds."""
+    _write(tmp_path, "m.obj", OBJ)
+    text = XML.format(group="quad", light="tri")
+    with pytest.raises(SceneError):
+        InitSceneState(text, base_dir=str(tmp_path), manager=MaterialManager())
+    st = InitSceneState(text, base_dir=str(tmp_path), manager=MaterialManager(), light_fallback="release")
+    assert st.light["intensity"] == (20.0, 20.0, 20.0)
+    assert st.light["normal"] == (0.0, -1.0, 0.0)
+    assert st.light["p"][0] == (-0.24, 1.98, 0.16) and st.light["p"][3] == (0.23, 1.98, 0.16)
+    with pytest.raises(ValueError):
+        InitSceneState(text, base_dir=str(tmp_path), manager=MaterialManager(), light_fallback="fast")
