@@ -4,9 +4,16 @@
 Workload (BASELINE.json configs[1]; --config C3/C4/C5 for the others):
 scenes/spot.xml — spot (5,856 triangles)
 on a floor quad under a quad light, 1920x1080, 64 samples per pixel per GPU, maxDepth 3.
-A step = one 64-spp-per-GPU frame: every rank traces its disjoint sample partition into an FP64
-accumulator, then (N > 1) one RCCL sum-reduce of that [3][w*h] buffer to rank 0. Per-GPU work is
-fixed as N grows ("scaling": "weak"): the N-GPU job renders 64*N spp of the same frame.
+A step = one frame: every GPU traces its disjoint sample partition into an FP64 accumulator,
+then (N > 1) one RCCL sum-reduce of that [3][w*h] buffer to GPU 0.
+  --scaling weak (default): 64 spp per GPU, the N-GPU job renders 64*N spp of the same frame;
+  --scaling strong: the job renders the config's 64 spp, split over the N GPUs.
+N > 1 runs one process per GPU under torch.distributed.run (the driver's launch;
+mafrixraytracing_amd/distributed.py, RCCL through torch.distributed), or with --single-process
+one process whose library context drives all N devices and reduces with its own RCCL
+communicator (mfx_options.devices, the path the F# host binds).
+--api render times the reference's real call pattern instead: Scene.Render = 1 spp per call,
+mfx_render_rgba8(ctx, 1, buf) with the 8 MB RGBA8 readback, the config's spp calls per step.
 
 Rays counted = primary + extension (closest-hit queries actually traced) + shadow rays, read
 from the kernel's own counters. Inputs (scene, BVH) are resident in HBM before timing starts.
@@ -18,8 +25,12 @@ Extra objects on the JSON line:
                 bytes per launch / its HIP-event duration vs HBM 8 TB/s; bytes per ray frozen in
                 profiles/bray_fixture.json; traffic = PMC HBM bytes per launch
                 (profiles/traffic_<scene>.json, scripts/profile_r01.sh)
-  cpu_baseline  the CPU oracle (FP64 restatement of the reference algorithm) timed on this host
-                on a bounded random sample of the same workload's paths (rank 0, N = 1 only)
+  render_api    (N = 1) the same workload through Scene.Render's call pattern: the config's spp
+                calls of mfx_render_rgba8(ctx, 1, buf), each with film, post and readback
+  cpu_baseline  the CPU oracle timed on this host on a bounded random sample of the same
+                workload's paths (rank 0, N = 1 only): "strict" (the FP64 restatement of the
+                reference algorithm; `value`) and "fast" (SAH BVH2, tMax culling, any-hit
+                shadows), with the thread count, nproc and CPU model
 """
 from __future__ import annotations
 
@@ -59,6 +70,13 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the traversal-counter pass")
     ap.add_argument("--megakernel", action="store_true", help="persistent megakernel instead of the wavefront")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: config spp per GPU; strong: config spp per job, split over the GPUs")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N > 1 from one process: one library context over N devices (its own RCCL reduce)")
+    ap.add_argument("--api", default="batch", choices=["batch", "render"],
+                    help="batch: mfx_trace_accumulate of the frame's spp; render: spp x mfx_render_rgba8(1)")
+    ap.add_argument("--no-render-api", action="store_true", help="skip the render_api sub-measurement")
     return ap.parse_args()
 
 
@@ -75,48 +93,123 @@ def relaunch_distributed(args):
     return subprocess.call(cmd)
 
 
+def host_cpu():
+    """(nproc, CPUs this process may run on, CPU model name)."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    return os.cpu_count() or 1, allowed, model
+
+
 def cpu_baseline(arrays, spp, seed, budget_s):
-    """Oracle (port) on random (pixel, sample) paths of the same workload, time-boxed."""
+    """Oracle (port) on random (pixel, sample) paths of the same workload, time-boxed: "strict"
+    (the reference algorithm) for `value`, then "fast" for half the budget.
+
+    Threads: the job's CPU share. On the GPU box OMP_NUM_THREADS (16, the share of one GPU's
+    job) is set and honoured — the box's rules forbid sizing a pool to the whole machine, whose
+    nproc it reports. Without it, every CPU this process may run on. The per-thread rate and
+    its linear extrapolation to nproc are reported beside it as an estimate."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
     pyoracle.build()
-    nthreads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    nproc, allowed, model = host_cpu()
+    nthreads = int(os.environ.get("OMP_NUM_THREADS") or allowed)
     o = pyoracle.OracleScene(arrays)
-    rng = np.random.default_rng(7)
-    rays = paths = 0.0
-    t_total = 0.0
-    batch = 20000
-    while t_total < budget_s:
-        px = rng.integers(0, arrays.width, batch)
-        py = rng.integers(0, arrays.height, batch)
-        sm = rng.integers(0, spp, batch)
-        _, st = o.paths(px, py, sm, seed, nthreads=nthreads)
-        rays += st[0] + st[1] + st[2]
-        paths += st[3]
-        t_total += st[7]
+    res = {}
+    for mode, budget in (("strict", budget_s), ("fast", budget_s / 2)):
+        rng = np.random.default_rng(7)
+        rays = paths = 0.0
+        t_total = 0.0
+        batch = 20000
+        while t_total < budget:
+            px = rng.integers(0, arrays.width, batch)
+            py = rng.integers(0, arrays.height, batch)
+            sm = rng.integers(0, spp, batch)
+            _, st = o.paths(px, py, sm, seed, nthreads=nthreads, mode=mode)
+            rays += st[0] + st[1] + st[2]
+            paths += st[3]
+            t_total += st[7]
+        res[mode] = (rays / t_total / 1e6, paths, rays, t_total)
     o.close()
-    return {"value": round(rays / t_total / 1e6, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+    v, paths, rays, t = res["strict"]
+    return {"value": round(v, 4), "unit": "Mrays/s", "cores": nthreads, "kind": "port",
+            "strict": round(v, 4), "fast": round(res["fast"][0], 4),
+            "nproc": nproc, "cpus_allowed": allowed, "model": model,
+            "per_thread_strict": round(v / nthreads, 4),
+            "nproc_estimate_strict": round(v / nthreads * nproc, 2),
             "sample": f"{int(paths)} random (pixel, sample) paths of the same {arrays.width}x{arrays.height}x{spp} workload "
-                      f"({int(rays)} rays, {t_total:.1f} s), oracle/mfx_oracle.c strict FP64 restatement, "
-                      f"OpenMP {nthreads} threads"}
+                      f"({int(rays)} rays, {t:.1f} s), oracle/mfx_oracle.c strict FP64 restatement of the reference "
+                      f"algorithm, OpenMP {nthreads} threads; fast = the same paths' integrator over a SAH BVH2 "
+                      f"with tMax culling and any-hit shadows ({res['fast'][3]:.1f} s); nproc_estimate = "
+                      f"per-thread rate x nproc (linear, not measured)"}
+
+
+def render_api(arrays, seed, calls, devices=None):
+    """Scene.Render's call pattern (Scene.fs:331-333): `calls` x mfx_render_rgba8(ctx, 1, buf), each
+    one 1-spp frame into the film, ACES/sqrt/RGBA8 post and the RGBA8 readback to host memory.
+    Rays from the kernels' counters of every call; wall time per call by the host clock."""
+    import numpy as np
+    from mafrixraytracing_amd.native import NativeContext
+    ctx = NativeContext(arrays, seed=seed, devices=devices)
+    buf = np.empty(arrays.width * arrays.height * 4, dtype=np.uint8)
+    import ctypes as C
+    bp = buf.ctypes.data_as(C.POINTER(C.c_uint8))
+    from mafrixraytracing_amd.abi import check
+    for _ in range(3):
+        check(ctx.lib.mfx_render_rgba8(ctx._h, 1, bp), "mfx_render_rgba8")
+    wall, dev, rays = [], [], 0.0
+    for _ in range(calls):
+        t0 = time.perf_counter()
+        check(ctx.lib.mfx_render_rgba8(ctx._h, 1, bp), "mfx_render_rgba8")
+        wall.append(time.perf_counter() - t0)
+        r, sec = ctx.stats()
+        rays += r
+        dev.append(sec)
+    ctx.close()
+    total = sum(wall)
+    return {"value": round(rays / total / 1e6, 2), "unit": "Mrays/s", "calls": calls,
+            "ms_per_call": round(total / calls * 1e3, 4), "ms_per_call_min": round(min(wall) * 1e3, 4),
+            "trace_device_ms_per_call": round(sum(dev) / calls * 1e3, 4),
+            "rays_per_call": round(rays / calls, 1),
+            "includes": "per call: mfx_render_rgba8(ctx, 1, buf) = trace of 1 spp (all bounces), film add, "
+                        "ACES/sqrt/RGBA8 post, 8 MB RGBA8 copy to pageable host memory, synchronize"}
 
 
 def main():
     args = parse()
+    # the JSON line is the only thing on stdout: libraries that print banners there (RCCL prints
+    # its version at communicator creation) are sent to stderr instead
+    sys.stdout.flush()
+    json_out = os.fdopen(os.dup(1), "w")
+    os.dup2(2, 1)
     cfg_scene, cfg_spp, cfg_label = CONFIGS[args.config]
     if args.scene is None:
         args.scene = os.path.join(ROOT, "scenes", cfg_scene)
     if args.spp is None:
         args.spp = cfg_spp
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    if args.gpus > 1 and "RANK" not in os.environ:
+    if args.gpus > 1 and not args.single_process and "RANK" not in os.environ:
         sys.exit(relaunch_distributed(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    ngpu = args.gpus if args.single_process else world  # GPUs of the job
+    if args.api == "render" and world > 1:
+        sys.exit("--api render is one process (use --single-process for N > 1)")
 
     import numpy as np
     from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE
+    from mafrixraytracing_amd.distributed import native_partitioned_render, step_spp
     from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
@@ -130,13 +223,16 @@ def main():
     arrays = load_scene_file(args.scene)
     W, H = arrays.width, arrays.height
     npix = W * H
-    spp_step = args.spp * world
+    spp_step = step_spp(args.spp, ngpu, args.scaling)  # the whole job's spp per step
     mode = MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE
-    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world)
-    acc = None
+    devices = list(range(args.gpus)) if args.single_process else None
+    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world,
+                        devices=devices)
+    pr = None
     if world > 1:
         acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
-        ctx.accum_attach(acc.data_ptr(), acc.numel() * 8)
+        pr = native_partitioned_render(ctx, acc, rank, world)
+    rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
         if world > 1:
@@ -145,12 +241,18 @@ def main():
         ctx.sync()
 
     def step(k):
-        ctx.accum_clear()
-        ctx.trace_accumulate(spp_step, k * spp_step)
-        ctx.sync()
-        if world > 1:
-            dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM)
-            torch.cuda.synchronize()
+        base = k * spp_step
+        if args.api == "render":  # Scene.Render x spp: 1 spp per call, film + post + readback
+            for _ in range(spp_step):
+                ctx.render_rgba8(1, out=rbuf)
+        elif pr is not None:  # one process per GPU: trace own partition, RCCL reduce via torch
+            pr.frame(spp_step, base)
+        else:  # one GPU, or one context over the device list (the library's RCCL reduce)
+            ctx.accum_clear()
+            ctx.trace_accumulate(spp_step, base)
+            if devices:
+                ctx.accum_reduce()
+            ctx.sync()
 
     for k in range(args.warmup):
         step(k)
@@ -159,7 +261,18 @@ def main():
     rays = 0.0
     closest_rays = 0.0
     timings = []
+    call_s = 0.0  # --api render: host time inside the render calls (counters are read between calls)
     for k in range(args.steps):
+        if args.api == "render":
+            for _ in range(spp_step):
+                tc = time.perf_counter()
+                ctx.render_rgba8(1, out=rbuf)
+                call_s += time.perf_counter() - tc
+                c = ctx.ray_counts()
+                rays += c[0] + c[1] + c[2]
+                closest_rays += c[0] + c[1]
+                timings.append(ctx.trace_timing())
+            continue
         step(args.warmup + k)
         c = ctx.ray_counts()
         rays += c[0] + c[1] + c[2]
@@ -167,6 +280,8 @@ def main():
         timings.append(ctx.trace_timing())
     barrier()
     elapsed = time.perf_counter() - t0
+    if args.api == "render":
+        elapsed = call_s
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -181,6 +296,8 @@ def main():
                           "generations")}
 
     result = None
+    # launches per timed unit: a step, or (--api render) one 1-spp call
+    nt = args.steps * (spp_step if args.api == "render" else 1)
     if rank == 0:
         # traversal counters (separate, untimed pass at 1 spp of the same frame)
         stats = None
@@ -218,7 +335,7 @@ def main():
             if sname == "spot":
                 tfile = os.path.join(ROOT, "profiles", "traffic_spot_1080p.json")
             tdata = None
-            if os.path.exists(tfile) and world == 1:
+            if os.path.exists(tfile) and ngpu == 1 and args.api == "batch":
                 with open(tfile) as f:
                     tdata = json.load(f)
                 if tdata.get("spp", args.spp) != args.spp:
@@ -247,44 +364,57 @@ def main():
                     fc, fs = fixture["closest"], fixture["shadow"]
                     n_c, n_s = fixture["closest_rays"], fixture["shadow_rays"]
                     bray = (fc["B_ray"] * n_c + fs["B_ray"] * n_s) / (n_c + n_s)
-                roofline = kernel_roofline("trace_kernel<false>", stage_ms["total_ms"], rays / args.steps, 1, bray)
+                roofline = kernel_roofline("trace_kernel<false>", stage_ms["total_ms"], rays / nt, 1, bray)
             else:
                 # the two wavefront kernels; the roofline object is the one with the larger share of
                 # the step (the dominant kernel), the other is reported beside it
                 launches = stage_ms["launches"]
                 bc = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
                 bs = fixture["shadow"]["B_ray"] if fixture else bytes_per_ray(stats["shadow"])
-                ext = kernel_roofline("k_extend<false>", stage_ms["extend_ms"], closest_rays / args.steps, launches, bc)
-                shd = kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"], (rays - closest_rays) / args.steps,
+                ext = kernel_roofline("k_extend<false>", stage_ms["extend_ms"], closest_rays / nt, launches, bc)
+                shd = kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"], (rays - closest_rays) / nt,
                                       launches, bs)
                 dom, other = (shd, ext) if stage_ms["shadow_ms"] > stage_ms["extend_ms"] else (ext, shd)
                 roofline = dict(dom)
                 roofline["other_kernel"] = other
-                step_bytes = (closest_rays * bc + (rays - closest_rays) * bs) / args.steps
+                step_bytes = (closest_rays * bc + (rays - closest_rays) * bs) / nt
                 roofline["step"] = {"achieved": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9, 2),
                                     "frac": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
                                     "note": "both kernels' algorithmic bytes over the whole traced step"}
             roofline["stage_ms"] = {k: round(v, 3) for k, v in stage_ms.items()}
             roofline["counters"] = {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
                                         else round(d, 4)) for g, d in stats.items()}
-        cpu = None
-        if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
         value = rays_all / elapsed / 1e6
+        rapi = None
+        if ngpu == 1 and args.api == "batch" and not args.no_render_api and not args.megakernel:
+            rapi = render_api(arrays, DEFAULT_SEED, args.spp)
+            rapi["vs_batch"] = round(rapi["value"] / value, 4)
+        cpu = None
+        if ngpu == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
+        if ngpu == 1:
+            par = "one GPU"
+        elif args.single_process:
+            par = f"sample-partition x{ngpu}, one process, library RCCL reduce (mfx_options.devices)"
+        else:
+            par = f"sample-partition x{ngpu}, one process per GPU, RCCL reduce via torch.distributed"
+        per_gpu = spp_step / ngpu
+        api = ("Scene.Render pattern: mfx_render_rgba8(ctx, 1, buf) x spp, readback included"
+               if args.api == "render" else "mfx_trace_accumulate of the step's spp (inputs resident in HBM)")
         result = {
-            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": world,
+            "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": ngpu,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64",
+            "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
-            "config": {"workload": f"{cfg_label}, {W}x{H}, {args.spp} spp per GPU per step",
+            "config": {"workload": f"{cfg_label}, {W}x{H}, {spp_step} spp per step over {ngpu} GPU(s)",
                        "baseline_config": args.config,
                        "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
-                       "spp_per_gpu": args.spp, "global_spp_per_step": spp_step, "max_depth": 3,
-                       "pipeline": "megakernel" if args.megakernel else "wavefront",
-                       "parallelism": f"sample-partition x{world}" + (" + RCCL reduce" if world > 1 else "")},
-            "roofline": roofline, "cpu_baseline": cpu,
+                       "spp_per_gpu": per_gpu, "global_spp_per_step": spp_step, "max_depth": 3,
+                       "pipeline": "megakernel" if args.megakernel else "wavefront", "api": api,
+                       "parallelism": par},
+            "roofline": roofline, "render_api": rapi, "cpu_baseline": cpu,
         }
-        print(json.dumps(result), flush=True)
+        print(json.dumps(result), file=json_out, flush=True)
     ctx.close()
     if world > 1:
         dist.barrier()

@@ -459,7 +459,15 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.ntop_shd = c->wf_ntop_shd;
     P.shadow_waves = c->wf_shadow_waves;
     P.spill = c->d_spill;
-    P.chunk = c->wf_chunk;
+    // Slots per chunk fetch: the default 1024 when every wave of the larger grid gets >= 8
+    // chunks; smaller for a small generation (a 1-spp Scene.Render call at 1080p is 2 M paths:
+    // 1024-slot chunks left half the waves without work and the rest with 16 rays per lane)
+    {
+        const int64_t waves = (int64_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 4;
+        int64_t ch = c->wf_chunk;
+        while (ch > 64 && (int64_t)pool / ch < 8 * waves) ch /= 2;
+        P.chunk = (int)(ch / 64 * 64);
+    }
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;

@@ -1,4 +1,5 @@
-"""Multi-GPU composition: one process per GPU, disjoint sample partitions, one RCCL reduce.
+"""Multi-GPU composition across processes: one process per GPU, disjoint sample partitions, one
+RCCL reduce. This is the path `bench.py --gpus N` runs under torch.distributed.run.
 
 Every (pixel, sample) path is independent (Integrators.fs:164-171), so rank r of W renders the
 global samples s with s % W == r (mfx_options.part_index/part_count) into an FP64 accumulator it
@@ -6,9 +7,13 @@ owns; the only exchange is one sum-reduce of the [3][w*h] accumulator to rank 0 
 (torch.distributed backend "nccl" == RCCL on ROCm). The counter RNG is keyed on the global
 sample index, so the W-rank image equals the 1-rank image up to FP64 summation order.
 
-`render_fn` is the per-rank tracer; in production it drives the HIP context
-(`native.NativeContext.trace_accumulate` writing straight into the reduce buffer), and the
-gloo tests substitute a CPU function of the same signature to check the composition.
+(A single process can drive the same partitions itself: a context over a device list,
+mfx_options.devices, reduces with the library's own RCCL communicator — `bench.py
+--single-process`.)
+
+`PartitionedRender` is the per-rank frame: clear, trace this rank's partition, wait for the
+trace, reduce. `native_partitioned_render` wires it to a HIP context (`NativeContext`) whose
+accumulator is the reduce buffer; the gloo tests drive the same class with a CPU tracer.
 """
 from __future__ import annotations
 
@@ -20,6 +25,19 @@ import numpy as np
 def partition_samples(spp: int, rank: int, world: int) -> np.ndarray:
     """Sample indices (within one call of spp samples) that `rank` renders."""
     return np.arange(rank, spp, world, dtype=np.int64)
+
+
+def step_spp(config_spp: int, world: int, scaling: str) -> int:
+    """Samples per pixel of one whole-job step: weak scaling keeps config_spp per GPU (the job
+    renders config_spp * world), strong scaling keeps the job at config_spp (each GPU renders
+    about config_spp / world)."""
+    if scaling == "weak":
+        return config_spp * world
+    if scaling == "strong":
+        if config_spp < world:
+            raise ValueError(f"strong scaling needs spp >= GPUs ({config_spp} < {world})")
+        return config_spp
+    raise ValueError(f"scaling must be 'weak' or 'strong', not {scaling!r}")
 
 
 def reduce_accumulator(acc, dst: int = 0, all_ranks: bool = False):
@@ -35,15 +53,45 @@ def reduce_accumulator(acc, dst: int = 0, all_ranks: bool = False):
 
 
 class PartitionedRender:
-    """One rank's share of a frame: trace own partition into `acc`, then reduce to rank 0."""
+    """One rank's share of a frame: clear, trace own partition into `acc`, wait, reduce to rank 0.
 
-    def __init__(self, render_fn: Callable, acc, rank: int, world: int):
+    render_fn(acc, spp, sample_base, rank, world) traces; clear_fn() zeroes the accumulator
+    (default acc.zero_()); sync_fn() waits for the trace before the reduce reads the buffer (a
+    HIP context traces on its own stream, the reduce runs on torch's)."""
+
+    def __init__(self, render_fn: Callable, acc, rank: int, world: int,
+                 clear_fn: Callable | None = None, sync_fn: Callable | None = None, after_reduce: Callable | None = None):
         self.render_fn = render_fn
         self.acc = acc
         self.rank = rank
         self.world = world
+        self.clear_fn = clear_fn or acc.zero_
+        self.sync_fn = sync_fn
+        self.after_reduce = after_reduce
 
     def frame(self, spp: int, sample_base: int, all_ranks: bool = False):
-        self.acc.zero_()
+        self.clear_fn()
         self.render_fn(self.acc, spp, sample_base, self.rank, self.world)
-        return reduce_accumulator(self.acc, 0, all_ranks)
+        if self.sync_fn is not None:
+            self.sync_fn()
+        out = reduce_accumulator(self.acc, 0, all_ranks)
+        if self.after_reduce is not None:
+            self.after_reduce()
+        return out
+
+
+def native_partitioned_render(ctx, acc, rank: int, world: int) -> PartitionedRender:
+    """PartitionedRender over a HIP context: `acc` (a device tensor on the context's GPU, at least
+    3*w*h doubles) becomes the context's accumulator (mfx_accum_attach), so the trace writes
+    straight into the buffer RCCL reduces. The context must render partition `rank` of `world`."""
+    ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
+
+    def sync_torch():  # the reduce ran on torch's stream
+        import torch
+        if acc.is_cuda:
+            torch.cuda.synchronize()
+
+    return PartitionedRender(
+        render_fn=lambda a, spp, base, r, w: ctx.trace_accumulate(spp, base),
+        acc=acc, rank=rank, world=world,
+        clear_fn=ctx.accum_clear, sync_fn=ctx.sync, after_reduce=sync_torch if world > 1 else None)

@@ -58,11 +58,15 @@ class NativeContext:
         check(self.lib.mfx_sample(self._h, spp, dptr(frame)), "mfx_sample")
         return frame
 
-    def render_rgba8(self, spp: int = 1, want_pixels: bool = True) -> np.ndarray | None:
+    def render_rgba8(self, spp: int = 1, want_pixels: bool = True, out: np.ndarray | None = None) -> np.ndarray | None:
+        """Film.GetFrame(spp) + post into `out` (a uint8 buffer of w*h*4, allocated if None), as
+        Scene.Render writes its byte[] (mfx_render_rgba8)."""
         if not want_pixels:
             check(self.lib.mfx_render_rgba8(self._h, spp, None), "mfx_render_rgba8")
             return None
-        out = np.empty(self.w * self.h * 4, dtype=np.uint8)
+        if out is None:
+            out = np.empty(self.w * self.h * 4, dtype=np.uint8)
+        assert out.dtype == np.uint8 and out.size == self.w * self.h * 4 and out.flags.c_contiguous
         check(self.lib.mfx_render_rgba8(self._h, spp, out.ctypes.data_as(C.POINTER(C.c_uint8))), "mfx_render_rgba8")
         return out
 

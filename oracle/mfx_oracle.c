@@ -419,6 +419,154 @@ static HitRecord bvh_hit(const Bvh* b, V3 o, V3 d, double tMin, double tMax, Tra
 }
 
 /* ------------------------------------------------------------------------------------------ */
+/* "fast" mode — the CPU baseline's second figure, NOT the reference          */
+/* algorithm: a 16-bin SAH BVH2 (leaves <= 4 primitives), closest hit front to back with tMax   */
+/* culling and hits beyond the current best rejected, and any-hit shadow rays that stop at the  */
+/* first occluder in (tMin, tMax). It shows what a conventional CPU tracer of the same         */
+/* integrator does; its results can differ from "strict" where the reference's missing tMax     */
+/* check in Triangle.Hit decides (the leaf quirk).                                */
+/* ------------------------------------------------------------------------------------------ */
+typedef struct { double lo[3], hi[3]; int first, count; } FNode; /* count > 0: leaf; else first = left child */
+typedef struct { FNode* nodes; int* idx; int nnodes; } FastBvh;
+
+static void fb_box(const Prim* prims, const int* idx, int n, double lo[3], double hi[3], int centroid) {
+    for (int a = 0; a < 3; a++) { lo[a] = INFINITY; hi[a] = -INFINITY; }
+    for (int k = 0; k < n; k++) {
+        Bound b = prim_bound(&prims[idx[k]]);
+        for (int a = 0; a < 3; a++) {
+            double l = vget(b.pmin, a), h = vget(b.pmax, a);
+            if (centroid) l = h = 0.5 * (l + h);
+            if (l < lo[a]) lo[a] = l;
+            if (h > hi[a]) hi[a] = h;
+        }
+    }
+}
+static double fb_area(const double lo[3], const double hi[3]) {
+    double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+    return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
+}
+static int fb_build(FastBvh* f, const Prim* prims, int* idx, int first, int n) {
+    const int me = f->nnodes++;
+    FNode* nd = &f->nodes[me];
+    fb_box(prims, idx + first, n, nd->lo, nd->hi, 0);
+    double clo[3], chi[3];
+    fb_box(prims, idx + first, n, clo, chi, 1);
+    int axis = 0;
+    for (int a = 1; a < 3; a++) if (chi[a] - clo[a] > chi[axis] - clo[axis]) axis = a;
+    const double ext = chi[axis] - clo[axis];
+    int best_split = -1;
+    double best_cost = (double)n;
+    enum { NB = 16 };
+    if (n > 4 && ext > 0) {
+        int cnt[NB] = {0};
+        double blo[NB][3], bhi[NB][3];
+        for (int b = 0; b < NB; b++) for (int a = 0; a < 3; a++) { blo[b][a] = INFINITY; bhi[b][a] = -INFINITY; }
+        for (int k = 0; k < n; k++) {
+            Bound bb = prim_bound(&prims[idx[first + k]]);
+            double c = 0.5 * (vget(bb.pmin, axis) + vget(bb.pmax, axis));
+            int b = (int)((c - clo[axis]) / ext * NB);
+            if (b >= NB) b = NB - 1;
+            if (b < 0) b = 0;
+            cnt[b]++;
+            for (int a = 0; a < 3; a++) {
+                if (vget(bb.pmin, a) < blo[b][a]) blo[b][a] = vget(bb.pmin, a);
+                if (vget(bb.pmax, a) > bhi[b][a]) bhi[b][a] = vget(bb.pmax, a);
+            }
+        }
+        const double inv = 1.0 / fb_area(nd->lo, nd->hi);
+        for (int sp = 1; sp < NB; sp++) {
+            double llo[3] = {INFINITY, INFINITY, INFINITY}, lhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            double rlo[3] = {INFINITY, INFINITY, INFINITY}, rhi[3] = {-INFINITY, -INFINITY, -INFINITY};
+            int nl = 0, nr = 0;
+            for (int b = 0; b < NB; b++) {
+                double* lo = b < sp ? llo : rlo;
+                double* hi = b < sp ? lhi : rhi;
+                if (b < sp) nl += cnt[b]; else nr += cnt[b];
+                for (int a = 0; a < 3; a++) {
+                    if (blo[b][a] < lo[a]) lo[a] = blo[b][a];
+                    if (bhi[b][a] > hi[a]) hi[a] = bhi[b][a];
+                }
+            }
+            if (!nl || !nr) continue;
+            const double cost = 0.125 + (nl * fb_area(llo, lhi) + nr * fb_area(rlo, rhi)) * inv;
+            if (cost < best_cost) { best_cost = cost; best_split = sp; }
+        }
+    }
+    if (best_split < 0 && n > 8) best_split = NB / 2; /* no SAH win but too many to test: median-ish */
+    if (best_split < 0) {
+        nd->first = first;
+        nd->count = n;
+        return me;
+    }
+    /* partition by bin (stable enough for a baseline); fall back to halves if a side is empty */
+    int mid = first;
+    for (int k = first; k < first + n; k++) {
+        Bound bb = prim_bound(&prims[idx[k]]);
+        double c = 0.5 * (vget(bb.pmin, axis) + vget(bb.pmax, axis));
+        int b = ext > 0 ? (int)((c - clo[axis]) / ext * NB) : 0;
+        if (b >= NB) b = NB - 1;
+        if (b < best_split) { int t = idx[k]; idx[k] = idx[mid]; idx[mid] = t; mid++; }
+    }
+    if (mid == first || mid == first + n) mid = first + n / 2;
+    nd->count = 0;
+    fb_build(f, prims, idx, first, mid - first);
+    f->nodes[me].first = fb_build(f, prims, idx, mid, first + n - mid);
+    return me;
+}
+static void fast_bvh_build(FastBvh* f, const Prim* prims, int n) {
+    f->idx = (int*)malloc(sizeof(int) * (size_t)n);
+    for (int k = 0; k < n; k++) f->idx[k] = k;
+    f->nodes = (FNode*)calloc((size_t)(2 * n), sizeof(FNode));
+    f->nnodes = 0;
+    fb_build(f, prims, f->idx, 0, n);
+}
+/* slab test with precomputed reciprocals; returns the entry distance or INFINITY */
+static double fb_slab(const FNode* nd, const double o[3], const double inv[3], double tMin, double tMax) {
+    double t0 = tMin, t1 = tMax;
+    for (int a = 0; a < 3; a++) {
+        double ta = (nd->lo[a] - o[a]) * inv[a], tb = (nd->hi[a] - o[a]) * inv[a];
+        if (ta > tb) { double t = ta; ta = tb; tb = t; }
+        if (ta > t0) t0 = ta;
+        if (tb < t1) t1 = tb;
+        if (t0 > t1) return INFINITY;
+    }
+    return t0;
+}
+static HitRecord fast_hit(const FastBvh* f, const Prim* prims, V3 o, V3 d, double tMin, double tMax, int any,
+                          TravStats* st) {
+    const double oo[3] = {o.x, o.y, o.z};
+    const double inv[3] = {1.0 / d.x, 1.0 / d.y, 1.0 / d.z};
+    HitRecord best = HIT_EMPTY;
+    double tbest = tMax;
+    int stack[128], sp = 0;
+    stack[sp++] = 0;
+    while (sp) {
+        const FNode* nd = &f->nodes[stack[--sp]];
+        if (st) st->nodes++;
+        if (fb_slab(nd, oo, inv, tMin, tbest) == INFINITY) continue;
+        if (nd->count > 0) {
+            if (st) { st->leaves++; st->prims += nd->count; }
+            for (int k = 0; k < nd->count; k++) {
+                const int pi = f->idx[nd->first + k];
+                HitRecord h = prim_hit(&prims[pi], o, d, tMin, tbest);
+                if (h.hit && h.t < tbest) {
+                    h.prim = pi;
+                    best = h;
+                    tbest = h.t;
+                    if (any) return best;
+                }
+            }
+            continue;
+        }
+        const int l = (int)(nd - f->nodes) + 1, r = nd->first;
+        const double tl = fb_slab(&f->nodes[l], oo, inv, tMin, tbest), tr = fb_slab(&f->nodes[r], oo, inv, tMin, tbest);
+        if (tl <= tr) { if (tr != INFINITY) stack[sp++] = r; if (tl != INFINITY) stack[sp++] = l; }
+        else { if (tl != INFINITY) stack[sp++] = l; if (tr != INFINITY) stack[sp++] = r; }
+    }
+    return best;
+}
+
+/* ------------------------------------------------------------------------------------------ */
 /* Counter-based RNG shared with the GPU                                         */
 /* ------------------------------------------------------------------------------------------ */
 static inline uint64_t mix64(uint64_t z) {
@@ -484,6 +632,7 @@ typedef struct {
     C3 light_color;     /* NewAreaLight.color */
     Pinhole cam;
     int width, height, max_depth;
+    FastBvh fast; /* built on first use of the "fast" mode */
 } OScene;
 
 static V3 arr3(const double* p) { return v3(p[0], p[1], p[2]); }
@@ -528,6 +677,8 @@ void oracle_destroy(OScene* s) {
     if (!s) return;
     free(s->bvh.indices);
     free(s->bvh.nodes);
+    free(s->fast.nodes);
+    free(s->fast.idx);
     free(s->prims);
     free(s->albedo);
     free(s);
@@ -570,9 +721,15 @@ static C3 light_L(const OScene* s, V3 toLight) {
 }
 
 /* PathIntegrator.TraceRay — Integrators.fs:107-137 (recursive, as the reference) */
-static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts* rc) {
+/* the closest-hit / shadow query of the selected mode: strict = the reference's Bvh.Hit */
+static HitRecord scene_hit(const OScene* s, int fast, int shadow, V3 o, V3 d, double tMin, double tMax, TravStats* st) {
+    if (fast) return fast_hit(&s->fast, s->prims, o, d, tMin, tMax, shadow, st);
+    return bvh_hit(&s->bvh, o, d, tMin, tMax, st);
+}
+
+static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts* rc, int fast) {
     if (depth < 0) return c3(0, 0, 0); /* the discarded depth -1 query (:108-109) is skipped */
-    HitRecord hit = bvh_hit(&s->bvh, o, d, 1e-6, 99999999., rc ? &rc->trav : NULL);
+    HitRecord hit = scene_hit(s, fast, 0, o, d, 1e-6, 99999999., rc ? &rc->trav : NULL);
     if (hit.hit && depth >= 0) {
         /* bxdf.SampleF — Material.fs:33-36 */
         C3 a = s->albedo[hit.material];
@@ -587,27 +744,27 @@ static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts*
         double pdf_li = 1. / s->light_rect.area;
         V3 unitToLight = vdiv(toLight, dist);
         if (rc) rc->shadow++;
-        HitRecord sh = bvh_hit(&s->bvh, hit.point, unitToLight, 1e-6, dist - 1e-6, rc ? &rc->trav : NULL);
+        HitRecord sh = scene_hit(s, fast, 1, hit.point, unitToLight, 1e-6, dist - 1e-6, rc ? &rc->trav : NULL);
         C3 l;
         if (sh.hit) l = c3(0, 0, 0);
         else l = cscale(vdot(unitToLight, hit.normal), light_L(s, toLight));
         /* (l / pdf_li + TraceRay(Ray(hit.point, wi), depth - 1)) * col / pdf   (:135-136) */
         if (rc && depth - 1 >= 0) rc->extension++;
-        C3 ind = trace_ray(s, hit.point, wi, depth - 1, rng, rc);
+        C3 ind = trace_ray(s, hit.point, wi, depth - 1, rng, rc, fast);
         return cdivf(cmul(cadd(cdivf(l, pdf_li), ind), col), pdf);
     }
     return c3(0, 0, 0);
 }
 
 /* One path's radiance for (pixel column i, row j, global sample) — Integrators.fs:166-170 */
-static C3 render_path(const OScene* s, uint64_t seed, int i, int j, int64_t sample, RayCounts* rc) {
+static C3 render_path(const OScene* s, uint64_t seed, int i, int j, int64_t sample, RayCounts* rc, int fast) {
     Rng rng = rng_path(seed, (uint64_t)i * (uint64_t)s->height + (uint64_t)j, (uint64_t)sample);
     double u = ((double)i + rng_next(&rng)) / (double)s->width;
     double v = ((double)j + rng_next(&rng)) / (double)s->height;
     V3 o, d;
     pinhole_get_ray(&s->cam, u, v, &o, &d);
     if (rc) { rc->primary++; rc->paths++; }
-    return trace_ray(s, o, d, s->max_depth, &rng, rc);
+    return trace_ray(s, o, d, s->max_depth, &rng, rc, fast);
 }
 
 /* PixelIntegrator.Sample(n) — Integrators.fs:161-172. frame is Color[w,h] x-major RGBA.
@@ -629,7 +786,7 @@ int oracle_sample(const OScene* s, uint64_t seed, int32_t spp, int64_t sample_ba
         RayCounts rc;
         memset(&rc, 0, sizeof(rc));
         for (int sidx = 0; sidx < spp; sidx++)
-            color = cadd(color, render_path(s, seed, i, j, sample_base + sidx, stats ? &rc : NULL));
+            color = cadd(color, render_path(s, seed, i, j, sample_base + sidx, stats ? &rc : NULL, 0));
         C3 m = cdivf(color, (double)spp);
         frame[q * 4 + 0] = m.r;
         frame[q * 4 + 1] = m.g;
@@ -651,9 +808,11 @@ int oracle_sample(const OScene* s, uint64_t seed, int32_t spp, int64_t sample_ba
 }
 
 /* Radiance of an explicit list of (pixel, sample) paths — for timing a bounded sample of a
- * workload (bench.py cpu_baseline) and for per-path parity tests. out[k*3+c]. */
-int oracle_paths(const OScene* s, uint64_t seed, int64_t n, const int32_t* px, const int32_t* py,
-                 const int64_t* sample, int32_t nthreads, double* out, double* stats) {
+ * workload (bench.py cpu_baseline) and for per-path parity tests. out[k*3+c].
+ * mode 0 = strict (the reference algorithm), 1 = fast (SAH BVH2, tMax culling, any-hit shadows). */
+int oracle_paths_mode(OScene* s, uint64_t seed, int64_t n, const int32_t* px, const int32_t* py,
+                      const int64_t* sample, int32_t nthreads, int32_t mode, double* out, double* stats) {
+    if (mode == 1 && !s->fast.nodes) fast_bvh_build(&s->fast, s->prims, s->nprims);
     int64_t tp = 0, te = 0, ts = 0, tpaths = 0;
 #ifdef _OPENMP
     if (nthreads > 0) omp_set_num_threads(nthreads);
@@ -663,7 +822,7 @@ int oracle_paths(const OScene* s, uint64_t seed, int64_t n, const int32_t* px, c
     for (int64_t k = 0; k < n; k++) {
         RayCounts rc;
         memset(&rc, 0, sizeof(rc));
-        C3 c = render_path(s, seed, px[k], py[k], sample[k], &rc);
+        C3 c = render_path(s, seed, px[k], py[k], sample[k], &rc, mode == 1);
         out[k * 3 + 0] = c.r; out[k * 3 + 1] = c.g; out[k * 3 + 2] = c.b;
         tp += rc.primary; te += rc.extension; ts += rc.shadow; tpaths += rc.paths;
     }
@@ -674,6 +833,11 @@ int oracle_paths(const OScene* s, uint64_t seed, int64_t n, const int32_t* px, c
 #endif
     }
     return 0;
+}
+
+int oracle_paths(OScene* s, uint64_t seed, int64_t n, const int32_t* px, const int32_t* py,
+                 const int64_t* sample, int32_t nthreads, double* out, double* stats) {
+    return oracle_paths_mode(s, seed, n, px, py, sample, nthreads, 0, out, stats);
 }
 
 /* Bvh.Hit for a batch of rays (closest hit). rays[k*6..]: origin, direction. */

@@ -39,6 +39,8 @@ def lib():
         L.oracle_sample.argtypes = [C.c_void_p, C.c_uint64, C.c_int32, C.c_int64, C.c_int32, _dp, _dp]
         L.oracle_paths.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, _ip, _ip, C.POINTER(C.c_int64),
                                    C.c_int32, _dp, _dp]
+        L.oracle_paths_mode.argtypes = [C.c_void_p, C.c_uint64, C.c_int64, _ip, _ip, C.POINTER(C.c_int64),
+                                        C.c_int32, C.c_int32, _dp, _dp]
         L.oracle_closest_hit.argtypes = [C.c_void_p, C.c_int64, _dp, C.c_double, C.c_double, _dp, _ip, _dp]
         L.oracle_any_hit.argtypes = [C.c_void_p, C.c_int64, _dp, C.c_double, _dp, _ip]
         L.oracle_bvh_leaves.argtypes = [C.c_void_p, _ip, _ip, _ip, _ip]
@@ -88,14 +90,17 @@ class OracleScene:
         assert rc == 0
         return (frame, stats) if with_stats else frame
 
-    def paths(self, px, py, samples, seed: int, nthreads: int = 0):
+    def paths(self, px, py, samples, seed: int, nthreads: int = 0, mode: str = "strict"):
+        """Radiance of explicit (pixel, sample) paths. mode "strict" = the reference algorithm;
+        "fast" = SAH BVH2 with tMax culling and any-hit shadows (a CPU-baseline figure only)."""
         px = np.ascontiguousarray(px, dtype=np.int32)
         py = np.ascontiguousarray(py, dtype=np.int32)
         samples = np.ascontiguousarray(samples, dtype=np.int64)
         out = np.zeros((len(px), 3), dtype=np.float64)
         stats = np.zeros(8, dtype=np.float64)
-        lib().oracle_paths(self.h, seed, len(px), iptr(px), iptr(py),
-                           samples.ctypes.data_as(C.POINTER(C.c_int64)), nthreads, dptr(out), dptr(stats))
+        lib().oracle_paths_mode(self.h, seed, len(px), iptr(px), iptr(py),
+                                samples.ctypes.data_as(C.POINTER(C.c_int64)), nthreads,
+                                {"strict": 0, "fast": 1}[mode], dptr(out), dptr(stats))
         return out, stats
 
     def closest_hit(self, rays: np.ndarray, tmin=1e-6, tmax=99999999.0):

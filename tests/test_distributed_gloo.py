@@ -1,7 +1,8 @@
-"""Multi-rank composition (DESIGN.md §7) on CPU: world_size 2 over gloo. Each rank renders its
-sample partition — here with the CPU oracle standing in for the per-rank GPU tracer, since the
-container has no GPU — into an FP64 accumulator, PartitionedRender reduces to rank 0, and the
-result must equal the single-rank image."""
+"""Multi-rank composition (DESIGN.md §8) on CPU: world_size 2 over gloo. Each rank renders its
+sample partition into an FP64 accumulator and the partitions are reduced to rank 0; the result
+must equal the single-rank image. The ranks run `native_partitioned_render` — the function
+bench.py's multi-process path runs — over a stand-in context whose trace is the CPU oracle (the
+container has no GPU), so the clear / trace / sync / reduce sequence tested is the bench's."""
 import os
 import socket
 import sys
@@ -22,6 +23,41 @@ def _free_port():
     return p
 
 
+class OracleContext:
+    """Stand-in for NativeContext with the methods native_partitioned_render calls; its trace adds
+    this rank's partition of the frame (global samples s = base + part_index mod part_count,
+    mfx_trace_accumulate's contract) to the attached accumulator, with the CPU oracle."""
+
+    def __init__(self, oscene, acc, part_index, part_count):
+        self.o, self.acc, self.pi, self.pc = oscene, acc, part_index, part_count
+        self.calls = []
+
+    def accum_attach(self, ptr, nbytes):
+        assert ptr == self.acc.data_ptr() and nbytes == self.acc.numel() * 8
+        self.calls.append("attach")
+
+    def accum_clear(self):
+        self.acc.zero_()
+        self.calls.append("clear")
+
+    def sync(self):
+        self.calls.append("sync")
+
+    def trace_accumulate(self, spp, base):
+        import torch
+        from mafrixraytracing_amd.distributed import partition_samples
+        s = partition_samples(spp, self.pi, self.pc) + base
+        px, py, ss = np.meshgrid(np.arange(W), np.arange(H), s, indexing="ij")
+        out, _ = self.o.paths(px.ravel(), py.ravel(), ss.ravel(), SEED, nthreads=2)
+        pix = (px.ravel() * H + py.ravel())
+        npix = W * H
+        acc_np = np.zeros(3 * npix)
+        for c in range(3):
+            np.add.at(acc_np, c * npix + pix, out[:, c])
+        self.acc += torch.from_numpy(acc_np)
+        self.calls.append("trace")
+
+
 def _worker(rank, world, port, outdir):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
@@ -30,25 +66,14 @@ def _worker(rank, world, port, outdir):
 
     import pyoracle
     from conftest import scene
-    from mafrixraytracing_amd.distributed import PartitionedRender, partition_samples
+    from mafrixraytracing_amd.distributed import native_partitioned_render
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     a = scene("spot", W, H)
-    o = pyoracle.OracleScene(a)
-    npix = W * H
-
-    def render_fn(acc, spp, base, r, w):
-        s = partition_samples(spp, r, w) + base
-        px, py, ss = np.meshgrid(np.arange(W), np.arange(H), s, indexing="ij")
-        out, _ = o.paths(px.ravel(), py.ravel(), ss.ravel(), SEED, nthreads=2)
-        pix = (px.ravel() * H + py.ravel())
-        acc_np = np.zeros(3 * npix)
-        for c in range(3):
-            np.add.at(acc_np, c * npix + pix, out[:, c])
-        acc += torch.from_numpy(acc_np)
-
-    acc = torch.zeros(3 * npix, dtype=torch.float64)
-    PartitionedRender(render_fn, acc, rank, world).frame(SPP, sample_base=7)
+    acc = torch.zeros(3 * W * H, dtype=torch.float64)
+    ctx = OracleContext(pyoracle.OracleScene(a), acc, rank, world)
+    native_partitioned_render(ctx, acc, rank, world).frame(SPP, sample_base=7)
+    assert ctx.calls == ["attach", "clear", "trace", "sync"], ctx.calls
     if rank == 0:
         np.save(os.path.join(outdir, "reduced.npy"), acc.numpy())
     dist.barrier()
@@ -73,3 +98,13 @@ def test_partition_covers_every_sample_once():
         for world in (1, 2, 3, 8):
             allp = np.concatenate([partition_samples(spp, r, world) for r in range(world)])
             assert sorted(allp.tolist()) == list(range(spp))
+
+
+def test_step_spp_weak_and_strong():
+    from mafrixraytracing_amd.distributed import step_spp
+    assert step_spp(64, 8, "weak") == 512 and step_spp(64, 1, "weak") == 64
+    assert step_spp(64, 8, "strong") == 64
+    with pytest.raises(ValueError):
+        step_spp(4, 8, "strong")
+    with pytest.raises(ValueError):
+        step_spp(64, 2, "linear")
