@@ -358,7 +358,7 @@ def main():
                             "profiles/bray_fixture.json (frozen)" if fixture else "live counters",
                         "rays_per_launch": round(krays / launches, 1)}
 
-            if args.megakernel:
+            if args.megakernel or stage_ms["shadow_ms"] == 0:  # the megakernel ran (also: 1-spp calls)
                 bray = bytes_per_ray(stats["all"])
                 if fixture:
                     fc, fs = fixture["closest"], fixture["shadow"]

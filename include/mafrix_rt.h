@@ -115,6 +115,9 @@ typedef struct mfx_options {
 #define MFX_F_COUNT_STATS 1 /* count traversal node/leaf/prim visits (slower; for the roofline model) */
 #define MFX_F_MEGAKERNEL 2  /* one persistent megakernel instead of the wavefront pipeline */
 #define MFX_F_HOST_BVH 4    /* build the traversal BVH on the host CPU (default: on the GPU; the same tree) */
+#define MFX_F_WAVEFRONT 8   /* always the wavefront pipeline. Default: a call in which a device renders one
+                               sample per pixel (Scene.Render) runs the megakernel, which is faster there
+                               and gives the same bits (one path per pixel: no summation order) */
 
 typedef struct mfx_ctx mfx_ctx;
 

@@ -20,6 +20,7 @@ MFX_F_NONE = 0
 MFX_F_COUNT_STATS = 1
 MFX_F_MEGAKERNEL = 2
 MFX_F_HOST_BVH = 4
+MFX_F_WAVEFRONT = 8
 MFX_MAX_DEVICES = 64
 MFX_ABI_VERSION = 2
 

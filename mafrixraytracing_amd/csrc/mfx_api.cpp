@@ -459,15 +459,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.ntop_shd = c->wf_ntop_shd;
     P.shadow_waves = c->wf_shadow_waves;
     P.spill = c->d_spill;
-    // Slots per chunk fetch: the default 1024 when every wave of the larger grid gets >= 8
-    // chunks; smaller for a small generation (a 1-spp Scene.Render call at 1080p is 2 M paths:
-    // 1024-slot chunks left half the waves without work and the rest with 16 rays per lane)
-    {
-        const int64_t waves = (int64_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 4;
-        int64_t ch = c->wf_chunk;
-        while (ch > 64 && (int64_t)pool / ch < 8 * waves) ch /= 2;
-        P.chunk = (int)(ch / 64 * 64);
-    }
+    P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
@@ -522,7 +514,11 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
     HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
     HIPCHECK(hipMemsetAsync(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long), c->stream));
-    c->mega_last = (c->flags & MFX_F_MEGAKERNEL) != 0;
+    // One sample per pixel on this device (Scene.Render's call): the megakernel, unless the caller
+    // pins the wavefront. With one path per pixel its FP64 atomic add onto the zeroed accumulator
+    // is exact, and its per-path arithmetic is the wavefront's, so the bits are the same; it does
+    // not pay the wavefront's per-bounce launches over a 2 M-path frame (r02e: 1.7 vs 7.9 ms at 1080p).
+    c->mega_last = (c->flags & MFX_F_MEGAKERNEL) != 0 || (ns == 1 && (c->flags & MFX_F_WAVEFRONT) == 0);
     if (ns == 0) {  // this partition has no sample in the call: zero rays in zero device time
         HIPCHECK(hipEventRecord(c->ev0, c->stream));
         HIPCHECK(hipEventRecord(c->ev1, c->stream));

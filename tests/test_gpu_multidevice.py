@@ -103,3 +103,23 @@ def test_bad_device_lists_fail_loudly(gpu):
         with NativeContext(a, seed=SEED, devices=[0, 0], part_index=0, part_count=2) as m:
             m.sample(1)
     _ = C
+
+
+def test_one_sample_calls_megakernel_equals_wavefront(gpu):
+    """A call in which the device renders one sample per pixel (Scene.Render) runs the megakernel
+    by default; MFX_F_WAVEFRONT pins the wavefront. Same paths, same per-path arithmetic, one path
+    per pixel (exact accumulation): identical bits, counters and bytes."""
+    from mafrixraytracing_amd.abi import MFX_F_WAVEFRONT
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 96, 54)
+    with NativeContext(a, seed=SEED) as auto, NativeContext(a, seed=SEED, flags=MFX_F_WAVEFRONT) as wf:
+        for _ in range(3):
+            assert np.array_equal(auto.render_rgba8(1), wf.render_rgba8(1))
+            assert np.array_equal(auto.ray_counts()[:4], wf.ray_counts()[:4])
+            assert auto.trace_timing()["launches"] == 1 and wf.trace_timing()["launches"] == 4
+        assert np.array_equal(auto.film_mean(), wf.film_mean())
+        assert np.array_equal(auto.sample(1), wf.sample(1))
+    # two devices of one sample each: every device takes the megakernel
+    with NativeContext(a, seed=SEED, devices=[0, 0]) as m2, NativeContext(a, seed=SEED, devices=[0, 0],
+                                                                         flags=MFX_F_WAVEFRONT) as w2:
+        assert np.array_equal(m2.sample(2), w2.sample(2))
