@@ -123,6 +123,7 @@ struct mfx_ctx {
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
+    int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int wf_stack_lds = 1;            // traversal stack entries per lane in LDS (the rest spill)
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
@@ -219,6 +220,7 @@ static int ctx_setup(mfx_ctx* c) {
     }
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
+    if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
@@ -549,7 +551,16 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.height = c->host.height;
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
-    P.chunk = 256;
+    // paths per chunk: 256, halved while fewer than 16 chunks per wave remain (a 1-spp frame:
+    // 64, one path per lane per fetch; r02g/r02i A/B at 1 spp: 256 -> 64 is +21 %)
+    if (c->mega_chunk > 0) {
+        P.chunk = c->mega_chunk;
+    } else {
+        const int64_t total = (int64_t)((c->host.width + 7) / 8) * ((c->host.height + 7) / 8) * 64 * ns;
+        int64_t ch = 256;
+        while (ch > 64 && total / ch < 16 * (int64_t)c->grid * 4) ch /= 2;
+        P.chunk = (int)ch;
+    }
     HIPCHECK(hipEventRecord(c->ev0, c->stream));
     HIPCHECK(mfx_launch_trace(P, (c->flags & MFX_F_COUNT_STATS) != 0, c->grid, c->stream));
     HIPCHECK(hipEventRecord(c->ev1, c->stream));

@@ -12,6 +12,8 @@
 //   query kernels     Bvh.Hit closest / shadow for explicit ray lists (parity tests).
 //   film/post         accumulate -> mean -> ACES -> sqrt -> RGBA8 (Scene.fs:273-330, Film.fs:18-23).
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <stdint.h>
 
 #include "mfx_layout.h"
@@ -28,6 +30,8 @@
 
 template <bool STATS>
 __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TraceParams P) {
+    // one traversal-stack column per lane in LDS. (The top BVH levels in LDS, as the wavefront
+    // kernels keep them, measured -21 % here at 1 spp, r02i: the per-node LDS/global branch.)
     extern __shared__ int lds[];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -337,8 +341,10 @@ __global__ void fp64_selftest_kernel(const double* a, const double* b, int64_t n
 // ----------------------------------------------------------------------------------------------
 static inline unsigned grid_for(int64_t n, int block) { return (unsigned)((n + block - 1) / block); }
 
+static size_t trace_lds_bytes(int stack_size) { return (size_t)4 * stack_size * 64 * sizeof(int); }
+
 hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st) {
-    const size_t lds = (size_t)4 * P.stack_size * 64 * sizeof(int);
+    const size_t lds = trace_lds_bytes(P.stack_size);
     if (stats)
         hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(256), lds, st, P);
     else
@@ -347,8 +353,12 @@ hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStrea
 }
 
 hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu) {
-    const size_t lds = (size_t)4 * stack_size * 64 * sizeof(int);
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false>, 256, lds);
+    const size_t lds = trace_lds_bytes(stack_size);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false>, 256, lds);
+    // gfx950 allocates LDS in 1,280-byte granules of its 160 KB (the API counts finer ones)
+    const size_t g = 1280;
+    *blocks_per_cu = std::min(*blocks_per_cu, (int)(160 * 1024 / ((lds + g - 1) / g * g)));
+    return e;
 }
 
 hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st) {

@@ -35,7 +35,7 @@ def main():
     for r in range(rounds):
         for l in libs:
             code = CHILD.replace("ROOT", repr(ROOT)).replace("LIB", repr(l)).replace("SCENE", repr(scene)) \
-                .replace("STEPS", "2").replace("SPP", str(spp))
+                .replace("STEPS", str(min(20, max(2, 64 // spp)))).replace("SPP", str(spp))
             env = dict(os.environ)
             ef = l[:-3] + ".env"  # optional KEY=VALUE lines for this variant (e.g. MFX_CHUNK=1024)
             if os.path.exists(ef):
