@@ -128,6 +128,7 @@ struct mfx_ctx {
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
+    double* d_vscratch = nullptr;    // megakernel: per-lane vertex records [max_depth + 1][6][grid * 256]
     bool diag_iter = false;
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
@@ -156,7 +157,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->it_ev)
@@ -214,7 +215,8 @@ static int ctx_setup(mfx_ctx* c) {
     {
         size_t mfree = 0, mtotal = 0;
         if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
-            const int64_t fit = (int64_t)(mfree / 4 / (WF_DOUBLES_PER_SLOT * 8 + WF_WORDS_PER_SLOT * 4));
+            const int64_t fit =
+                (int64_t)(mfree / 4 / (WF_DOUBLES_PER_SLOT(c->host.max_depth + 1) * 8 + WF_WORDS_PER_SLOT * 4));
             c->wf_pool_max = std::max<int64_t>(1 << 20, std::min<int64_t>(c->wf_pool_max, fit));
         }
     }
@@ -289,6 +291,7 @@ static int ctx_setup(mfx_ctx* c) {
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
         CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, c->stack_size - c->wf_stack_lds)));
     }
+    CK(hipMalloc((void**)&c->d_vscratch, sizeof(double) * 6 * (size_t)(c->host.max_depth + 1) * c->grid * 256));
 #undef CK
     return MFX_OK;
 }
@@ -402,15 +405,18 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     c->wf_mem = nullptr;
     c->wf_pool = 0;
     const size_t P = (size_t)pool;
-    const size_t bytes = P * (WF_DOUBLES_PER_SLOT * 8 + WF_WORDS_PER_SLOT * 4) + 64 * 256;
+    const int nv = c->host.max_depth + 1;  // vertices per path
+    const size_t bytes = P * (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT * 4) + 64 * 256;
     hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
     char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
-    double** dbl[WF_DOUBLES_PER_SLOT - 1] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz,
-                                             &c->wf.tx, &c->wf.ty, &c->wf.tz, &c->wf.lx, &c->wf.ly, &c->wf.lz};
+    double** dbl[6] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz};
     for (double** d : dbl) *d = (double*)take(P * 8);
+    c->wf.va = (double*)take(P * 8 * 3 * nv);
+    c->wf.vc = (double*)take(P * 8 * 3 * nv);
+    c->wf.vstride = (int64_t)P;
     c->wf.key = (uint64_t*)take(P * 8);
     c->wf.rn = (uint32_t*)take(P * 4);
     c->wf.depth = (int32_t*)take(P * 4);
@@ -497,8 +503,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
                 HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
                 fprintf(stderr, "gen %lld iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
-                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g\n", (long long)g, d + 1,
-                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15]);
+                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g; cumulative traversal closest %.0f %.0f %.0f"
+                        " shadow %.0f %.0f %.0f\n", (long long)g, d + 1,
+                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9]);
             }
         }
         HIPCHECK(mfx_wf_resolve(P, c->stream));
@@ -551,6 +558,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.height = c->host.height;
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
+    P.vscratch = c->d_vscratch;
     // paths per chunk: 256, halved while fewer than 16 chunks per wave remain (a 1-spp frame:
     // 64, one path per lane per fetch; r02g/r02i A/B at 1 spp: 256 -> 64 is +21 %)
     if (c->mega_chunk > 0) {

@@ -25,6 +25,7 @@ struct TraceParams {
     int32_t width, height, max_depth;
     int32_t stack_size;              // LDS traversal stack entries per lane
     int32_t chunk;                   // path indices a wave takes per atomic
+    double* vscratch;                // [max_depth + 1][6][grid * 256] per-lane vertex records (a_v, c_v)
 };
 
 struct QueryParams {

@@ -45,13 +45,17 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
     const int64_t total = per_sample * P.nsamples;
 
-    // path state
+    // path state. A vertex's direct term a_v and col c_v go to this lane's scratch column and are
+    // folded back to the camera when the path ends, in the reference's recursion order (see k_resolve)
     bool alive = false;
     int depth = 0;
+    int lit = 0;  // bit v: vertex v's a_v is recorded
     int64_t pixel = 0;
     uint64_t key = 0;
     uint32_t rn = 0;
-    DV o = dv(0, 0, 0), d = dv(0, 0, 0), T = dv(0, 0, 0), L = dv(0, 0, 0);
+    DV o = dv(0, 0, 0), d = dv(0, 0, 0);
+    const int64_t vstride = (int64_t)gridDim.x * blockDim.x;
+    double* const vs = P.vscratch + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // [v][a/c][rgb][vstride]
     uint32_t c_primary = 0, c_ext = 0, c_shadow = 0;
     Stats st{0, 0, 0}, st2{0, 0, 0};
 
@@ -99,8 +103,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
                     const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
                     o = ld3(CAM.position);
                     d = vnormalize(vsub(target, o));
-                    T = dv(1, 1, 1);
-                    L = dv(0, 0, 0);
+                    lit = 0;
                     depth = P.max_depth;
                     alive = true;
                     c_primary++;
@@ -145,7 +148,11 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             const DV wi = vnormalize(p);
             const double ei = vdot(nm, wi);
             const double* a = sh.albedo;
-            const DV col = dv(TWOPI * (ei * (INVPI * a[0])), TWOPI * (ei * (INVPI * a[1])), TWOPI * (ei * (INVPI * a[2])));
+            const int v = P.max_depth - depth;  // this vertex's index
+            double* vrec = vs + (int64_t)(6 * v) * vstride;
+            vrec[3 * vstride] = TWOPI * (ei * (INVPI * a[0]));  // c_v = col (Material.fs:36)
+            vrec[4 * vstride] = TWOPI * (ei * (INVPI * a[1]));
+            vrec[5 * vstride] = TWOPI * (ei * (INVPI * a[2]));
             // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
             const double sel = rng_next(key, rn);
             const int lt = sel < 0.5 ? 0 : 1;
@@ -168,17 +175,16 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
             const double solid = fabs(cos_o) * LT.area / dist2;
             const double cs = vdot(unit, nm);
-            const bool lit = cos_o < 0.;
-            T = dv(T.x * col.x, T.y * col.y, T.z * col.z);  // path throughput incl. this vertex's col
+            const bool lightable = cos_o < 0.;
             // SingleDirectLightIntegrator.Eval — Integrators.fs:41-52
             Best sb;
             const bool occluded = traverse<true, STATS>(S, hp, unit, 1e-6, dist - 1e-6, stack, sb, st2);
             c_shadow++;
-            if (!occluded && lit) {
-                // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
-                L.x += T.x * ((cs * (solid * LT.color[0])) / LT.pdf);
-                L.y += T.y * ((cs * (solid * LT.color[1])) / LT.pdf);
-                L.z += T.z * ((cs * (solid * LT.color[2])) / LT.pdf);
+            if (!occluded && lightable) {  // a_v = l / pdf_li
+                vrec[0] = (cs * (solid * LT.color[0])) / LT.pdf;
+                vrec[vstride] = (cs * (solid * LT.color[1])) / LT.pdf;
+                vrec[2 * vstride] = (cs * (solid * LT.color[2])) / LT.pdf;
+                lit |= 1 << v;
             }
             depth -= 1;
             if (depth < 0) {
@@ -189,9 +195,20 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             }
         }
         if (finish) {
-            if (L.x != 0.0) unsafeAtomicAdd(P.accum + pixel, L.x);
-            if (L.y != 0.0) unsafeAtomicAdd(P.accum + npix + pixel, L.y);
-            if (L.z != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pixel, L.z);
+            if (lit) {  // (l / pdf_li + TraceRay(next)) * col / pdf, deepest lit vertex first (Integrators.fs:136)
+                double fx = 0.0, fy = 0.0, fz = 0.0;
+                for (int v = 31 - __builtin_clz(lit); v >= 0; --v) {
+                    const double* vv = vs + (int64_t)(6 * v) * vstride;
+                    const bool l = (lit >> v) & 1;
+                    fx = ((l ? vv[0] : 0.0) + fx) * vv[3 * vstride];
+                    fy = ((l ? vv[vstride] : 0.0) + fy) * vv[4 * vstride];
+                    fz = ((l ? vv[2 * vstride] : 0.0) + fz) * vv[5 * vstride];
+                }
+                // one path per pixel and call (Scene.Render): the add onto the zeroed accumulator is exact
+                if (fx != 0.0) unsafeAtomicAdd(P.accum + pixel, fx);
+                if (fy != 0.0) unsafeAtomicAdd(P.accum + npix + pixel, fy);
+                if (fz != 0.0) unsafeAtomicAdd(P.accum + 2 * npix + pixel, fz);
+            }
             alive = false;
         }
     }

@@ -445,6 +445,11 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
         err = "max_depth must be >= 0";
         return false;
     }
+    // a path's vertices are recorded for the exact fold (mfx_wavefront.h): at most 16 of them
+    if (d->max_depth >= 16) {
+        err = "max_depth must be <= 15 (the reference uses 3, Scene.fs:304)";
+        return false;
+    }
     const int n = (int)d->nprims;
     s.width = d->width;
     s.height = d->height;

@@ -9,8 +9,13 @@
 // Each slot carries its path through a state machine; each kernel scans the pool for the slots
 // in its state, so no ray queue (and no hot queue-tail atomic) exists:
 //   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
-//   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (radiance in lx..lz) or FREE (black)
+//   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (a lit vertex recorded) or FREE (none)
 //   MISS -(k_shadow)-> DONE, or FREE for a camera ray's miss
+// A path's radiance is not summed forward. Each vertex v records its direct term a_v = l / pdf_li
+// and its BRDF factor c_v = col (both FP64 RGB), and k_resolve folds them from the deepest lit
+// vertex back to the camera, acc = (a_v + acc) * c_v, which is the reference's recursion
+// (l / pdf_li + TraceRay(next)) * col / pdf (Integrators.fs:135-136, pdf = 1) in its own
+// operation order: the image is the oracle's bit for bit.
 // A HIT state word also carries the hit's shade[] index, so the shading needs no extra lookup.
 // The only atomics are per-wave chunk fetches, spread over WF_SHARDS counters (a returning
 // atomic on one word saturates near 88 per microsecond).
@@ -28,9 +33,13 @@
 #define WF_MISS 3   // k_extend found no hit
 #define WF_FRESH 4  // flag on WF_HIT / WF_MISS: the path's camera ray. Its throughput (1), radiance
                     // (0), draw count (2) and depth (max_depth) are implicit: never stored
-#define WF_DONE 8   // finished with radiance in lx..lz: k_resolve adds it to its pixel
+#define WF_DONE 8   // finished with a lit vertex: k_resolve folds its vertices and adds them to its pixel
 #define WF_STATE_MASK 15
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
+// depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
+// shadow ray reached the light); so at most WF_MAX_VERTS vertices (max_depth < WF_MAX_VERTS)
+#define WF_MAX_VERTS 16
+#define WF_LIT_SHIFT 8
 
 #ifndef WF_SHARDS
 #define WF_SHARDS 64  // returning atomics on one word serialize (~88 per us): 8 shards -> 64 is +13 % on C2
@@ -57,8 +66,9 @@ struct WfParams {
     // path slots (SoA)
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
     double *dx, *dy, *dz;  // ray direction
-    double *tx, *ty, *tz;  // throughput
-    double *lx, *ly, *lz;  // radiance
+    double* va;            // [vertex][channel][stride] direct term a_v = l / pdf_li of a lit vertex
+    double* vc;            // [vertex][channel][stride] BRDF factor c_v = col of every vertex
+    int64_t vstride;       // slots per va / vc row (the allocated pool)
     uint64_t* key;         // RNG key of the path
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)
@@ -84,8 +94,8 @@ struct WfParams {
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
 };
 
-// 8-byte and 4-byte words per slot in the SoA pool
-#define WF_DOUBLES_PER_SLOT 13  // o, d, throughput, radiance (12) + key
+// 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and 6 per vertex (a_v, c_v)
+#define WF_DOUBLES_PER_SLOT(nvert) (7 + 6 * (nvert))
 #define WF_WORDS_PER_SLOT 3     // rn, depth, state
 
 #ifndef WF_STACK_LDS

@@ -6,12 +6,13 @@
 //              generation's first iteration every FREE slot j starts path path_base + j
 //              (PixelIntegrator.Sample + PinholeCamera.GetRay, Integrators.fs:161-169,
 //              Camera.fs:134-139). Writes the hit point and the hit's shade index.
-//   k_shadow   one vertex of PathIntegrator.TraceRay for HIT slots: LambertianBrdf.SampleF,
-//              NewAreaLight.Sample_Li and the throughput update (Integrators.fs:110-136), then
-//              the vertex's shadow ray (Integrators.fs:44) traced by a lane of the same wave;
-//              unoccluded -> L += direct term. Finished paths keep their radiance in the slot.
-//   k_resolve  after a generation: each pixel's finished paths added to the accumulator in
-//              sample order (PixelIntegrator's `color <- color + ...`, Integrators.fs:169).
+//   k_shadow   one vertex of PathIntegrator.TraceRay for HIT slots: LambertianBrdf.SampleF and
+//              NewAreaLight.Sample_Li (Integrators.fs:110-134), recording the vertex's col, then
+//              its shadow ray (Integrators.fs:44) traced by a lane of the same wave; unoccluded ->
+//              the vertex's direct term l / pdf_li is recorded too (mfx_wavefront.h).
+//   k_resolve  after a generation: each finished path's vertices folded back to the camera in the
+//              reference's recursion order, (l / pdf_li + TraceRay(next)) * col (Integrators.fs:136),
+//              and added to its pixel in sample order (`color <- color + ...`, Integrators.fs:169).
 //
 // Both trace kernels keep lanes busy: a lane that finishes its ray takes the next pending ray at
 // the next step (persistent while-while with dynamic fetch, Aila & Laine 2009). Pending rays come
@@ -20,7 +21,7 @@
 // popcount ranks) into a per-wave LDS list, and the per-slot data is loaded by the lane that takes
 // the entry. k_shadow shades 64 listed hits at a time with all lanes and hands the shadow rays to
 // the traversal in LDS, so a shadow ray never round-trips through HBM. Path state lives in HBM as
-// SoA FP64; every arithmetic step is the same FP64 expression as the megakernel and the oracle.
+// SoA FP64; every arithmetic step is the same FP64 expression as the oracle, in the same order.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -436,13 +437,13 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
     int nshade = 0;      // wave-uniform: hits listed for shading
-    bool fresh = false;  // the lane's vertex is its path's first (radiance 0 in registers only)
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
     Trav T{};
-    double scx = 0.0, scy = 0.0, scz = 0.0;  // this vertex's direct term if unoccluded
-    bool cont = false;                        // the path continues after this vertex
+    double scx = 0.0, scy = 0.0, scz = 0.0;  // this vertex's direct term a_v = l / pdf_li if unoccluded
+    int vflag = 0;  // the lane's vertex: bit 0 the path continues, bit 1 lightable (cos_o < 0),
+                    // bits 2..5 its index v, bits 8.. the path's lit mask so far (PD_* below)
     uint32_t c_shadow = 0;
     Stats st{0, 0, 0};
 #ifdef MFX_DIAG_OCCLUSION
@@ -484,7 +485,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 const int cnt = nshade < 64 ? nshade : 64;
                 if (lane < cnt) {
                     const int j = shl[lane] & 0x7fffffff;
-                    const bool first = shl[lane] < 0;  // throughput 1, draws 2, depth max_depth implicit
+                    const bool first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
                     const int slot = shl[WF_SHD_LIST + lane];
                     const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
@@ -534,30 +535,31 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
                     const double solid = fabs(cos_o) * LT.area / dist2;
                     const double cs = vdot(unit, nm);
-                    double Tx = 1.0, Ty = 1.0, Tz = 1.0;
-                    if (!first) { Tx = P.tx[j]; Ty = P.ty[j]; Tz = P.tz[j]; }
-                    Tx = Tx * (TWOPI * (ei * (INVPI * a[0])));
-                    Ty = Ty * (TWOPI * (ei * (INVPI * a[1])));
-                    Tz = Tz * (TWOPI * (ei * (INVPI * a[2])));
-                    // (l / pdf_li + TraceRay(next)) * col / pdf, unrolled forward (Integrators.fs:135-136)
+                    const int dw = first ? P.max_depth : P.depth[j];  // remaining depth | lit mask << 8
+                    const int v = P.max_depth - (dw & 0xff);          // this vertex's index
+                    // col = INVPI * a * ei * TwoPi (Material.fs:36): the vertex's factor c_v
+                    double* vc = P.vc + (int64_t)(3 * v) * P.vstride + j;
+                    vc[0] = TWOPI * (ei * (INVPI * a[0]));
+                    vc[P.vstride] = TWOPI * (ei * (INVPI * a[1]));
+                    vc[2 * P.vstride] = TWOPI * (ei * (INVPI * a[2]));
+                    // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56):
+                    // the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0
                     double dx = 0.0, dy = 0.0, dz = 0.0;
-                    if (cos_o < 0.) {
-                        dx = Tx * ((cs * (solid * LT.color[0])) / LT.pdf);
-                        dy = Ty * ((cs * (solid * LT.color[1])) / LT.pdf);
-                        dz = Tz * ((cs * (solid * LT.color[2])) / LT.pdf);
+                    const bool lightable = cos_o < 0.;
+                    if (lightable) {
+                        dx = (cs * (solid * LT.color[0])) / LT.pdf;
+                        dy = (cs * (solid * LT.color[1])) / LT.pdf;
+                        dz = (cs * (solid * LT.color[2])) / LT.pdf;
                     }
-                    const int depth = (first ? P.max_depth : P.depth[j]) - 1;
                     // the depth -1 query's result is discarded (Integrators.fs:109): never traced
-                    const bool cn = depth >= 0;
-                    if (cn) {  // what the next vertex reads
-                        P.tx[j] = Tx; P.ty[j] = Ty; P.tz[j] = Tz;
+                    const bool cn = (dw & 0xff) - 1 >= 0;
+                    if (cn) {  // what the next vertex reads (its depth word is written after the shadow ray)
                         P.rn[j] = rn;
-                        P.depth[j] = depth;
                         P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
                     }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
                     pd.slot[lane] = j;
-                    pd.flag[lane] = (cn ? 1 : 0) | (first ? 2 : 0);
+                    pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
                     pd.v[4 * 64 + lane] = dx; pd.v[5 * 64 + lane] = dy; pd.v[6 * 64 + lane] = dz;
@@ -580,8 +582,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             if (idle && rank < avail) {
                 const int e = pend_lo + rank;
                 s = pd.slot[e];
-                cont = (pd.flag[e] & 1) != 0;
-                fresh = (pd.flag[e] & 2) != 0;
+                vflag = pd.flag[e];
                 scx = pd.v[4 * 64 + e]; scy = pd.v[5 * 64 + e]; scz = pd.v[6 * 64 + e];
                 // origin = the hit point k_extend stored (a cache hit: the shading just read it)
                 trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
@@ -618,18 +619,20 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 dg_occ_leaves += st.clusters - T.l0;
             }
 #endif
-            double lx = 0.0, ly = 0.0, lz = 0.0;  // a first vertex's radiance so far is 0
-            if (!fresh) { lx = P.lx[s]; ly = P.ly[s]; lz = P.lz[s]; }
-            if (!T.B.found) {  // unoccluded: add this vertex's direct-light term
-                lx += scx;
-                ly += scy;
-                lz += scz;
+            const int v = (vflag >> 2) & 15;
+            int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
+            if (!T.B.found && (vflag & 2)) {  // unoccluded: record the vertex's direct term a_v
+                double* va = P.va + (int64_t)(3 * v) * P.vstride + s;
+                va[0] = scx;
+                va[P.vstride] = scy;
+                va[2 * P.vstride] = scz;
+                mask |= 1 << v;
             }
-            const bool store = !T.B.found || fresh;  // the radiance in HBM is stale
-            const bool black = lx == 0.0 && ly == 0.0 && lz == 0.0;
-            if (store && (cont || !black)) { P.lx[s] = lx; P.ly[s] = ly; P.lz[s] = lz; }
-            // continue; or finished: k_resolve adds the radiance (nothing to add: FREE)
-            P.state[s] = cont ? WF_NEED_EXT : (black ? WF_FREE : WF_DONE);
+            const bool cont = (vflag & 1) != 0;
+            // continue with the next vertex's remaining depth; or finished: k_resolve folds the
+            // recorded vertices (none lit: nothing to add, FREE)
+            if (cont || mask) P.depth[s] = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
+            P.state[s] = cont ? WF_NEED_EXT : (mask ? WF_DONE : WF_FREE);
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
@@ -658,7 +661,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
 
 // ------------------------------------------------------------------------------------------------
 // k_resolve: after a generation, every pixel adds its finished paths' radiance in sample order
-// (PixelIntegrator.Sample: color <- color + TraceRay(...), Integrators.fs:169). One thread per
+// (PixelIntegrator.Sample: color <- color + TraceRay(...), Integrators.fs:169). A path's radiance
+// is its recorded vertices folded from the deepest lit one back to the camera: TraceRay returns
+// (l / pdf_li + TraceRay(next)) * col / pdf (Integrators.fs:135-136; pdf = 1, so the division is
+// exact), black below the last lit vertex, and l = 0 at an occluded or unlit one. One thread per
 // tile-ordered pixel position q; for a fixed sample, consecutive q are consecutive slots, so the
 // loads are coalesced. No atomics: one thread owns each pixel, generations are stream-ordered.
 // ------------------------------------------------------------------------------------------------
@@ -681,9 +687,20 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         if (p < P.path_base || p >= end) continue;
         const int64_t j = p - P.path_base;
         if ((P.state[j] & WF_STATE_MASK) == WF_DONE) {
-            ax += P.lx[j];
-            ay += P.ly[j];
-            az += P.lz[j];
+            const int mask = (P.depth[j] >> WF_LIT_SHIFT) & 0xffff;
+            if (mask == 0) continue;  // no lit vertex: the path's radiance is black
+            double fx = 0.0, fy = 0.0, fz = 0.0;  // TraceRay below the deepest lit vertex: Color()
+            for (int v = 31 - __builtin_clz(mask); v >= 0; --v) {
+                const double* va = P.va + (int64_t)(3 * v) * P.vstride + j;
+                const double* vc = P.vc + (int64_t)(3 * v) * P.vstride + j;
+                const bool lit = (mask >> v) & 1;
+                fx = ((lit ? va[0] : 0.0) + fx) * vc[0];
+                fy = ((lit ? va[P.vstride] : 0.0) + fy) * vc[P.vstride];
+                fz = ((lit ? va[2 * P.vstride] : 0.0) + fz) * vc[2 * P.vstride];
+            }
+            ax += fx;
+            ay += fy;
+            az += fz;
         }
     }
     P.accum[pixel] = ax;

@@ -32,6 +32,6 @@ def test_gpu_matches_golden(gpu, name):
         counts = ctx.ray_counts()
         t, prim, _ = ctx.closest_hit(G[f"{name}/rays"])
     ref = G[f"{name}/image"]
-    assert np.abs(img - ref).max() <= 1e-12
+    assert np.array_equal(img, ref), np.abs(img - ref).max()  # bit for bit
     assert np.array_equal(counts[:3], G[f"{name}/counts"][:3])
     assert np.array_equal(t, G[f"{name}/t"]) and np.array_equal(prim, G[f"{name}/prim"])

@@ -73,6 +73,4 @@ def test_soup_image_parity(gpu, oracle, n):
         img = ctx.sample(4)
         counts = ctx.ray_counts()
     assert tuple(counts[:3]) == tuple(st[:3]), (counts[:3], st[:3])
-    diff = np.abs(img[:, :3] - ref[:, :3])
-    assert np.all(np.sqrt((diff ** 2).mean(axis=0)) <= 1e-4)
-    assert diff.max() <= 1e-12 * max(1.0, np.abs(ref).max()), diff.max()
+    assert np.array_equal(img, ref), np.abs(img - ref).max()  # bit for bit

@@ -2,7 +2,7 @@
 
 The oracle renders one sample per pixel of the full frame (all 2.07 M / 8.29 M paths) in a few
 seconds on the host cores, so the comparison is per pixel against the CPU restatement, at a
-non-zero global sample index. At the configs' full sample counts the size-independent
+non-zero global sample index: bit for bit. At the configs' full sample counts the size-independent
 properties are checked instead: the wavefront and megakernel pipelines (independent traversal
 and integrator schedules) produce identical ray counts and images equal up to FP64 summation
 order, and sample partitions (the multi-GPU decomposition) sum to the whole.
@@ -29,10 +29,8 @@ def test_full_frame_one_spp_matches_oracle(gpu, oracle, name):
         img = ctx.accum_read_mean(1.0)
         counts = ctx.ray_counts()
     assert tuple(counts[:3]) == tuple(st[:3]), (counts[:3], st[:3])
-    diff = np.abs(img[:, :3] - ref[:, :3])
-    rmse = np.sqrt((diff ** 2).mean(axis=0))
-    assert np.all(rmse <= 1e-4), rmse  # north_star gate
-    assert diff.max() <= 1e-12 * max(1.0, np.abs(ref).max()), diff.max()
+    # every path's radiance is folded in the reference's recursion order: the frame is the oracle's bit for bit
+    assert np.array_equal(img[:, :3], ref[:, :3]), np.abs(img[:, :3] - ref[:, :3]).max()
 
 
 @pytest.mark.parametrize("name,spp", [("spot", 64), ("cube_cornell", 32), ("renault", 16), ("spot16", 4)])
