@@ -24,7 +24,7 @@ Extra objects on the JSON line:
                 takes the larger share of the step, the other in `other_kernel`) — algorithmic
                 bytes per launch / its HIP-event duration vs HBM 8 TB/s; bytes per ray frozen in
                 profiles/bray_fixture.json; traffic = PMC HBM bytes per launch
-                (profiles/traffic_<scene>.json, scripts/profile_r01.sh)
+                (profiles/traffic_<scene>.json, scripts/profile_traffic.sh)
   render_api    (N = 1) the same workload through Scene.Render's call pattern: the config's spp
                 calls of mfx_render_rgba8(ctx, 1, buf), each with film, post and readback
   cpu_baseline  the CPU oracle timed on this host on a bounded random sample of the same

@@ -129,6 +129,7 @@ struct mfx_ctx {
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     double* d_vscratch = nullptr;    // megakernel: per-lane vertex records [max_depth + 1][6][grid * 256]
+    double* d_albedo = nullptr;      // [nmat][3]
     bool diag_iter = false;
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
@@ -157,7 +158,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->it_ev)
@@ -203,6 +204,7 @@ static int ctx_setup(mfx_ctx* c) {
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
+    CK(upload(&c->d_albedo, c->host.albedo));
     const size_t plane = sizeof(double) * (size_t)c->npix;
     CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
     c->d_accum = c->d_accum_own;
@@ -216,7 +218,8 @@ static int ctx_setup(mfx_ctx* c) {
         size_t mfree = 0, mtotal = 0;
         if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
             const int64_t fit =
-                (int64_t)(mfree / 4 / (WF_DOUBLES_PER_SLOT(c->host.max_depth + 1) * 8 + WF_WORDS_PER_SLOT * 4));
+                (int64_t)(mfree / 4 / (WF_DOUBLES_PER_SLOT(c->host.max_depth + 1) * 8 +
+                                       WF_WORDS_PER_SLOT(c->host.max_depth + 1) * 4));
             c->wf_pool_max = std::max<int64_t>(1 << 20, std::min<int64_t>(c->wf_pool_max, fit));
         }
     }
@@ -406,7 +409,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     c->wf_pool = 0;
     const size_t P = (size_t)pool;
     const int nv = c->host.max_depth + 1;  // vertices per path
-    const size_t bytes = P * (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT * 4) + 64 * 256;
+    const size_t bytes = P * (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4) + 64 * 256;
     hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
@@ -414,8 +417,9 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
     double** dbl[6] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz};
     for (double** d : dbl) *d = (double*)take(P * 8);
-    c->wf.va = (double*)take(P * 8 * 3 * nv);
-    c->wf.vc = (double*)take(P * 8 * 3 * nv);
+    c->wf.vei = (double*)take(P * 8 * nv);
+    c->wf.vls = (double*)take(P * 8 * 2 * nv);
+    c->wf.vmat = (int32_t*)take(P * 4 * nv);
     c->wf.vstride = (int64_t)P;
     c->wf.key = (uint64_t*)take(P * 8);
     c->wf.rn = (uint32_t*)take(P * 4);
@@ -434,6 +438,7 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.light = c->host.light;
     P.cam = c->host.camera;
     P.accum = c->d_accum;
+    P.albedo = c->d_albedo;
 }
 
 // The wavefront pipeline. The frame's path indices (sample-major, 8x8 tiles) are cut into

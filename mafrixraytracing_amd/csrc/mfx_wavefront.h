@@ -11,11 +11,13 @@
 //   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
 //   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (a lit vertex recorded) or FREE (none)
 //   MISS -(k_shadow)-> DONE, or FREE for a camera ray's miss
-// A path's radiance is not summed forward. Each vertex v records its direct term a_v = l / pdf_li
-// and its BRDF factor c_v = col (both FP64 RGB), and k_resolve folds them from the deepest lit
-// vertex back to the camera, acc = (a_v + acc) * c_v, which is the reference's recursion
-// (l / pdf_li + TraceRay(next)) * col / pdf (Integrators.fs:135-136, pdf = 1) in its own
-// operation order: the image is the oracle's bit for bit.
+// A path's radiance is not summed forward. Each vertex v records the operands of its BRDF factor
+// c_v = col (the cosine ei and the material) and, when its shadow ray reaches the light, those of
+// its direct term a_v = l / pdf_li (the cosine cs and the solid-angle factor), and k_resolve
+// rebuilds c_v and a_v with the same FP64 expressions and folds them from the deepest lit vertex
+// back to the camera, acc = (a_v + acc) * c_v: the reference's recursion (l / pdf_li +
+// TraceRay(next)) * col / pdf (Integrators.fs:135-136, pdf = 1) in its own operation order, so the
+// image is the oracle's bit for bit.
 // A HIT state word also carries the hit's shade[] index, so the shading needs no extra lookup.
 // The only atomics are per-wave chunk fetches, spread over WF_SHARDS counters (a returning
 // atomic on one word saturates near 88 per microsecond).
@@ -66,9 +68,11 @@ struct WfParams {
     // path slots (SoA)
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
     double *dx, *dy, *dz;  // ray direction
-    double* va;            // [vertex][channel][stride] direct term a_v = l / pdf_li of a lit vertex
-    double* vc;            // [vertex][channel][stride] BRDF factor c_v = col of every vertex
-    int64_t vstride;       // slots per va / vc row (the allocated pool)
+    double* vei;           // [vertex][stride] the vertex's cosine ei = n . wi (Material.fs:35)
+    int32_t* vmat;         // [vertex][stride] its material (MaterialManager slot)
+    double* vls;           // [vertex][2][stride] a lit vertex's cs = unit . n and solid = |cos_o| A / dist^2
+    int64_t vstride;       // slots per vertex-record row (the allocated pool)
+    const double* albedo;  // [nmat][3] Lambert albedo per material (Material.fs:29-37)
     uint64_t* key;         // RNG key of the path
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)
@@ -94,9 +98,10 @@ struct WfParams {
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
 };
 
-// 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and 6 per vertex (a_v, c_v)
-#define WF_DOUBLES_PER_SLOT(nvert) (7 + 6 * (nvert))
-#define WF_WORDS_PER_SLOT 3     // rn, depth, state
+// 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
+// and the material (4 B)
+#define WF_DOUBLES_PER_SLOT(nvert) (7 + 3 * (nvert))
+#define WF_WORDS_PER_SLOT(nvert) (3 + (nvert))  // rn, depth, state + the vertices' materials
 
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)

@@ -537,20 +537,15 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const double cs = vdot(unit, nm);
                     const int dw = first ? P.max_depth : P.depth[j];  // remaining depth | lit mask << 8
                     const int v = P.max_depth - (dw & 0xff);          // this vertex's index
-                    // col = INVPI * a * ei * TwoPi (Material.fs:36): the vertex's factor c_v
-                    double* vc = P.vc + (int64_t)(3 * v) * P.vstride + j;
-                    vc[0] = TWOPI * (ei * (INVPI * a[0]));
-                    vc[P.vstride] = TWOPI * (ei * (INVPI * a[1]));
-                    vc[2 * P.vstride] = TWOPI * (ei * (INVPI * a[2]));
-                    // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56):
-                    // the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0
-                    double dx = 0.0, dy = 0.0, dz = 0.0;
+                    // the operands of col = INVPI * a * ei * TwoPi (Material.fs:36), c_v (k_resolve)
+                    P.vei[v * P.vstride + j] = ei;
+                    P.vmat[v * P.vstride + j] = sh.material;
+                    (void)a;
+                    // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56)
+                    // is the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0.
+                    // Its operands cs and solid travel with the shadow ray.
                     const bool lightable = cos_o < 0.;
-                    if (lightable) {
-                        dx = (cs * (solid * LT.color[0])) / LT.pdf;
-                        dy = (cs * (solid * LT.color[1])) / LT.pdf;
-                        dz = (cs * (solid * LT.color[2])) / LT.pdf;
-                    }
+                    const double dx = cs, dy = solid, dz = 0.0;
                     // the depth -1 query's result is discarded (Integrators.fs:109): never traced
                     const bool cn = (dw & 0xff) - 1 >= 0;
                     if (cn) {  // what the next vertex reads (its depth word is written after the shadow ray)
@@ -621,11 +616,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
 #endif
             const int v = (vflag >> 2) & 15;
             int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
-            if (!T.B.found && (vflag & 2)) {  // unoccluded: record the vertex's direct term a_v
-                double* va = P.va + (int64_t)(3 * v) * P.vstride + s;
-                va[0] = scx;
-                va[P.vstride] = scy;
-                va[2 * P.vstride] = scz;
+            if (!T.B.found && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
+                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + s;
+                vl[0] = scx;
+                vl[P.vstride] = scy;
                 mask |= 1 << v;
             }
             const bool cont = (vflag & 1) != 0;
@@ -689,14 +683,26 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         if ((P.state[j] & WF_STATE_MASK) == WF_DONE) {
             const int mask = (P.depth[j] >> WF_LIT_SHIFT) & 0xffff;
             if (mask == 0) continue;  // no lit vertex: the path's radiance is black
+            const MfxLight& LT = P.light;
             double fx = 0.0, fy = 0.0, fz = 0.0;  // TraceRay below the deepest lit vertex: Color()
             for (int v = 31 - __builtin_clz(mask); v >= 0; --v) {
-                const double* va = P.va + (int64_t)(3 * v) * P.vstride + j;
-                const double* vc = P.vc + (int64_t)(3 * v) * P.vstride + j;
-                const bool lit = (mask >> v) & 1;
-                fx = ((lit ? va[0] : 0.0) + fx) * vc[0];
-                fy = ((lit ? va[P.vstride] : 0.0) + fy) * vc[P.vstride];
-                fz = ((lit ? va[2 * P.vstride] : 0.0) + fz) * vc[2 * P.vstride];
+                const double ei = P.vei[v * P.vstride + j];
+                const double* al = P.albedo + 3 * P.vmat[v * P.vstride + j];
+                // c_v = col = TwoPi * (ei * (INVPI * a)) (Material.fs:36, the expression k_shadow had)
+                const double cx = TWOPI * (ei * (INVPI * al[0]));
+                const double cy = TWOPI * (ei * (INVPI * al[1]));
+                const double cz = TWOPI * (ei * (INVPI * al[2]));
+                double ax = 0.0, ay = 0.0, az = 0.0;
+                if ((mask >> v) & 1) {  // a_v = (cs * (solid * I)) / pdf_li (Integrators.fs:52, Light.fs:52-53)
+                    const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
+                    const double cs = vl[0], solid = vl[P.vstride];
+                    ax = (cs * (solid * LT.color[0])) / LT.pdf;
+                    ay = (cs * (solid * LT.color[1])) / LT.pdf;
+                    az = (cs * (solid * LT.color[2])) / LT.pdf;
+                }
+                fx = (ax + fx) * cx;
+                fy = (ay + fy) * cy;
+                fz = (az + fz) * cz;
             }
             ax += fx;
             ay += fy;

@@ -3,7 +3,7 @@
 # 1) kernel trace + stats of the bench command; 2) FETCH_SIZE; 3) WRITE_SIZE (separate --pmc
 # passes: the two counters do not fit one TCC pass on gfx950). Then summarise into
 # $OUT/traffic.json (per-kernel HBM bytes per launch, gfx950 FETCH_SIZE correction applied).
-# Usage: scripts/profile_r01.sh TAG [extra bench args...]
+# Usage: scripts/profile_traffic.sh TAG [extra bench args...]
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise a scripts/profile_r01.sh output directory: per-kernel launch count and average
+"""Summarise a scripts/profile_traffic.sh output directory: per-kernel launch count and average
 duration (kernel trace) and HBM bytes per launch from the separate FETCH_SIZE / WRITE_SIZE
 passes. FETCH_SIZE is doubled (MI355X_MICROARCH.md: gfx950 tallies 128-B requests at 64 B);
 WRITE_SIZE is taken as reported (calibrated for 16-B stores and dword atomics; the FP64 pixel
