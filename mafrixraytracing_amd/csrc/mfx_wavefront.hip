@@ -260,10 +260,11 @@ __device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x,
 #define WF_EXT_PEND 128  // k_extend per-wave pending list: slot indices (sign bit: camera ray)
 #define WF_SHD_LIST 128  // k_shadow per-wave shade list entries
 
-// Per-wave LDS list of k_shadow's pending shadow rays: slot index, a flag word and 7 doubles
-// (direction, tmax, the vertex's direct term), each field a 64-entry column (conflict-free).
+// Per-wave LDS list of k_shadow's pending shadow rays: slot index, a flag word and 6 doubles
+// (direction, tmax, the direct term's operands cs and solid), each field a 64-entry column
+// (conflict-free).
 struct PendShd {
-    static constexpr int BYTES = 64 * (4 + 4 + 8 * 7);
+    static constexpr int BYTES = 64 * (4 + 4 + 8 * 6);
     int* slot;
     int* flag;
     double* v;  // v[f * 64 + entry]
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     bool active = false;
     int s = 0;
     Trav T{};
-    double scx = 0.0, scy = 0.0, scz = 0.0;  // this vertex's direct term a_v = l / pdf_li if unoccluded
+    double scs = 0.0, ssolid = 0.0;  // the operands of this vertex's direct term a_v (cs, solid)
     int vflag = 0;  // the lane's vertex: bit 0 the path continues, bit 1 lightable (cos_o < 0),
                     // bits 2..5 its index v, bits 8.. the path's lit mask so far (PD_* below)
     uint32_t c_shadow = 0;
@@ -545,7 +546,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     // is the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0.
                     // Its operands cs and solid travel with the shadow ray.
                     const bool lightable = cos_o < 0.;
-                    const double dx = cs, dy = solid, dz = 0.0;
                     // the depth -1 query's result is discarded (Integrators.fs:109): never traced
                     const bool cn = (dw & 0xff) - 1 >= 0;
                     if (cn) {  // what the next vertex reads (its depth word is written after the shadow ray)
@@ -557,7 +557,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
-                    pd.v[4 * 64 + lane] = dx; pd.v[5 * 64 + lane] = dy; pd.v[6 * 64 + lane] = dz;
+                    pd.v[4 * 64 + lane] = cs; pd.v[5 * 64 + lane] = solid;
                     c_shadow++;
                 }
                 // the unshaded rest of the list moves to its front
@@ -578,7 +578,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 const int e = pend_lo + rank;
                 s = pd.slot[e];
                 vflag = pd.flag[e];
-                scx = pd.v[4 * 64 + e]; scy = pd.v[5 * 64 + e]; scz = pd.v[6 * 64 + e];
+                scs = pd.v[4 * 64 + e]; ssolid = pd.v[5 * 64 + e];
                 // origin = the hit point k_extend stored (a cache hit: the shading just read it)
                 trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            pd.v[3 * 64 + e]);
@@ -618,8 +618,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
             if (!T.B.found && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
                 double* vl = P.vls + (int64_t)(2 * v) * P.vstride + s;
-                vl[0] = scx;
-                vl[P.vstride] = scy;
+                vl[0] = scs;
+                vl[P.vstride] = ssolid;
                 mask |= 1 << v;
             }
             const bool cont = (vflag & 1) != 0;
