@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MFX_ABI_VERSION 2
+#define MFX_ABI_VERSION 3
 #define MFX_MAX_DEVICES 64
 
 /* error codes */
@@ -118,6 +118,26 @@ typedef struct mfx_options {
 #define MFX_F_WAVEFRONT 8   /* always the wavefront pipeline. Default: a call in which a device renders one
                                sample per pixel (Scene.Render) runs the megakernel, which is faster there
                                and gives the same bits (one path per pixel: no summation order) */
+#define MFX_F_FLATTEN 16    /* mfx_create_instanced: flatten every instance into one BVH (no two-level
+                               traversal); the same world scene, hits and images */
+
+/* One entry of an instanced scene (mfx_create_instanced; an extension: the reference has no
+ * instancing, its scenes are flat lists). The world primitive list — the index space Bvh.Build
+ * sorts (BvhNode.fs:25) and every result refers to — is the concatenation, in entry order, of
+ * each entry's copy of template primitives prims[first .. first + count): translated by `offset`
+ * (every vertex, or a sphere's centre, + offset: one FP64 rounding per coordinate), or copied as
+ * they are with MFX_INSTANCE_VERBATIM. Translated entries that share one template range are traced
+ * through one template BVH (two-level traversal); everything else is flattened into the top level.
+ * Results equal those of mfx_create on the expanded list (mfx_expand_instances), bit for bit.   */
+typedef struct mfx_instance {
+    int64_t first;
+    int64_t count;
+    double offset[3];
+    int32_t flags;    /* MFX_INSTANCE_* */
+    int32_t reserved;
+} mfx_instance; /* 48 bytes */
+
+#define MFX_INSTANCE_VERBATIM 1
 
 typedef struct mfx_ctx mfx_ctx;
 
@@ -127,6 +147,24 @@ typedef struct mfx_ctx mfx_ctx;
  * (BvhNode.fs:24-61), the GPU traversal BVH over it, uploads everything to HBM.            */
 int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out);
 void mfx_destroy(mfx_ctx* ctx);
+/* mfx_create for an instanced scene: scene->prims are the template primitives, `instances`
+ * lists the entries whose expansion is the world scene (see mfx_instance).                    */
+int mfx_create_instanced(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                         const mfx_options* opt, mfx_ctx** out);
+/* Host-only: the world primitive list an instanced scene stands for (the library's own
+ * expansion). out may be NULL to query the count; *nout = world primitives.                  */
+int mfx_expand_instances(const mfx_prim* prims, int64_t nprims, const mfx_instance* instances,
+                         int32_t ninstances, mfx_prim* out, int64_t cap, int64_t* nout);
+/* How a context traces instances: out[0] = instances traced two-level, out[1] = template BVHs,
+ * out[2] = top-level BVH4 nodes, out[3] = template BVH4 nodes, out[4] = template slots,
+ * out[5] = top-level slots, out[6] = world slots (what a flat build would hold), out[7] = bytes of
+ * the traversal images (nodes, slots, instance table, per-instance slot records). All 0 but [5..7]
+ * for a flat context.                                                                          */
+int mfx_instancing_info(mfx_ctx* ctx, double out[8]);
+/* Host-only (no device needed): the same figures for a scene built on the host from an instanced
+ * description (MFX_F_FLATTEN honoured), plus the traversal stack bound.                       */
+int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                             int32_t flags, double out[8], int32_t* stack_entries);
 
 /* ---- the reference's render API --------------------------------------------------------- */
 

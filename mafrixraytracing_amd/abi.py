@@ -21,8 +21,10 @@ MFX_F_COUNT_STATS = 1
 MFX_F_MEGAKERNEL = 2
 MFX_F_HOST_BVH = 4
 MFX_F_WAVEFRONT = 8
+MFX_F_FLATTEN = 16
+MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
-MFX_ABI_VERSION = 2
+MFX_ABI_VERSION = 3
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -56,19 +58,37 @@ class MfxOptions(C.Structure):
                 ("ndevices", C.c_int32), ("reserved", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
+class MfxInstance(C.Structure):
+    _fields_ = [("first", C.c_int64), ("count", C.c_int64), ("offset", C.c_double * 3),
+                ("flags", C.c_int32), ("reserved", C.c_int32)]
+
+
 assert C.sizeof(MfxPrim) == 104
+assert C.sizeof(MfxInstance) == 48
 
 # numpy structured dtype with the same layout as mfx_prim (for building big prim arrays fast)
 PRIM_DTYPE = np.dtype([("kind", "<i4"), ("material", "<i4"), ("p", "<f8", (4, 3))], align=True)
 assert PRIM_DTYPE.itemsize == 104
+# mfx_instance: template range, translation, flags
+INSTANCE_DTYPE = np.dtype([("first", "<i8"), ("count", "<i8"), ("offset", "<f8", (3,)), ("flags", "<i4"),
+                           ("reserved", "<i4")], align=True)
+assert INSTANCE_DTYPE.itemsize == 48
 
 
 class SceneArrays:
-    """Owns the numpy buffers an MfxSceneDesc points into (keeps them alive)."""
+    """Owns the numpy buffers an MfxSceneDesc points into (keeps them alive).
+
+    prims is the world primitive list (the reference's flat scene). `instancing`, when given, is
+    (templates, instances): the same world scene as template primitives and mfx_instance entries
+    whose expansion is `prims` (mfx_create_instanced traces it two-level)."""
 
     def __init__(self, prims: np.ndarray, albedo: np.ndarray, light: dict, camera: dict,
-                 width: int, height: int, max_depth: int = 3):
+                 width: int, height: int, max_depth: int = 3, instancing=None):
         self.prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+        self.instancing = None
+        if instancing is not None:
+            self.instancing = (np.ascontiguousarray(instancing[0], dtype=PRIM_DTYPE),
+                               np.ascontiguousarray(instancing[1], dtype=INSTANCE_DTYPE))
         self.albedo = np.ascontiguousarray(albedo, dtype=np.float64).reshape(-1, 3)
         self.light = light
         self.camera = camera
@@ -76,10 +96,12 @@ class SceneArrays:
         self.height = int(height)
         self.max_depth = int(max_depth)
 
-    def desc(self) -> MfxSceneDesc:
+    def desc(self, templates: bool = False) -> MfxSceneDesc:
+        """templates: point at the instancing template primitives instead of the world list."""
         d = MfxSceneDesc()
-        d.prims = self.prims.ctypes.data_as(C.POINTER(MfxPrim))
-        d.nprims = len(self.prims)
+        pr = self.instancing[0] if templates else self.prims
+        d.prims = pr.ctypes.data_as(C.POINTER(MfxPrim))
+        d.nprims = len(pr)
         d.albedo = self.albedo.ctypes.data_as(C.POINTER(C.c_double))
         d.nmat = len(self.albedo)
         d.width, d.height, d.max_depth = self.width, self.height, self.max_depth
@@ -96,7 +118,13 @@ class SceneArrays:
         return d
 
     def with_film(self, width: int, height: int) -> "SceneArrays":
-        return SceneArrays(self.prims, self.albedo, self.light, self.camera, width, height, self.max_depth)
+        return SceneArrays(self.prims, self.albedo, self.light, self.camera, width, height, self.max_depth,
+                           self.instancing)
+
+    def flat(self) -> "SceneArrays":
+        """The same scene without its instancing (the reference's flat primitive list)."""
+        return SceneArrays(self.prims, self.albedo, self.light, self.camera, self.width, self.height,
+                           self.max_depth)
 
 
 _P = C.POINTER
@@ -107,6 +135,12 @@ _ip = _P(C.c_int32)
 def _bind(lib):
     sig = {
         "mfx_create": (C.c_int, [_P(MfxSceneDesc), _P(MfxOptions), _P(C.c_void_p)]),
+        "mfx_create_instanced": (C.c_int, [_P(MfxSceneDesc), _P(MfxInstance), C.c_int32, _P(MfxOptions),
+                                           _P(C.c_void_p)]),
+        "mfx_expand_instances": (C.c_int, [_P(MfxPrim), C.c_int64, _P(MfxInstance), C.c_int32, _P(MfxPrim),
+                                           C.c_int64, _P(C.c_int64)]),
+        "mfx_instancing_info": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_build_instanced_info": (C.c_int, [_P(MfxSceneDesc), _P(MfxInstance), C.c_int32, C.c_int32, _dp, _ip]),
         "mfx_destroy": (None, [C.c_void_p]),
         "mfx_sample": (C.c_int, [C.c_void_p, C.c_int32, _dp]),
         "mfx_render_rgba8": (C.c_int, [C.c_void_p, C.c_int32, _P(C.c_uint8)]),
@@ -143,7 +177,7 @@ def _bind(lib):
 
 
 EXPORTED_SYMBOLS = [
-    "mfx_create", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
+    "mfx_create", "mfx_create_instanced", "mfx_expand_instances", "mfx_instancing_info", "mfx_build_instanced_info", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
     "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
@@ -199,3 +233,36 @@ def build_leaves(arrays: SceneArrays):
     k = int(nl[0])
     return idx, lf[:k], lc[:k], {"clusters": int(info[0]), "nodes": int(info[1]), "stack": int(info[2]),
                                  "slots": int(info[3])}
+
+
+def expand_instances(templates: np.ndarray, instances: np.ndarray) -> np.ndarray:
+    """Host-only: the world primitive list the library derives from an instanced scene."""
+    lib = load_library()
+    t = np.ascontiguousarray(templates, dtype=PRIM_DTYPE)
+    ins = np.ascontiguousarray(instances, dtype=INSTANCE_DTYPE)
+    n = C.c_int64()
+    tp = t.ctypes.data_as(_P(MfxPrim))
+    ip = ins.ctypes.data_as(_P(MfxInstance))
+    check(lib.mfx_expand_instances(tp, len(t), ip, len(ins), None, 0, C.byref(n)), "mfx_expand_instances")
+    out = np.zeros(n.value, dtype=PRIM_DTYPE)
+    check(lib.mfx_expand_instances(tp, len(t), ip, len(ins), out.ctypes.data_as(_P(MfxPrim)), len(out), C.byref(n)),
+          "mfx_expand_instances")
+    return out
+
+
+INSTANCING_KEYS = ("instances", "templates", "top_nodes", "template_nodes", "template_slots", "top_slots",
+                   "world_slots", "image_bytes")
+
+
+def build_instanced_info(arrays: SceneArrays, flags: int = 0) -> dict:
+    """Host-only: how an instanced scene's traversal images come out (no GPU needed)."""
+    lib = load_library()
+    d = arrays.desc(templates=True)
+    ins = arrays.instancing[1]
+    out = np.zeros(8)
+    st = np.zeros(1, dtype=np.int32)
+    check(lib.mfx_build_instanced_info(C.byref(d), ins.ctypes.data_as(_P(MfxInstance)), len(ins), flags, dptr(out),
+                                       iptr(st)), "mfx_build_instanced_info")
+    r = {k: int(v) for k, v in zip(INSTANCING_KEYS, out)}
+    r["stack"] = int(st[0])
+    return r

@@ -89,6 +89,8 @@ struct mfx_ctx {
     int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
+    MfxInstance* d_inst = nullptr;    // two-level scenes only
+    MfxInstSlot* d_meta = nullptr;
     double* d_accum = nullptr;   // [3][npix] (the active accumulator)
     double* d_accum_own = nullptr;
     double* d_film = nullptr;    // [3][npix]
@@ -157,7 +159,7 @@ static void free_ctx(mfx_ctx* c) {
     for (hipEvent_t e : c->peer_done)
         if (e) (void)hipEventDestroy(e);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_meta, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -205,6 +207,11 @@ static int ctx_setup(mfx_ctx* c) {
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
     CK(upload(&c->d_albedo, c->host.albedo));
+    const bool inst = !c->host.inst.empty();
+    if (inst) {
+        CK(upload(&c->d_inst, c->host.inst));
+        CK(upload(&c->d_meta, c->host.meta));
+    }
     const size_t plane = sizeof(double) * (size_t)c->npix;
     CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
     c->d_accum = c->d_accum_own;
@@ -233,7 +240,7 @@ static int ctx_setup(mfx_ctx* c) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, c->device));
     int bpc = 0;
-    CK(mfx_trace_occupancy(c->stack_size, &bpc));
+    CK(mfx_trace_occupancy(c->stack_size, &bpc, inst));
     bpc = std::max(1, std::min(bpc, 8));
     c->grid = prop.multiProcessorCount * bpc;
     // Traversal stacks: the whole bound in LDS unless that costs resident blocks. Measured (C2 / C4
@@ -242,11 +249,11 @@ static int ctx_setup(mfx_ctx* c) {
     // +14 %; when the full stacks already allow k_extend its 4 blocks and k_shadow 3 (C2, C5), the
     // spilling instances' extra stack arithmetic costs more than k_shadow's fourth block gains.
     int ebpc = 0, sbpc = 0;
-    CK(mfx_wf_occupancy(c->stack_size, false, 0, 0, &ebpc, &sbpc));
+    CK(mfx_wf_occupancy(c->stack_size, false, 0, 0, &ebpc, &sbpc, inst));
     c->wf_stack_lds = c->stack_size;
     if (c->stack_size > WF_STACK_LDS) {
         int e2 = 0, s2 = 0;
-        CK(mfx_wf_occupancy(WF_STACK_LDS, true, 0, 0, &e2, &s2));
+        CK(mfx_wf_occupancy(WF_STACK_LDS, true, 0, 0, &e2, &s2, inst));
         if (e2 > ebpc || (sbpc < 3 && s2 > sbpc)) {
             c->wf_stack_lds = WF_STACK_LDS;
             ebpc = e2;
@@ -255,7 +262,7 @@ static int ctx_setup(mfx_ctx* c) {
     }
     if (const char* e = getenv("MFX_STACK_LDS")) {
         c->wf_stack_lds = std::max(1, std::min(c->stack_size, atoi(e)));
-        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, 0, 0, &ebpc, &sbpc));
+        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, 0, 0, &ebpc, &sbpc, inst));
     }
     {  // top BVH nodes in LDS: as many as fit in the LDS the resident blocks leave over
         const bool spill = c->wf_stack_lds < c->stack_size;
@@ -267,7 +274,7 @@ static int ctx_setup(mfx_ctx* c) {
             while (lo < hi) {
                 const int mid = (lo + hi + 1) / 2, ne = k == 0 ? mid : 0, ns = k == 0 ? 0 : mid;
                 int e3 = 0, s3 = 0;
-                CK(mfx_wf_occupancy(c->wf_stack_lds, spill, ne, ns, &e3, &s3));
+                CK(mfx_wf_occupancy(c->wf_stack_lds, spill, ne, ns, &e3, &s3, inst));
                 if ((k == 0 ? e3 : s3) >= want) lo = mid;
                 else hi = mid - 1;
             }
@@ -299,7 +306,8 @@ static int ctx_setup(mfx_ctx* c) {
     return MFX_OK;
 }
 
-int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out) {
+static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                       const mfx_options* opt, mfx_ctx** out) {
     if (!scene || !opt || !out) return fail(MFX_E_INVALID, "mfx_create: null argument");
     *out = nullptr;
     if (opt->part_count < 1 || opt->part_index < 0 || opt->part_index >= opt->part_count)
@@ -319,7 +327,8 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     std::string err;
     // the traversal BVH is built on the first device unless the caller asks for the host build
     // (the same tree either way: tests/test_gpu_build.py); the other devices get copies
-    if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0)) {
+    if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0, instances, ninstances,
+                         (opt->flags & MFX_F_FLATTEN) != 0)) {
         delete c;
         const bool dev = err.rfind("GPU BVH build", 0) == 0;
         return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
@@ -399,6 +408,60 @@ int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** ou
     return MFX_OK;
 }
 
+int mfx_create(const mfx_scene_desc* scene, const mfx_options* opt, mfx_ctx** out) {
+    return create_impl(scene, nullptr, 0, opt, out);
+}
+
+int mfx_create_instanced(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                         const mfx_options* opt, mfx_ctx** out) {
+    if (!instances || ninstances < 1) return fail(MFX_E_INVALID, "mfx_create_instanced: no instances");
+    return create_impl(scene, instances, ninstances, opt, out);
+}
+
+int mfx_expand_instances(const mfx_prim* prims, int64_t nprims, const mfx_instance* instances, int32_t ninstances,
+                         mfx_prim* out, int64_t cap, int64_t* nout) {
+    if (!nout) return fail(MFX_E_INVALID, "mfx_expand_instances: null count");
+    std::vector<mfx_prim> w;
+    std::string err;
+    if (!mfx_expand(prims, nprims, instances, ninstances, w, err)) return fail(MFX_E_INVALID, "mfx_expand_instances: " + err);
+    *nout = (int64_t)w.size();
+    if (out) {
+        if (cap < (int64_t)w.size()) return fail(MFX_E_INVALID, "mfx_expand_instances: output too small");
+        std::copy(w.begin(), w.end(), out);
+    }
+    return MFX_OK;
+}
+
+static void instancing_info(const MfxHostScene& h, double out[8]) {
+    out[0] = (double)h.inst.size();
+    out[1] = h.ntemplates;
+    out[2] = h.inst.empty() ? 0 : h.tlas_nodes;
+    out[3] = h.blas_nodes;
+    out[4] = h.blas_slots;
+    out[5] = (double)(h.slots.size() - MFX_LEAF_SLOTS_MAX) - h.blas_slots;
+    out[6] = h.world_slots;
+    out[7] = (double)(h.nodes.size() * sizeof(MfxNode) + h.slots.size() * sizeof(MfxSlot) +
+                      h.inst.size() * sizeof(MfxInstance) + h.meta.size() * sizeof(MfxInstSlot));
+}
+
+int mfx_instancing_info(mfx_ctx* c, double out[8]) {
+    if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    instancing_info(c->host, out);
+    return MFX_OK;
+}
+
+int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                             int32_t flags, double out[8], int32_t* stack_entries) {
+    if (!out) return fail(MFX_E_INVALID, "null argument");
+    MfxHostScene h;
+    std::string err;
+    if (!mfx_build_scene(scene, h, err, false, instances, ninstances, (flags & MFX_F_FLATTEN) != 0))
+        return fail(MFX_E_INVALID, "mfx_build_instanced_info: " + err);
+    instancing_info(h, out);
+    if (stack_entries) *stack_entries = h.stack_entries;
+    return MFX_OK;
+}
+
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
 // Allocate (or grow) the wavefront path-slot pool (SoA).
@@ -435,6 +498,8 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
+    P.inst = c->d_inst;
+    P.meta = c->d_meta;
     P.light = c->host.light;
     P.cam = c->host.camera;
     P.accum = c->d_accum;
@@ -549,6 +614,8 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
+    P.inst = c->d_inst;
+    P.meta = c->d_meta;
     P.accum = c->d_accum;
     P.work_counter = c->d_work;
     P.counters = c->d_counters;
@@ -839,6 +906,8 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
     Q.slot_ref = c->d_slot_ref;
         Q.ref_blob = c->d_ref_blob;
         Q.shade = c->d_shade;
+        Q.inst = c->d_inst;
+        Q.meta = c->d_meta;
         Q.rays = d_rays;
         Q.tmax_per_ray = d_tmax;
         Q.t_out = d_t;
@@ -909,6 +978,8 @@ int mfx_build_info(mfx_ctx* c, double out[8], uint64_t* digest) {
         mix(h.slot_ref.data(), h.slot_ref.size() * sizeof(int32_t));
         mix(h.ref_blob.data(), h.ref_blob.size());
         mix(h.shade.data(), h.shade.size() * sizeof(MfxShade));
+        mix(h.inst.data(), h.inst.size() * sizeof(MfxInstance));
+        mix(h.meta.data(), h.meta.size() * sizeof(MfxInstSlot));
         *digest = x;
     }
     return MFX_OK;

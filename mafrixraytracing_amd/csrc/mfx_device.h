@@ -13,6 +13,8 @@ struct TraceParams {
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
+    const MfxInstance* inst;         // two-level scenes (null for a flat scene)
+    const MfxInstSlot* meta;
     double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
     unsigned long long* work_counter;
     unsigned long long* counters;    // [8] ray / traversal counters
@@ -34,6 +36,8 @@ struct QueryParams {
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
+    const MfxInstance* inst;
+    const MfxInstSlot* meta;
     const double* rays;
     const double* tmax_per_ray;
     double* t_out;
@@ -46,7 +50,7 @@ struct QueryParams {
 };
 
 hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st);
-hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu);
+hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst = false);
 hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st);
 hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st);
 hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h, double spp, double frame_count,

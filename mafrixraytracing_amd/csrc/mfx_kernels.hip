@@ -28,7 +28,7 @@
 #define MFX_TRACE_MIN_WAVES 1  // __launch_bounds__ 2nd arg: minimum waves per SIMD
 #endif
 
-template <bool STATS>
+template <bool STATS, bool INST>
 __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TraceParams P) {
     // one traversal-stack column per lane in LDS. (The top BVH levels in LDS, as the wavefront
     // kernels keep them, measured -21 % here at 1 spp, r02i: the per-node LDS/global branch.)
@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
     const MfxLight& LT = P.light;
     const MfxCamera& CAM = P.cam;
     const int W = P.width, H = P.height;
@@ -123,7 +123,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
 
         // ---- closest hit: bvh.Hit(ray, 1e-6, 99999999.)  (Integrators.fs:108) ----
         Best hb;
-        const bool hit = traverse<false, STATS>(S, o, d, 1e-6, 99999999., stack, hb, st);
+        const bool hit = traverse<false, STATS, INST>(S, o, d, 1e-6, 99999999., stack, hb, st);
         const double th = hb.t;
         const int slot = hb.info & MFX_INFO_SHADE_MASK;
         if (depth != P.max_depth) c_ext++;
@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
             const bool lightable = cos_o < 0.;
             // SingleDirectLightIntegrator.Eval — Integrators.fs:41-52
             Best sb;
-            const bool occluded = traverse<true, STATS>(S, hp, unit, 1e-6, dist - 1e-6, stack, sb, st2);
+            const bool occluded = traverse<true, STATS, INST>(S, hp, unit, 1e-6, dist - 1e-6, stack, sb, st2);
             c_shadow++;
             if (!occluded && lightable) {  // a_v = l / pdf_li
                 vrec[0] = (cs * (solid * LT.color[0])) / LT.pdf;
@@ -244,17 +244,18 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
 // ----------------------------------------------------------------------------------------------
 // Query kernels (Bvh.Hit on explicit rays)
 // ----------------------------------------------------------------------------------------------
+template <bool INST>
 __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     extern __shared__ int lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, Q.meta};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
-    const bool h = traverse<false, false>(S, o, d, Q.tmin, Q.tmax, stack, B, st);
+    const bool h = traverse<false, false, INST>(S, o, d, Q.tmin, Q.tmax, stack, B, st);
     const double t = B.t;
     const int slot = B.info & MFX_INFO_SHADE_MASK;
     if (h) {
@@ -276,17 +277,18 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     }
 }
 
+template <bool INST>
 __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     extern __shared__ int lds[];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, Q.meta};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
-    Q.occ_out[k] = traverse<true, false>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, B, st) ? 1 : 0;
+    Q.occ_out[k] = traverse<true, false, INST>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, B, st) ? 1 : 0;
 }
 
 // ----------------------------------------------------------------------------------------------
@@ -362,16 +364,20 @@ static size_t trace_lds_bytes(int stack_size) { return (size_t)4 * stack_size * 
 
 hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st) {
     const size_t lds = trace_lds_bytes(P.stack_size);
-    if (stats)
-        hipLaunchKernelGGL(trace_kernel<true>, dim3(grid), dim3(256), lds, st, P);
-    else
-        hipLaunchKernelGGL(trace_kernel<false>, dim3(grid), dim3(256), lds, st, P);
+    if (P.inst) {
+        if (stats) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(grid), dim3(256), lds, st, P);
+        else hipLaunchKernelGGL((trace_kernel<false, true>), dim3(grid), dim3(256), lds, st, P);
+    } else {
+        if (stats) hipLaunchKernelGGL((trace_kernel<true, false>), dim3(grid), dim3(256), lds, st, P);
+        else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(grid), dim3(256), lds, st, P);
+    }
     return hipGetLastError();
 }
 
-hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu) {
+hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst) {
     const size_t lds = trace_lds_bytes(stack_size);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, trace_kernel<false>, 256, lds);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        blocks_per_cu, inst ? (const void*)trace_kernel<false, true> : (const void*)trace_kernel<false, false>, 256, lds);
     // gfx950 allocates LDS in 1,280-byte granules of its 160 KB (the API counts finer ones)
     const size_t g = 1280;
     *blocks_per_cu = std::min(*blocks_per_cu, (int)(160 * 1024 / ((lds + g - 1) / g * g)));
@@ -380,10 +386,14 @@ hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu) {
 
 hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st) {
     const size_t lds = (size_t)4 * Q.stack_size * 64 * sizeof(int);
-    if (shadow)
-        hipLaunchKernelGGL(anyhit_kernel, dim3(grid_for(Q.n, 256)), dim3(256), lds, st, Q);
-    else
-        hipLaunchKernelGGL(closest_kernel, dim3(grid_for(Q.n, 256)), dim3(256), lds, st, Q);
+    const dim3 g(grid_for(Q.n, 256));
+    if (shadow) {
+        if (Q.inst) hipLaunchKernelGGL(anyhit_kernel<true>, g, dim3(256), lds, st, Q);
+        else hipLaunchKernelGGL(anyhit_kernel<false>, g, dim3(256), lds, st, Q);
+    } else {
+        if (Q.inst) hipLaunchKernelGGL(closest_kernel<true>, g, dim3(256), lds, st, Q);
+        else hipLaunchKernelGGL(closest_kernel<false>, g, dim3(256), lds, st, Q);
+    }
     return hipGetLastError();
 }
 

@@ -69,12 +69,42 @@ struct alignas(16) MfxSlot {
 
 // leaf child code: ~((first slot << 3) | (slots - 1)), at most 8 slots (4 primitives, rects take 2)
 #define MFX_LEAF_SLOTS_MAX 8
+#define MFX_SLOTS_MAX (1 << 27)  // leaf codes stay below MFX_INST_FLAG
 
 struct alignas(16) MfxShade {
     double n[3];        // face normal of this triangle slot; a sphere's centre
     double albedo[3];   // MaterialManager[material] flattened to its Lambert albedo (Material.fs:52-68)
     int32_t material;   // MaterialManager slot
     int32_t prim_kind;  // original primitive index (mfx_prim order) << 2 | MFX_KIND_*
+};
+
+// ---- two-level scenes (mfx_create_instanced) ----------------------------------------------------
+// The top-level BVH (nodes[0..)) holds the loose primitives' leaves and, as leaf children, the
+// instances: child = ~(MFX_INST_FLAG | instance). Entering one pushes MFX_INST_EXIT onto the
+// traversal stack, moves the ray's FP32 origin into the template's frame (o - off) and continues at
+// the template BVH's root; popping MFX_INST_EXIT returns to the world frame. Template slots hold the
+// template primitive's own vertices (v0, v1, v2: not edges), so the exact FP64 test rebuilds the
+// world triangle exactly as the host flattened it — v = template + off, then e1 = v1 - v0, e2 =
+// v2 - v0 (Trangle.fs:107-119) — and per (instance, template slot) an MfxInstSlot carries what the
+// world primitive's own slot would: its reference leaf's box, `first`, info and ref_blob offset.
+#define MFX_INST_FLAG (1 << 30)                 // leaf codes stay below it (first slot < 2^27)
+#define MFX_INST_EXIT (~(MFX_INST_FLAG | 0x3ffffffe))  // stack marker: leave the instance
+#define MFX_INST_MAX 0x3ffffffe
+
+struct alignas(16) MfxInstance {
+    double off[3];      // world = template + off, one FP64 rounding per coordinate
+    int32_t root;       // its template BVH's root node
+    int32_t meta_base;  // meta[] index of the instance's first template slot
+    int32_t slot_base;  // slots[] index of the template's first slot
+    int32_t pad;
+};
+
+struct alignas(16) MfxInstSlot {
+    double lo[3], hi[3];  // the world primitive's reference leaf FP64 box
+    int32_t first;        // MfxLeaf.first of that leaf
+    int32_t info;         // MFX_INFO_* of the world slot (its shade[] index, position, kind, rect2)
+    int32_t ref16;        // the leaf's 16-byte offset in ref_blob (whole-leaf evaluation)
+    int32_t pad;
 };
 
 // Quad light = NewAreaLight (Light.fs:31-64): two sample triangles (v0, e1, e2), normal, color.

@@ -228,6 +228,7 @@ struct SahBuilder {
     std::vector<float> cent;    // centroids [3*n]
     std::vector<float> weight;  // intersection cost of an item (slots it tests)
     std::vector<int32_t> ids;   // permutation being partitioned
+    std::vector<char> solo;     // optional: items that must sit alone in a leaf (instances)
     std::vector<std::pair<int, int>> leaves;  // [b, e) ranges of ids, in creation order
     std::vector<Node2>& nodes;
     int max_depth = 0;
@@ -251,7 +252,9 @@ struct SahBuilder {
         if (n == 1) return make_leaf(b, e, out);
         FBox cbox = FBox::empty(), box = FBox::empty();
         float wsum = 0.f;
+        bool any_solo = false;
         for (int i = b; i < e; ++i) {
+            if (!solo.empty() && solo[ids[i]]) any_solo = true;
             FBox p;
             for (int a = 0; a < 3; ++a) p.lo[a] = p.hi[a] = cent[3 * ids[i] + a];
             cbox.grow(p);
@@ -305,7 +308,7 @@ struct SahBuilder {
         }
         // SAH: leaf if testing everything here is no dearer than one more node step plus the split
         const float area = box.area();
-        if (n <= max_leaf && (best_axis < 0 || c_isect * wsum * area <= area + c_isect * best_cost))
+        if (n <= max_leaf && !any_solo && (best_axis < 0 || c_isect * wsum * area <= area + c_isect * best_cost))
             return make_leaf(b, e, out);
         int mid;
         if (best_axis < 0) {
@@ -413,14 +416,192 @@ inline float round_up(double x) {
     return f;
 }
 
+// FP64 box of a primitive in its own coordinates (Trangle.fs:113, Rect.fs:18, Sphere.fs:14-15)
+Box prim_box(const mfx_prim& p) {
+    if (p.kind == MFX_PRIM_SPHERE) {
+        const double r = p.p[1][0];
+        const D3 c = d3(p.p[0]), v{r, r, r};
+        return box2(sub(c, v), add(c, v));
+    }
+    const Box b = tri_box(d3(p.p[0]), d3(p.p[1]), d3(p.p[2]));
+    return p.kind == MFX_PRIM_RECT ? join(b, tri_box(d3(p.p[0]), d3(p.p[2]), d3(p.p[3]))) : b;
+}
+
+// A binned-SAH BVH2 over items (their conservative FP32 boxes, centroids and slot weights), built
+// on the current HIP device (mfx_build.hip: the host builder's tree exactly) or on the host.
+struct Tree {
+    std::vector<Node2> nodes2;
+    std::vector<std::pair<int, int>> leaves;  // [b, e) ranges of ids
+    std::vector<int32_t> ids;
+    int root2 = 0;
+    FBox rootbox;
+    int levels = 0;
+};
+bool build_tree(const std::vector<FBox>& cb, const std::vector<float>& cent, const std::vector<int32_t>& weight,
+                const std::vector<char>* solo, bool gpu, int max_leaf, float c_isect, Tree& t, std::string& err) {
+    const int n = (int)cb.size();
+    t.nodes2.clear();
+    if (gpu && !solo) {
+        std::vector<float> pbox(6 * (size_t)n);
+        for (int i = 0; i < n; ++i)
+            for (int a = 0; a < 3; ++a) {
+                pbox[6 * (size_t)i + a] = cb[i].lo[a];
+                pbox[6 * (size_t)i + 3 + a] = cb[i].hi[a];
+            }
+        MfxBvh2 g;
+        const hipError_t he = mfx_gpu_sah_build(pbox.data(), cent.data(), weight.data(), n, max_leaf, c_isect, g);
+        if (he != hipSuccess) {
+            err = std::string("GPU BVH build: ") + hipGetErrorString(he);
+            return false;
+        }
+        t.nodes2.resize(g.child.size() / 2);
+        for (size_t i = 0; i < t.nodes2.size(); ++i)
+            for (int k = 0; k < 2; ++k) {
+                t.nodes2[i].child[k] = g.child[2 * i + k];
+                for (int a = 0; a < 3; ++a) {
+                    t.nodes2[i].box[k].lo[a] = g.box[(2 * i + k) * 6 + a];
+                    t.nodes2[i].box[k].hi[a] = g.box[(2 * i + k) * 6 + 3 + a];
+                }
+            }
+        t.leaves.clear();
+        for (size_t l = 0; l < g.leaf_b.size(); ++l) t.leaves.emplace_back(g.leaf_b[l], g.leaf_e[l]);
+        t.ids = g.ids;
+        t.root2 = g.root;
+        for (int a = 0; a < 3; ++a) {
+            t.rootbox.lo[a] = g.root_box[a];
+            t.rootbox.hi[a] = g.root_box[3 + a];
+        }
+        t.levels = g.levels;
+        return true;
+    }
+    SahBuilder sb(t.nodes2);
+    sb.max_leaf = max_leaf;
+    sb.c_isect = c_isect;
+    sb.cb = cb;
+    sb.cent = cent;
+    sb.weight.resize(n);
+    sb.ids.resize(n);
+    for (int i = 0; i < n; ++i) {
+        sb.weight[i] = (float)weight[i];
+        sb.ids[i] = i;
+    }
+    if (solo) sb.solo = *solo;
+    t.root2 = sb.build(0, n, 0, t.rootbox);
+    t.levels = sb.max_depth + 1;
+    t.leaves = sb.leaves;
+    t.ids = sb.ids;
+    return true;
+}
+
+// leaves (~child refs) of a BVH4 in depth-first order, children in order
+std::vector<int> dfs_leaves(const std::vector<MfxNode>& nodes, int root) {
+    std::vector<int> order, st{root};
+    while (!st.empty()) {
+        const int ref = st.back();
+        st.pop_back();
+        if (ref < 0) {
+            order.push_back(~ref);
+        } else {
+            for (int k = 3; k >= 0; --k)
+                if (nodes[ref].child[k] != MFX_CHILD_EMPTY) st.push_back(nodes[ref].child[k]);
+        }
+    }
+    return order;
+}
+
 }  // namespace
 
-bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err, bool gpu_bvh) {
+bool mfx_expand(const mfx_prim* prims, int64_t nprims, const mfx_instance* inst, int ninst,
+                std::vector<mfx_prim>& world, std::string& err) {
+    world.clear();
+    if (!prims || nprims < 1 || !inst || ninst < 1) {
+        err = "an instanced scene needs template primitives and at least one instance";
+        return false;
+    }
+    int64_t total = 0;
+    for (int k = 0; k < ninst; ++k) {
+        const mfx_instance& e = inst[k];
+        if (e.first < 0 || e.count < 0 || e.first > nprims || e.count > nprims - e.first) {
+            err = "instance " + std::to_string(k) + " names primitives outside the template array";
+            return false;
+        }
+        if (e.flags & ~MFX_INSTANCE_VERBATIM) {
+            err = "instance " + std::to_string(k) + " has unknown flags";
+            return false;
+        }
+        total += e.count;
+    }
+    if (total < 1 || total > (1 << 28)) {
+        err = total < 1 ? "the instances expand to no primitive" : "too many primitives";
+        return false;
+    }
+    world.reserve((size_t)total);
+    for (int k = 0; k < ninst; ++k) {
+        const mfx_instance& e = inst[k];
+        for (int64_t i = 0; i < e.count; ++i) {
+            mfx_prim p = prims[e.first + i];
+            if (!(e.flags & MFX_INSTANCE_VERBATIM)) {
+                const int nv = p.kind == MFX_PRIM_SPHERE ? 1 : (p.kind == MFX_PRIM_RECT ? 4 : 3);
+                for (int v = 0; v < nv; ++v)
+                    for (int a = 0; a < 3; ++a) p.p[v][a] = p.p[v][a] + e.offset[a];
+            }
+            world.push_back(p);
+        }
+    }
+    return true;
+}
+
+bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err, bool gpu_bvh,
+                     const mfx_instance* instances, int ninstances, bool flatten) {
     using clock = std::chrono::steady_clock;
     const auto t_start = clock::now();
     auto ms_since = [](clock::time_point t0) {
         return std::chrono::duration<double, std::milli>(clock::now() - t0).count();
     };
+    // ---- an instanced scene stands for its expansion (mfx_instance); translated entries that
+    //      share a template range are traced two-level through one template BVH ----------------
+    const mfx_scene_desc* d = d0;
+    mfx_scene_desc dw;
+    std::vector<mfx_prim> world;
+    struct Use {
+        int64_t wbase, count;  // its world primitives
+        double off[3];
+        int tmpl;
+    };
+    std::vector<Use> uses;
+    std::vector<std::pair<int64_t, int64_t>> templates;  // (first, count) in the template array
+    if (instances) {
+        if (!d0) {
+            err = "null scene";
+            return false;
+        }
+        if (!mfx_expand(d0->prims, d0->nprims, instances, ninstances, world, err)) return false;
+        dw = *d0;
+        dw.prims = world.data();
+        dw.nprims = (int64_t)world.size();
+        d = &dw;
+        std::vector<int> uses_of_range(ninstances, 0);
+        for (int k = 0; k < ninstances; ++k)
+            for (int q = 0; q < ninstances; ++q)
+                if (!(instances[q].flags & MFX_INSTANCE_VERBATIM) && instances[q].first == instances[k].first &&
+                    instances[q].count == instances[k].count)
+                    ++uses_of_range[k];
+        int64_t wb = 0;
+        for (int k = 0; k < ninstances; ++k) {
+            const mfx_instance& e = instances[k];
+            if (!flatten && !(e.flags & MFX_INSTANCE_VERBATIM) && e.count > 0 && uses_of_range[k] >= 2) {
+                int tm = 0;
+                while (tm < (int)templates.size() && templates[tm] != std::make_pair(e.first, e.count)) ++tm;
+                if (tm == (int)templates.size()) templates.emplace_back(e.first, e.count);
+                uses.push_back(Use{wb, e.count, {e.offset[0], e.offset[1], e.offset[2]}, tm});
+            }
+            wb += e.count;
+        }
+        if ((int)uses.size() > MFX_INST_MAX) {
+            err = "too many instances";
+            return false;
+        }
+    }
     if (!d || !d->prims || d->nprims < 1) {
         err = "scene has no primitives (Bvh.Build on an empty array throws, BvhNode.fs:26)";
         return false;
@@ -584,7 +765,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
         put(s.light.color, d3(L.intensity));
     }
 
-    // ---- conservative FP32 primitive boxes + SAH BVH2 over primitives ----------------------
+    // ---- conservative FP32 primitive boxes --------------------------------------------------
     double R = 0, T = 0;
     {
         Box all = pb[0];
@@ -596,74 +777,22 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
             for (int a = 0; a < 3; ++a) R = std::max(R, std::fabs(d->light.p[k][a]));
     }
     s.eps = (float)std::ldexp(R + T, -19);
-    std::vector<Node2> nodes2;
-    SahBuilder sb(nodes2);
-    if (const char* e = getenv("MFX_LEAF_MAX")) sb.max_leaf = std::max(1, std::min(4, atoi(e)));
-    if (const char* e = getenv("MFX_SAH_CI")) sb.c_isect = (float)atof(e);
-    sb.cb.resize(n);
-    sb.cent.resize(3 * (size_t)n);
-    sb.weight.resize(n);
-    sb.ids.resize(n);
-    for (int i = 0; i < n; ++i) {
+    int max_leaf = 4;
+    float c_isect = 1.5f;
+    if (const char* e = getenv("MFX_LEAF_MAX")) max_leaf = std::max(1, std::min(4, atoi(e)));
+    if (const char* e = getenv("MFX_SAH_CI")) c_isect = (float)atof(e);
+    auto fbox_of = [&](const Box& b, float eps) {
         FBox f;
         for (int a = 0; a < 3; ++a) {
-            const double lo = comp(pb[i].lo, a), hi = comp(pb[i].hi, a);
-            f.lo[a] = round_down(lo - (double)s.eps);
-            f.hi[a] = round_up(hi + (double)s.eps);
-            sb.cent[3 * i + a] = 0.5f * (f.lo[a] + f.hi[a]);
+            f.lo[a] = round_down(comp(b.lo, a) - (double)eps);
+            f.hi[a] = round_up(comp(b.hi, a) + (double)eps);
         }
-        sb.cb[i] = f;
-        sb.weight[i] = (float)nslot_of[i];
-        sb.ids[i] = i;
-    }
-    FBox rootbox;
-    int root2 = 0;
+        return f;
+    };
     const auto t_bvh = clock::now();
     s.bvh_gpu = gpu_bvh;
-    if (gpu_bvh) {  // the same tree, built breadth-first on the current HIP device (mfx_build.hip)
-        std::vector<float> pbox(6 * (size_t)n);
-        for (int i = 0; i < n; ++i)
-            for (int a = 0; a < 3; ++a) {
-                pbox[6 * (size_t)i + a] = sb.cb[i].lo[a];
-                pbox[6 * (size_t)i + 3 + a] = sb.cb[i].hi[a];
-            }
-        MfxBvh2 g;
-        const hipError_t he = mfx_gpu_sah_build(pbox.data(), sb.cent.data(), nslot_of.data(), n, sb.max_leaf,
-                                                sb.c_isect, g);
-        if (he != hipSuccess) {
-            err = std::string("GPU BVH build: ") + hipGetErrorString(he);
-            return false;
-        }
-        nodes2.resize(g.child.size() / 2);
-        for (size_t i = 0; i < nodes2.size(); ++i)
-            for (int k = 0; k < 2; ++k) {
-                nodes2[i].child[k] = g.child[2 * i + k];
-                for (int a = 0; a < 3; ++a) {
-                    nodes2[i].box[k].lo[a] = g.box[(2 * i + k) * 6 + a];
-                    nodes2[i].box[k].hi[a] = g.box[(2 * i + k) * 6 + 3 + a];
-                }
-            }
-        sb.leaves.clear();
-        for (size_t l = 0; l < g.leaf_b.size(); ++l) sb.leaves.emplace_back(g.leaf_b[l], g.leaf_e[l]);
-        sb.ids = g.ids;
-        root2 = g.root;
-        for (int a = 0; a < 3; ++a) {
-            rootbox.lo[a] = g.root_box[a];
-            rootbox.hi[a] = g.root_box[3 + a];
-        }
-        s.bvh_levels = g.levels;
-    } else {
-        root2 = sb.build(0, n, 0, rootbox);
-        s.bvh_levels = sb.max_depth + 1;
-    }
-    s.ms_bvh = ms_since(t_bvh);
-    s.nodes2 = (int32_t)nodes2.size();
-    s.nodes.clear();
-    Collapse4 c4{nodes2, s.nodes};
-    const int root = c4.run(root2, 0, 0, &rootbox);  // always an internal node (a lone leaf gets a parent)
-    s.bvh_depth = c4.max_depth;
-    s.stack_entries = std::max(1, c4.max_stack);
-    const int nl = (int)sb.leaves.size();
+    s.bvh_levels = 0;
+    s.nodes2 = 0;
 
     // ---- where each primitive sits in the reference grouping --------------------------------
     std::vector<int32_t> ref_leaf_of(n), pos_of(n);
@@ -685,70 +814,262 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
             return false;
         }
     }
+    auto slot_info = [&](int p, int j, int32_t shade) {
+        return shade | (pos_of[p] << MFX_INFO_POS_SHIFT) | (d->prims[p].kind << MFX_INFO_KIND_SHIFT) |
+               (j == 1 ? MFX_INFO_RECT2 : 0);
+    };
 
-    // ---- traversal leaves in depth-first order: runs of slots; child refs become leaf codes ---
-    std::vector<int> order;
-    order.reserve(nl);
-    {
-        std::vector<int> st{root};  // depth-first, children in order
-        while (!st.empty()) {
-            const int ref = st.back();
-            st.pop_back();
-            if (ref < 0) {
-                order.push_back(~ref);
-            } else {
-                for (int k = 3; k >= 0; --k)
-                    if (s.nodes[ref].child[k] != MFX_CHILD_EMPTY) st.push_back(s.nodes[ref].child[k]);
-            }
-        }
-    }
-    std::vector<int32_t> code_of(nl), shade_of(n);
+    // ---- traversal images --------------------------------------------------------------------
+    std::vector<int32_t> shade_of(n, -1);  // shade[] index of each world primitive's first slot
     s.slots.clear();
     s.slot_ref.clear();
     s.shade.clear();
-    for (int l : order) {
-        const int b = sb.leaves[l].first, e = sb.leaves[l].second;
-        const int s0 = (int)s.slots.size();
-        for (int k = b; k < e; ++k) {
-            const int p = sb.ids[k];
-            const MfxLeaf& rl = leaves[ref_leaf_of[p]];
-            shade_of[p] = (int32_t)s.shade.size();
-            for (int j = 0; j < nslot_of[p]; ++j) {
-                MfxSlot sl = pslots[slot_of[p] + j];
-                std::memcpy(sl.lo, rl.lo, sizeof(sl.lo));
-                std::memcpy(sl.hi, rl.hi, sizeof(sl.hi));
-                sl.first = rl.first;
-                sl.info = (int32_t)s.shade.size() | (pos_of[p] << MFX_INFO_POS_SHIFT) |
-                          (d->prims[p].kind << MFX_INFO_KIND_SHIFT) | (j == 1 ? MFX_INFO_RECT2 : 0);
-                s.slots.push_back(sl);
-                s.slot_ref.push_back(ref16[ref_leaf_of[p]]);
-                s.shade.push_back(pshade[slot_of[p] + j]);
-            }
+    s.inst.clear();
+    s.meta.clear();
+    s.tlas_nodes = s.blas_nodes = s.blas_slots = s.ntemplates = 0;
+    // a world primitive's slots at the end of slots[] (the top level / the flat BVH), shade[] in step
+    auto emit_world_prim = [&](int p) {
+        const MfxLeaf& rl = leaves[ref_leaf_of[p]];
+        shade_of[p] = (int32_t)s.shade.size();
+        for (int j = 0; j < nslot_of[p]; ++j) {
+            MfxSlot sl = pslots[slot_of[p] + j];
+            std::memcpy(sl.lo, rl.lo, sizeof(sl.lo));
+            std::memcpy(sl.hi, rl.hi, sizeof(sl.hi));
+            sl.first = rl.first;
+            sl.info = slot_info(p, j, (int32_t)s.shade.size());
+            s.slots.push_back(sl);
+            s.slot_ref.push_back(ref16[ref_leaf_of[p]]);
+            s.shade.push_back(pshade[slot_of[p] + j]);
         }
+    };
+    // a traversal leaf's child code once its slots [s0, slots.size()) are emitted
+    auto leaf_code = [&](int s0, int32_t& code) {
         const int ns = (int)s.slots.size() - s0;
-        if (ns > MFX_LEAF_SLOTS_MAX || s0 >= (1 << 28)) {
+        if (ns > MFX_LEAF_SLOTS_MAX || s0 >= MFX_SLOTS_MAX) {
             err = "scene too large for the traversal image";
             return false;
         }
-        code_of[l] = (s0 << 3) | (ns - 1);
+        code = (s0 << 3) | (ns - 1);
+        return true;
+    };
+    std::vector<int> roots;  // tree roots in nodes[] before renumbering: the top level first
+    if (uses.empty()) {
+        // ---- flat: one SAH BVH2 over the primitives, collapsed to a BVH4 ---------------------
+        std::vector<FBox> cb(n);
+        std::vector<float> cent(3 * (size_t)n);
+        std::vector<int32_t> w(n);
+        for (int i = 0; i < n; ++i) {
+            cb[i] = fbox_of(pb[i], s.eps);
+            for (int a = 0; a < 3; ++a) cent[3 * i + a] = 0.5f * (cb[i].lo[a] + cb[i].hi[a]);
+            w[i] = nslot_of[i];
+        }
+        Tree t;
+        if (!build_tree(cb, cent, w, nullptr, gpu_bvh, max_leaf, c_isect, t, err)) return false;
+        s.bvh_levels = t.levels;
+        s.nodes2 = (int32_t)t.nodes2.size();
+        s.nodes.clear();
+        Collapse4 c4{t.nodes2, s.nodes};
+        const int root = c4.run(t.root2, 0, 0, &t.rootbox);  // always an internal node (a lone leaf gets a parent)
+        s.bvh_depth = c4.max_depth;
+        s.stack_entries = std::max(1, c4.max_stack);
+        std::vector<int32_t> code_of(t.leaves.size());
+        for (int l : dfs_leaves(s.nodes, root)) {
+            const int s0 = (int)s.slots.size();
+            for (int k = t.leaves[l].first; k < t.leaves[l].second; ++k) emit_world_prim(t.ids[k]);
+            if (!leaf_code(s0, code_of[l])) return false;
+        }
+        for (MfxNode& nd : s.nodes)
+            for (int k = 0; k < 4; ++k)
+                if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~code_of[~nd.child[k]];
+        s.ntleaves = (int32_t)t.leaves.size();
+        roots.push_back(root);
+    } else {
+        // ---- two levels: a top-level BVH over the loose primitives and the instances, one
+        //      template BVH per distinct template range (local coordinates) ---------------------
+        const int K = (int)uses.size();
+        std::vector<int> use_of(n, -1);
+        for (int k = 0; k < K; ++k)
+            for (int64_t i = 0; i < uses[k].count; ++i) use_of[uses[k].wbase + i] = k;
+        double offmax = 0;
+        for (const Use& u : uses)
+            for (int a = 0; a < 3; ++a) offmax = std::max(offmax, std::fabs(u.off[a]));
+        // template frame: coordinates and ray origins up to R + |off| in magnitude
+        const float eps_t = (float)std::ldexp(R + offmax + T, -19);
+        // top level: loose primitives (items 0 .. nl-1), then the instances (solo leaves)
+        std::vector<int> loose;
+        for (int i = 0; i < n; ++i)
+            if (use_of[i] < 0) loose.push_back(i);
+        const int nl = (int)loose.size(), ni = nl + K;
+        std::vector<FBox> cb(ni);
+        std::vector<float> cent(3 * (size_t)ni);
+        std::vector<int32_t> w(ni);
+        std::vector<char> solo(ni, 0);
+        for (int i = 0; i < nl; ++i) {
+            cb[i] = fbox_of(pb[loose[i]], s.eps);
+            w[i] = nslot_of[loose[i]];
+        }
+        for (int k = 0; k < K; ++k) {
+            FBox f = FBox::empty();
+            for (int64_t i = 0; i < uses[k].count; ++i) f.grow(fbox_of(pb[uses[k].wbase + i], s.eps));
+            cb[nl + k] = f;
+            w[nl + k] = 8;  // ~ a few node steps and leaves: only steers the top-level SAH
+            solo[nl + k] = 1;
+        }
+        for (int i = 0; i < ni; ++i)
+            for (int a = 0; a < 3; ++a) cent[3 * i + a] = 0.5f * (cb[i].lo[a] + cb[i].hi[a]);
+        Tree tt;
+        if (!build_tree(cb, cent, w, &solo, false, max_leaf, c_isect, tt, err)) return false;
+        std::vector<MfxNode> top;
+        Collapse4 ct{tt.nodes2, top};
+        const int troot = ct.run(tt.root2, 0, 0, &tt.rootbox);
+        std::vector<int32_t> tcode(tt.leaves.size());
+        for (int l : dfs_leaves(top, troot)) {
+            const int b = tt.leaves[l].first, e = tt.leaves[l].second;
+            if (e - b == 1 && tt.ids[b] >= nl) {  // an instance: entered, not tested
+                tcode[l] = MFX_INST_FLAG | (tt.ids[b] - nl);
+                continue;
+            }
+            const int s0 = (int)s.slots.size();
+            for (int k = b; k < e; ++k) emit_world_prim(loose[tt.ids[k]]);
+            if (!leaf_code(s0, tcode[l])) return false;
+        }
+        s.nodes = top;
+        for (MfxNode& nd : s.nodes)
+            for (int k = 0; k < 4; ++k)
+                if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~tcode[~nd.child[k]];
+        s.tlas_nodes = (int32_t)top.size();
+        s.ntleaves = (int32_t)tt.leaves.size();
+        roots.push_back(troot);
+        s.bvh_depth = ct.max_depth;
+        int blas_stack = 0, blas_depth = 0;
+        // template BVHs: slots hold the template's own vertices (the exact test rebuilds the world
+        // triangle from them, mfx_layout.h); tslot[t][i] = first slot of template primitive i
+        std::vector<int> tmpl_root, tmpl_slot_base;
+        std::vector<std::vector<int32_t>> tslot;
+        for (int tm = 0; tm < (int)templates.size(); ++tm) {
+            const int64_t tf = templates[tm].first;
+            const int tn = (int)templates[tm].second;
+            std::vector<FBox> tb(tn);
+            std::vector<float> tc(3 * (size_t)tn);
+            std::vector<int32_t> tw(tn);
+            for (int i = 0; i < tn; ++i) {
+                const mfx_prim& p = d0->prims[tf + i];
+                tb[i] = fbox_of(prim_box(p), eps_t);
+                for (int a = 0; a < 3; ++a) tc[3 * i + a] = 0.5f * (tb[i].lo[a] + tb[i].hi[a]);
+                tw[i] = p.kind == MFX_PRIM_RECT ? 2 : 1;
+            }
+            Tree bt;
+            if (!build_tree(tb, tc, tw, nullptr, gpu_bvh, max_leaf, c_isect, bt, err)) return false;
+            s.bvh_levels = std::max(s.bvh_levels, bt.levels);
+            s.nodes2 += (int32_t)bt.nodes2.size();
+            std::vector<MfxNode> bn;
+            Collapse4 cbv{bt.nodes2, bn};
+            const int broot = cbv.run(bt.root2, 0, 0, &bt.rootbox);
+            blas_stack = std::max(blas_stack, cbv.max_stack);
+            blas_depth = std::max(blas_depth, cbv.max_depth);
+            const int base = (int)s.nodes.size();
+            tmpl_slot_base.push_back((int)s.slots.size());
+            std::vector<int32_t> ts(tn), bcode(bt.leaves.size());
+            for (int l : dfs_leaves(bn, broot)) {
+                const int s0 = (int)s.slots.size();
+                for (int k = bt.leaves[l].first; k < bt.leaves[l].second; ++k) {
+                    const int i = bt.ids[k];
+                    const mfx_prim& p = d0->prims[tf + i];
+                    ts[i] = (int32_t)s.slots.size();
+                    for (int j = 0; j < (p.kind == MFX_PRIM_RECT ? 2 : 1); ++j) {
+                        MfxSlot sl{};
+                        if (p.kind == MFX_PRIM_SPHERE) {
+                            std::memcpy(sl.a, p.p[0], sizeof(sl.a));
+                            sl.b[0] = p.p[1][0];
+                        } else {  // Rect: (v0, v1, v2) then (v0, v2, v3) (Rect.fs:11-20)
+                            std::memcpy(sl.a, p.p[0], sizeof(sl.a));
+                            std::memcpy(sl.b, p.p[j == 0 ? 1 : 2], sizeof(sl.b));
+                            std::memcpy(sl.c, p.p[j == 0 ? 2 : 3], sizeof(sl.c));
+                        }
+                        const int kind = p.kind == MFX_PRIM_TRIANGLE ? MFX_KIND_TRI
+                                         : p.kind == MFX_PRIM_RECT   ? MFX_KIND_RECT
+                                                                     : MFX_KIND_SPHERE;
+                        sl.first = -1;
+                        sl.info = (kind << MFX_INFO_KIND_SHIFT) | (j == 1 ? MFX_INFO_RECT2 : 0);
+                        s.slots.push_back(sl);
+                        s.slot_ref.push_back(0);
+                    }
+                }
+                if (!leaf_code(s0, bcode[l])) return false;
+            }
+            for (MfxNode nd : bn) {
+                for (int k = 0; k < 4; ++k) {
+                    if (nd.child[k] == MFX_CHILD_EMPTY) continue;
+                    nd.child[k] = nd.child[k] >= 0 ? nd.child[k] + base : ~bcode[~nd.child[k]];
+                }
+                s.nodes.push_back(nd);
+            }
+            tmpl_root.push_back(base + broot);
+            roots.push_back(base + broot);
+            tslot.push_back(std::move(ts));
+            s.ntleaves += (int32_t)bt.leaves.size();
+            s.blas_nodes += (int32_t)bn.size();
+        }
+        s.blas_slots = (int32_t)s.slots.size() - tmpl_slot_base[0];
+        s.ntemplates = (int32_t)templates.size();
+        // per instance: its world primitives' shade records (template slot order) and slot records
+        for (int k = 0; k < K; ++k) {
+            const Use& u = uses[k];
+            const int tm = u.tmpl, sb = tmpl_slot_base[tm];
+            const int nts = (tm + 1 < (int)templates.size() ? tmpl_slot_base[tm + 1] : (int)s.slots.size()) - sb;
+            MfxInstance I{};
+            std::memcpy(I.off, u.off, sizeof(I.off));
+            I.root = tmpl_root[tm];
+            I.meta_base = (int32_t)s.meta.size();
+            I.slot_base = sb;
+            const int32_t shade_base = (int32_t)s.shade.size();
+            s.shade.resize(s.shade.size() + nts);
+            s.meta.resize(s.meta.size() + nts);
+            for (int64_t i = 0; i < u.count; ++i) {
+                const int p = (int)(u.wbase + i);
+                const int local = tslot[tm][i] - sb;
+                shade_of[p] = shade_base + local;
+                const MfxLeaf& rl = leaves[ref_leaf_of[p]];
+                for (int j = 0; j < nslot_of[p]; ++j) {
+                    s.shade[shade_base + local + j] = pshade[slot_of[p] + j];
+                    MfxInstSlot& m = s.meta[I.meta_base + local + j];
+                    std::memcpy(m.lo, rl.lo, sizeof(m.lo));
+                    std::memcpy(m.hi, rl.hi, sizeof(m.hi));
+                    m.first = rl.first;
+                    m.info = slot_info(p, j, shade_base + local + j);
+                    m.ref16 = ref16[ref_leaf_of[p]];
+                    m.pad = 0;
+                }
+            }
+            s.inst.push_back(I);
+        }
+        // the top level's pushes before an instance, its exit marker, then the template's own
+        s.stack_entries = std::max(1, ct.max_stack + 1 + blas_stack);
+        s.bvh_depth += blas_depth;
     }
+    s.ms_bvh = ms_since(t_bvh);
     if (s.shade.size() > MFX_INFO_SHADE_MASK) {
         err = "scene too large for the traversal image";
         return false;
     }
     s.slots.resize(s.slots.size() + MFX_LEAF_SLOTS_MAX, MfxSlot{});  // speculative slot loads stay in bounds
-    for (MfxNode& nd : s.nodes)
-        for (int k = 0; k < 4; ++k)
-            if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~code_of[~nd.child[k]];
 
-    // ---- renumber: the first MFX_TOP_NODES nodes breadth-first from the root, then the rest in
-    //      preorder (mfx_layout.h) -----------------------------------------------------------------
+    // ---- renumber: the first MFX_TOP_NODES nodes breadth-first from the root(s) — the top level,
+    //      then the template BVHs' top levels —, then the rest in their order (mfx_layout.h) ------
     {
         const int nn = (int)s.nodes.size();
-        std::vector<int> bfs{root};
-        for (size_t h = 0; h < bfs.size() && (int)bfs.size() < MFX_TOP_NODES; ++h)
+        std::vector<int> bfs{roots[0]};
+        size_t h = 0, next_root = 1;
+        while ((int)bfs.size() < MFX_TOP_NODES) {
+            if (h == bfs.size()) {
+                if (next_root == roots.size()) break;
+                bfs.push_back(roots[next_root++]);
+                continue;
+            }
             for (int k = 0; k < 4 && (int)bfs.size() < MFX_TOP_NODES; ++k)
                 if (s.nodes[bfs[h]].child[k] >= 0) bfs.push_back(s.nodes[bfs[h]].child[k]);
+            ++h;
+        }
         std::vector<int> idx(nn, -1);
         int next = 0;
         for (int v : bfs) idx[v] = next++;
@@ -762,6 +1083,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
             renum[idx[v]] = nd;
         }
         s.nodes.swap(renum);
+        for (MfxInstance& I : s.inst) I.root = idx[I.root];
     }
 
     // ---- reference leaves (heap order): FP64 box header + slot copies ----------------------
@@ -784,7 +1106,7 @@ bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err,
     }
     s.ref_blob.resize(s.ref_blob.size() + 3 * sizeof(MfxSlot), 0);
     s.nclusters = nc;
-    s.ntleaves = nl;
+    s.world_slots = (int32_t)pslots.size();
     s.ms_total = ms_since(t_start);
     return true;
 }

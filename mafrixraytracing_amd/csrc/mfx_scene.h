@@ -17,9 +17,14 @@ struct MfxHostScene {
     std::vector<MfxSlot> slots;     // traversal leaves: runs of MfxSlot records, DFS order
     std::vector<int32_t> slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     std::vector<uint8_t> ref_blob;  // reference leaves: MfxLeaf headers + slot copies, heap order
-    std::vector<MfxShade> shade;    // per traversal slot, in slots[] order
+    std::vector<MfxShade> shade;    // per world slot: top-level / flat slots in slots[] order, then
+                                    // each traced instance's slots in template-slot order
+    std::vector<MfxInstance> inst;  // two-level scenes: instances traced through a template BVH
+    std::vector<MfxInstSlot> meta;  // [instance][template slot]: the world slot's reference-leaf data
     int32_t nclusters = 0;          // reference leaves
     int32_t ntleaves = 0;           // traversal leaves
+    int32_t world_slots = 0;        // slots of the world primitives (what a flat image holds)
+    int32_t tlas_nodes = 0, blas_nodes = 0, blas_slots = 0, ntemplates = 0;  // two-level shape
     std::vector<double> albedo;  // [nmat][3]
     MfxLight light;
     MfxCamera camera;
@@ -36,6 +41,12 @@ struct MfxHostScene {
 
 // Builds everything from the C-ABI scene description; returns false with `err` set on bad input.
 // gpu_bvh: build the traversal BVH2 on the current HIP device (the same tree as the host build).
-bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err, bool gpu_bvh = false);
+// instances (mfx_create_instanced): d->prims are templates, the world scene is their expansion;
+// flatten: trace it through one flat BVH instead of two levels.
+bool mfx_build_scene(const mfx_scene_desc* d, MfxHostScene& s, std::string& err, bool gpu_bvh = false,
+                     const mfx_instance* instances = nullptr, int ninstances = 0, bool flatten = false);
+// The world primitive list of an instanced scene (mfx_instance: template + offset, FP64).
+bool mfx_expand(const mfx_prim* prims, int64_t nprims, const mfx_instance* inst, int ninst,
+                std::vector<mfx_prim>& world, std::string& err);
 
 #endif

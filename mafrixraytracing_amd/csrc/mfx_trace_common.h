@@ -181,6 +181,8 @@ struct SceneView {
     const MfxSlot* __restrict__ slots;     // traversal leaves: runs of MfxSlot records
     const int32_t* __restrict__ slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
+    const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
+    const MfxInstSlot* __restrict__ meta;  // [instance][template slot] reference-leaf data
 };
 
 struct Stats {
@@ -419,6 +421,77 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     return improved;
 }
 
+// One template leaf of instance `inst` (two-level scenes, mfx_layout.h). The world primitive is
+// rebuilt from the template's vertices exactly as the host expanded the scene (mfx_expand: v +
+// off per coordinate) and as the Triangle constructor derives its edges (e1 = v1 - v0, e2 = v2 -
+// v0, Trangle.fs:107-119); a sphere's centre likewise. Everything the reference order and the
+// leaf semantics need — `first`, info, the reference leaf's box and ref_blob offset — is the world
+// slot's, from the instance's MfxInstSlot records, read only for a hit. Otherwise as leaf_hit.
+template <bool SHADOW, bool STATS>
+__device__ __forceinline__ bool leaf_hit_inst(const SceneView& S, int code, int inst, DV o, DV d, double tMin,
+                                              double tMax, Best& B, Stats& st) {
+    const int s0 = code >> 3, n = (code & 7) + 1;
+    const MfxSlot* __restrict__ sl = S.slots + s0;
+    const MfxInstance* __restrict__ I = S.inst + inst;
+    const DV off = ld3(I->off);
+    const MfxInstSlot* __restrict__ meta = S.meta + (I->meta_base + (s0 - I->slot_base));
+    if (STATS) st.clusters++;
+    bool improved = false;
+    for (int k = 0; k < n; ++k) {
+        SlotR r = load_slot(sl + k);
+        const int kind = (r.info >> MFX_INFO_KIND_SHIFT) & 3;
+        if (STATS) st.prims++;
+        double t = 0.0;
+        int hs = k;
+        bool hit;
+        if (kind == MFX_KIND_SPHERE) {
+            r.a = vadd(r.a, off);
+            hit = sphere_hit64(r, o, d, tMin, tMax, t);
+        } else {
+            SlotR w;
+            w.a = vadd(r.a, off);
+            w.b = vsub(vadd(r.b, off), w.a);
+            w.c = vsub(vadd(r.c, off), w.a);
+            hit = tri_hit64(w, o, d, tMin, t);
+            if (kind == MFX_KIND_RECT) {
+                ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
+                if (!hit) {
+                    hs = k;
+                    r = load_slot(sl + k);
+                    w.a = vadd(r.a, off);
+                    w.b = vsub(vadd(r.b, off), w.a);
+                    w.c = vsub(vadd(r.c, off), w.a);
+                    hit = tri_hit64(w, o, d, tMin, t);
+                }
+            }
+        }
+        if (!hit) continue;
+        const MfxInstSlot* __restrict__ m = meta + hs;
+        const int4 fi = *(const int4*)&m->first;  // first, info, ref16
+        if (t >= tMax) {
+            double t2;
+            int info2, first2;
+            if (ref_leaf_hit<SHADOW>(S.ref_blob, fi.z, o, d, tMin, tMax, t2, info2, first2)) {
+                if (SHADOW) return true;
+                if (beats(B, t2, first2, info2)) {
+                    B = Best{t2, info2, first2, true};
+                    improved = true;
+                }
+            }
+            continue;
+        }
+        if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
+        if (!SHADOW && !beats(B, t, fi.x, fi.y)) continue;
+        const double2 bx0 = *(const double2*)m->lo, bx1 = *(const double2*)(m->lo + 2), bx2 = *(const double2*)(m->hi + 1);
+        const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
+        if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
+        if (SHADOW) return true;
+        B = Best{t, fi.y, fi.x, true};
+        improved = true;
+    }
+    return improved;
+}
+
 __device__ __forceinline__ float f_round_up(double x) {
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, __builtin_inff());
@@ -443,6 +516,15 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 }
 
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
+
+// two-level scenes: a node value that enters an instance (~(MFX_INST_FLAG | instance)) or leaves
+// one (MFX_INST_EXIT); leaf codes stay below MFX_INST_FLAG
+__device__ __forceinline__ bool is_inst_code(int node) { return node > MFX_TRAV_EXIT && node <= ~MFX_INST_FLAG; }
+// the FP32 search ray in the frame of instance `inst` (-1: the world): origin o - off
+__device__ __forceinline__ RayF frame_ray(const SceneView& S, int inst, DV o, DV d) {
+    if (inst >= 0) o = vsub(o, ld3(S.inst[inst].off));
+    return make_rayf(o, d);
+}
 
 // A lane's traversal stack. LdsStack: the whole bound in an LDS column (stride 64 dwords:
 // conflict-free). SpillStack: the first `nlds` entries in LDS and deeper ones in a global column
@@ -504,6 +586,27 @@ __device__ __forceinline__ void load_top_nodes(float4* lds, const MfxNode* __res
     const float4* __restrict__ g = (const float4*)nodes;
     for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
     __syncthreads();
+}
+
+// Enter / leave instances until `node` is a node, a leaf or MFX_TRAV_EXIT: entering pushes the
+// exit marker and continues at the template's root in the instance's frame; the marker restores
+// the world frame and pops the next entry. The caller recomputes the FP32 ray (frame_ray).
+template <typename ST>
+__device__ __forceinline__ int inst_switch(const SceneView& S, int node, int& inst, const ST& stack, int& sp) {
+    do {
+        if (node == MFX_INST_EXIT) {
+            inst = -1;
+            if (sp == 0) return MFX_TRAV_EXIT;
+            node = stack.get(sp - 1, stack.deep(sp));
+            --sp;
+        } else {
+            inst = ~node & ~MFX_INST_FLAG;
+            stack.put(sp, MFX_INST_EXIT, stack.deep(sp + 1));
+            ++sp;
+            node = S.inst[inst].root;
+        }
+    } while (is_inst_code(node));
+    return node;
 }
 
 template <bool TOP = false, bool FAR = false, typename ST>
@@ -576,23 +679,32 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
 // (the reference's combine returns a hit iff some visited leaf does). Otherwise: the closest hit
 // under the reference's order (Best). The stack lives in LDS, one column per lane (stride 64
 // dwords: conflict-free).
-template <bool SHADOW, bool STATS>
+// INST: a two-level scene (instances entered and left through inst_switch).
+template <bool SHADOW, bool STATS, bool INST = false>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
                          Best& B, Stats& st) {
     B = Best{tMax, -1, -1, false};
-    const RayF rf = make_rayf(o, d);
+    RayF rf = make_rayf(o, d);
     float tlim = f_round_up(tMax);
     int sp = 0;
     int node = 0;
+    int inst = -1;
+    const LdsStack stk{stack};
     while (true) {
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, LdsStack{stack}, sp);
+            node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
+            if (INST && is_inst_code(node)) {
+                node = inst_switch(S, node, inst, stk, sp);
+                rf = frame_ray(S, inst, o, d);
+            }
         }
         if (node == MFX_TRAV_EXIT) return B.found;
         // ---- leaf ----
-        if (leaf_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, B, st)) {
+        const bool better = (INST && inst >= 0) ? leaf_hit_inst<SHADOW, STATS>(S, ~node, inst, o, d, tMin, tMax, B, st)
+                                                : leaf_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, B, st);
+        if (better) {
             if (SHADOW) {
                 B.found = true;
                 return true;
@@ -601,6 +713,10 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         }
         if (sp == 0) return B.found;
         node = stack[(--sp) * 64];
+        if (INST && is_inst_code(node)) {
+            node = inst_switch(S, node, inst, stk, sp);
+            rf = frame_ray(S, inst, o, d);
+        }
     }
 }
 

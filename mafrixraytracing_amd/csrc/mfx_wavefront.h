@@ -62,6 +62,8 @@ struct WfParams {
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
     const MfxShade* shade;
+    const MfxInstance* inst;  // two-level scenes: instances (null for a flat scene)
+    const MfxInstSlot* meta;  // [instance][template slot] reference-leaf data
     MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
     MfxCamera cam;
     double* accum;  // [3][w*h]
@@ -112,7 +114,7 @@ struct WfParams {
 // resident blocks per CU of each kernel with `stack_lds` stack entries per lane and ntop_* top
 // BVH nodes in LDS
 hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
-                            int* shd_blocks_per_cu);
+                            int* shd_blocks_per_cu, bool inst = false);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

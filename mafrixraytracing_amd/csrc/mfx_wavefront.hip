@@ -189,6 +189,7 @@ struct Trav {
     double tmax64;
     Best B;
     int node, sp;
+    int inst;  // two-level scenes: the instance whose template the lane is in (-1: the world)
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
@@ -198,17 +199,21 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.B = Best{tmax, -1, -1, false};
     T.sp = 0;
     T.node = 0;
+    T.inst = -1;
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
-template <bool SHADOW, bool STATS, typename ST>
+// INST: a two-level scene; a lane enters and leaves instances inside the node loop (inst_switch).
+template <bool SHADOW, bool STATS, bool INST, typename ST>
 __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
                                           DiagAcc& dg, bool diag) {
+    // an instance exit (or entry) popped at the end of the last round
+    if (INST && is_inst_code(T.node)) T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
     // the FP32 ray and the node-test limit are recomputed each round (the same values) rather than
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
-    const RayF rf = make_rayf(T.o, T.d);
+    RayF rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
     const float tlim = f_round_up(T.B.t);  // the query's tMax until the first hit, then the best t
     while (T.node >= 0) {
         if (STATS) st.nodes++;
@@ -217,6 +222,10 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
         T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, rf, tlim, stack, T.sp, tn);
+        if (INST && is_inst_code(T.node)) {
+            T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
+            rf = frame_ray(S, T.inst, T.o, T.d);
+        }
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
         if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
@@ -227,7 +236,10 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 #ifdef MFX_DIAG_OCCLUSION
     if (STATS && !SHADOW && T.B.found) st.after_leaves++;
 #endif
-    if (leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st)) {
+    const bool better = (INST && T.inst >= 0)
+                            ? leaf_hit_inst<SHADOW, STATS>(S, ~T.node, T.inst, T.o, T.d, 1e-6, T.tmax64, T.B, st)
+                            : leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st);
+    if (better) {
         if (SHADOW) {
             T.B.found = true;
             return true;
@@ -278,7 +290,7 @@ struct PendShd {
 // ------------------------------------------------------------------------------------------------
 // k_extend: closest hit for NEED_EXT slots; in a generation's first iteration FREE slots start paths
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool SPILL>
+template <bool STATS, bool SPILL, bool INST>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
@@ -290,7 +302,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds * 64 + lane, P);
     int* pend = lds + 4 * P.stack_lds * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -378,7 +390,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
-        if (active) fin = trav_step<false, STATS>(T, S, stack, tn, st, dg, DG);
+        if (active) fin = trav_step<false, STATS, INST>(T, S, stack, tn, st, dg, DG);
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
             const int fl = fresh ? WF_FRESH : 0;
@@ -418,7 +430,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool SPILL, int WAVES>
+template <bool STATS, bool SPILL, int WAVES, bool INST>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
@@ -431,7 +443,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -603,7 +615,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             fin = true;
         }
 #else
-        if (active) fin = trav_step<true, STATS>(T, S, stack, tn, st, dg, DG);
+        if (active) fin = trav_step<true, STATS, INST>(T, S, stack, tn, st, dg, DG);
 #endif
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
@@ -734,30 +746,44 @@ static int wf_lds_blocks(size_t bytes) {
 }
 
 hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
-                            int* shd_blocks_per_cu) {
+                            int* shd_blocks_per_cu, bool inst) {
     const size_t le = wf_lds_bytes(stack_lds, false, ntop_ext), ls = wf_lds_bytes(stack_lds, true, ntop_shd);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        ext_blocks_per_cu, spill ? k_extend<false, true> : k_extend<false, false>, 256, le);
+    const void* ke = inst ? (spill ? (const void*)k_extend<false, true, true> : (const void*)k_extend<false, false, true>)
+                          : (spill ? (const void*)k_extend<false, true, false> : (const void*)k_extend<false, false, false>);
+    const void* ks = inst ? (spill ? (const void*)k_shadow<false, true, 4, true> : (const void*)k_shadow<false, false, 4, true>)
+                          : (spill ? (const void*)k_shadow<false, true, 4, false> : (const void*)k_shadow<false, false, 4, false>);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, ke, 256, le);
     if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu,
-                                                     spill ? k_shadow<false, true, 4> : k_shadow<false, false, 4>, 256, ls);
+    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, ks, 256, ls);
     *ext_blocks_per_cu = std::min(*ext_blocks_per_cu, wf_lds_blocks(le));
     *shd_blocks_per_cu = std::min(*shd_blocks_per_cu, wf_lds_blocks(ls));
     return e;
 }
 
-template <bool SPILL, int WAVES>
+template <bool SPILL, int WAVES, bool INST>
 static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                              hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
     if (stats)
-        hipLaunchKernelGGL((k_extend<true, SPILL>), dim3(ext_grid), dim3(256), lds_e, st, P);
+        hipLaunchKernelGGL((k_extend<true, SPILL, INST>), dim3(ext_grid), dim3(256), lds_e, st, P);
     else
-        hipLaunchKernelGGL((k_extend<false, SPILL>), dim3(ext_grid), dim3(256), lds_e, st, P);
+        hipLaunchKernelGGL((k_extend<false, SPILL, INST>), dim3(ext_grid), dim3(256), lds_e, st, P);
     if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return;
     if (stats)
-        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES>), dim3(shd_grid), dim3(256), lds_s, st, P);
+        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST>), dim3(shd_grid), dim3(256), lds_s, st, P);
     else
-        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES>), dim3(shd_grid), dim3(256), lds_s, st, P);
+        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(shd_grid), dim3(256), lds_s, st, P);
+}
+
+template <bool INST>
+static void launch_iteration_inst(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
+                                  hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
+    // k_shadow compiled for 3 waves per SIMD (up to 168 VGPRs, no spills) when its LDS allows no
+    // more blocks anyway, else for 4 (128 VGPRs, a few spills)
+    const bool spill = P.stack_lds < P.stack_size, w3 = P.shadow_waves == 3;
+    if (spill && w3) launch_iteration<true, 3, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else if (spill) launch_iteration<true, 4, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else if (w3) launch_iteration<false, 3, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else launch_iteration<false, 4, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
@@ -766,13 +792,8 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     const size_t lds_s = wf_lds_bytes(P.stack_lds, true, P.ntop_shd);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    // k_shadow compiled for 3 waves per SIMD (up to 168 VGPRs, no spills) when its LDS allows no
-    // more blocks anyway, else for 4 (128 VGPRs, a few spills)
-    const bool spill = P.stack_lds < P.stack_size, w3 = P.shadow_waves == 3;
-    if (spill && w3) launch_iteration<true, 3>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else if (spill) launch_iteration<true, 4>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else if (w3) launch_iteration<false, 3>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else launch_iteration<false, 4>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    if (P.inst) launch_iteration_inst<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    else launch_iteration_inst<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from .abi import (MFX_F_NONE, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
+from .abi import (INSTANCING_KEYS, MFX_F_NONE, MfxInstance, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
 
 DEFAULT_SEED = 0x4D414652
 
@@ -19,20 +19,30 @@ class NativeContext:
     """One mfx_ctx: a scene resident in HBM on one GPU."""
 
     def __init__(self, arrays: SceneArrays, seed: int = DEFAULT_SEED, device: int = 0, flags: int = MFX_F_NONE,
-                 part_index: int = 0, part_count: int = 1, devices: list[int] | None = None):
+                 part_index: int = 0, part_count: int = 1, devices: list[int] | None = None,
+                 instancing: bool = True):
         """devices: drive this list of HIP devices from one context (mfx_options.devices; the
-        library's own RCCL reduce sums them into devices[0]); None: the single `device`."""
+        library's own RCCL reduce sums them into devices[0]); None: the single `device`.
+        instancing: a scene with instancing data is created through mfx_create_instanced (two-level
+        traversal; MFX_F_FLATTEN flattens it in the library); False: mfx_create on the world list."""
         self.lib = load_library()
         self.arrays = arrays
         self.w, self.h = arrays.width, arrays.height
-        self._desc = arrays.desc()
+        inst = instancing and arrays.instancing is not None
+        self._desc = arrays.desc(templates=inst)
         self.devices = list(devices) if devices else [device]
         self._devs = (C.c_int32 * len(self.devices))(*self.devices)
         opt = MfxOptions(seed=seed, device=device, flags=flags, part_index=part_index, part_count=part_count,
                          ndevices=len(devices) if devices else 0,
                          devices=C.cast(self._devs, C.POINTER(C.c_int32)) if devices else None)
         h = C.c_void_p()
-        check(self.lib.mfx_create(C.byref(self._desc), C.byref(opt), C.byref(h)), "mfx_create")
+        if inst:
+            self._inst = arrays.instancing[1]
+            ip = self._inst.ctypes.data_as(C.POINTER(MfxInstance))
+            check(self.lib.mfx_create_instanced(C.byref(self._desc), ip, len(self._inst), C.byref(opt), C.byref(h)),
+                  "mfx_create_instanced")
+        else:
+            check(self.lib.mfx_create(C.byref(self._desc), C.byref(opt), C.byref(h)), "mfx_create")
         self._h = h
 
     def close(self):
@@ -158,6 +168,12 @@ class NativeContext:
         return {"ref_bvh_ms": out[0], "bvh_ms": out[1], "scene_ms": out[2], "gpu_bvh": bool(out[3]),
                 "nodes4": int(out[4]), "slots": int(out[5]), "nodes2": int(out[6]), "levels": int(out[7]),
                 "digest": dig.value}
+
+    def instancing_info(self) -> dict:
+        """How instances are traced (mfx_instancing_info): two-level shape and image bytes."""
+        out = np.zeros(8)
+        check(self.lib.mfx_instancing_info(self._h, dptr(out)), "mfx_instancing_info")
+        return {k: int(v) for k, v in zip(INSTANCING_KEYS, out)}
 
     def ref_leaves(self):
         n = len(self.arrays.prims)

@@ -20,7 +20,11 @@ Documented extensions: `vt`/`vn`/`o`/`s` lines are accepted and 
 FParsec grammar as shipped rejects the bundled meshes — SURVEY.md §0.4); a `.npz` mesh
 (converted OBJ, scripts/make_scenes.py) may stand in for an `.obj`; and
 <Shape type="sphere"> adds a Sphere (the reference's scene graph has spheres, Scene.fs:159,
-but no loader produces one).
+but no loader produces one); and <Shape type="instances"> adds translated copies of a group
+(`obj_ref`, `material`, `offsets` = "x,y,z;x,y,z;..."): each copy's vertices (a sphere's centre)
+are the group's + offset in FP64, appended to the shape list like a shapelist per offset, and the
+scene carries that structure as instancing data (mfx_create_instanced). The reference has no
+instancing: its flat list is exactly the expansion, which is what every result refers to.
 """
 from __future__ import annotations
 
@@ -31,7 +35,8 @@ from dataclasses import dataclass, field
 
 import numpy as np
 
-from .abi import MFX_PRIM_RECT, MFX_PRIM_SPHERE, MFX_PRIM_TRIANGLE, PRIM_DTYPE, SceneArrays
+from .abi import (INSTANCE_DTYPE, MFX_INSTANCE_VERBATIM, MFX_PRIM_RECT, MFX_PRIM_SPHERE, MFX_PRIM_TRIANGLE,
+                  PRIM_DTYPE, SceneArrays)
 
 
 class SceneError(ValueError):
@@ -248,20 +253,51 @@ class SceneState:
     height: int
     prims: list
     manager: MaterialManager
+    # <Shape type="instances"> extension: ("verbatim", start, count) / ("instance", key, offset,
+    # start, count) runs of `prims`, and the template primitives per key
+    segments: list = field(default_factory=list)
+    templates: dict = field(default_factory=dict)
 
     def arrays(self, max_depth: int = 3, width: int | None = None, height: int | None = None) -> SceneArrays:
-        prims = np.zeros(len(self.prims), dtype=PRIM_DTYPE)
-        for k, p in enumerate(self.prims):
-            prims[k]["kind"] = p.kind
-            prims[k]["material"] = p.material
-            if p.kind == MFX_PRIM_SPHERE:
-                prims[k]["p"][0] = p.pts[0]
-                prims[k]["p"][1][0] = p.pts[1]
-            else:
-                for i, q in enumerate(p.pts):
-                    prims[k]["p"][i] = q
-        return SceneArrays(prims, self.manager.albedo_table(), self.light, self.camera,
-                           width or self.width, height or self.height, max_depth)
+        inst = None
+        if any(sg[0] == "instance" for sg in self.segments):
+            tmpl, rows, first_of = [], [], {}
+            for sg in self.segments:
+                if sg[0] == "instance":
+                    _, key, off, _start, count = sg
+                    if key not in first_of:
+                        first_of[key] = len(tmpl)
+                        tmpl.extend(self.templates[key])
+                    rows.append((first_of[key], count, off, 0, 0))
+                else:
+                    _, start, count = sg
+                    rows.append((len(tmpl), count, (0.0, 0.0, 0.0), MFX_INSTANCE_VERBATIM, 0))
+                    tmpl.extend(self.prims[start:start + count])
+            inst = (_prim_array(tmpl), np.array(rows, dtype=INSTANCE_DTYPE))
+        return SceneArrays(_prim_array(self.prims), self.manager.albedo_table(), self.light, self.camera,
+                           width or self.width, height or self.height, max_depth, instancing=inst)
+
+
+def _prim_array(plist) -> np.ndarray:
+    prims = np.zeros(len(plist), dtype=PRIM_DTYPE)
+    for k, p in enumerate(plist):
+        prims[k]["kind"] = p.kind
+        prims[k]["material"] = p.material
+        if p.kind == MFX_PRIM_SPHERE:
+            prims[k]["p"][0] = p.pts[0]
+            prims[k]["p"][1][0] = p.pts[1]
+        else:
+            for i, q in enumerate(p.pts):
+                prims[k]["p"][i] = q
+    return prims
+
+
+def translate(p: Prim, off) -> Prim:
+    """A translated copy (the instances extension): every vertex / a sphere's centre + off, FP64."""
+    if p.kind == MFX_PRIM_SPHERE:
+        c = p.pts[0]
+        return Prim(p.kind, ((c[0] + off[0], c[1] + off[1], c[2] + off[2]), p.pts[1]), p.material)
+    return Prim(p.kind, tuple((q[0] + off[0], q[1] + off[1], q[2] + off[2]) for q in p.pts), p.material)
 
 
 def _find_model(ref: str, models: dict):
@@ -382,9 +418,35 @@ def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager 
         xml_mats.append(alb)
     # Shapes (Scene.fs:137-177)
     prims = []
+    segments, templates = [], {}
     sn = nodes.get("Shapes")
     for s in (sn if sn is not None else []):
         t = s.get("type")
+        start = len(prims)
+        if t == "instances":  # extension: translated copies of a group
+            ref, mat, offs = "", 0, []
+            for a in s:
+                nm = a.get("name")
+                if nm == "obj_ref":
+                    ref = a.get("value")
+                elif nm == "material":
+                    mat = int(a.get("value"))
+                elif nm == "offsets":
+                    for o in a.get("value").split(";"):
+                        if o.strip():
+                            parts = o.split(",")
+                            if len(parts) != 3:
+                                raise SceneError(f"instance offset needs 3 floats: {o!r}")
+                            offs.append(tuple(float(x.strip()) for x in parts))
+                else:
+                    raise SceneError(f"unknown instances argument {nm!r}")
+            key = (ref, mat)
+            if key not in templates:
+                templates[key] = [Prim(p.kind, p.pts, mat) for p in _find_model(ref, models)]
+            for off in offs:
+                segments.append(("instance", key, off, len(prims), len(templates[key])))
+                prims.extend(translate(p, off) for p in templates[key])
+            continue
         if t == "shapelist":
             ref, mat = "", 0
             for a in s:
@@ -411,12 +473,14 @@ def InitSceneState(xml_text: str, base_dir: str = ".", manager: MaterialManager 
             prims.append(Prim(MFX_PRIM_SPHERE, (c, r), mat))
         else:
             raise SceneError(f"unknown shape type {t!r}")
+        if len(prims) > start:
+            segments.append(("verbatim", start, len(prims) - start))
     for alb in xml_mats:
         mgr.Add(alb)
     for p in prims:
         if not (0 <= p.material < len(mgr.materials)):
             raise SceneError(f"material index {p.material} out of range (manager has {len(mgr.materials)})")
-    return SceneState(cam, light, w, h, prims, mgr)
+    return SceneState(cam, light, w, h, prims, mgr, segments, templates)
 
 
 def load_scene_file(path: str, fresh_manager: bool = True, light_fallback: str = "debug", **kw) -> SceneArrays:

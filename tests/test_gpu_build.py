@@ -10,7 +10,7 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16"]
+SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced"]
 
 
 def both(a):

@@ -14,7 +14,7 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-FULL = ["spot", "cube_cornell", "renault", "spot16"]  # C2, C3, C4, C5 scenes at their film sizes
+FULL = ["spot", "cube_cornell", "renault", "spot16", "spot16_instanced"]  # C2-C5 at their film sizes (C5 flat and two-level)
 
 
 @pytest.mark.parametrize("name", FULL)

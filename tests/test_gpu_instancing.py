@@ -1,0 +1,145 @@
+"""Two-level traversal of instanced scenes (mfx_create_instanced, row (f3)) against the oracle on
+the flattened world scene: the oracle and the reference know only flat primitive lists, so every
+result — closest hit (t, primitive, normal), occlusion including the leaf quirk, ray counts and
+images — must equal the oracle's on the expansion bit for bit, and equal a flat context's.
+
+The scenes mix triangle soups (exact duplicates: equal-t ties across instances and against loose
+primitives), rects and spheres in the templates, awkward translations (not representable, tiny,
+large, zero), a template used once (flattened into the top level) and verbatim loose primitives.
+The C5 scene itself (spot16_instanced) runs through test_gpu_parity / test_gpu_fullsize.
+"""
+import numpy as np
+import pytest
+
+from conftest import SEED, scene
+from test_gpu_edge_parity import edge_rays
+from test_gpu_parity import random_rays
+
+pytestmark = pytest.mark.gpu
+
+
+def instanced_scene(rng, n_soup=300, w=48, h=27):
+    from mafrixraytracing_amd.abi import (INSTANCE_DTYPE, MFX_INSTANCE_VERBATIM, PRIM_DTYPE, SceneArrays,
+                                          expand_instances)
+    base = scene("cornell", w, h)
+    # template 0: a triangle soup with exact duplicates and flat triangles
+    s = np.zeros(n_soup, dtype=PRIM_DTYPE)
+    v0 = rng.uniform(-0.3, 0.3, size=(n_soup, 3))
+    s["p"][:, 0] = v0
+    s["p"][:, 1] = v0 + rng.uniform(-0.08, 0.08, size=(n_soup, 3))
+    s["p"][:, 2] = v0 + rng.uniform(-0.08, 0.08, size=(n_soup, 3))
+    nd = n_soup // 5
+    s[n_soup - nd:] = s[:nd]
+    flat = rng.random(n_soup) < 0.1
+    s["p"][flat, :, 1] = s["p"][flat, 0:1, 1]
+    s["material"] = rng.integers(0, len(base.albedo), size=n_soup)
+    # template 1: rects and spheres and a few triangles
+    m = np.zeros(7, dtype=PRIM_DTYPE)
+    m["kind"] = [1, 1, 2, 2, 0, 0, 0]
+    m["material"] = rng.integers(0, len(base.albedo), size=7)
+    c = rng.uniform(-0.2, 0.2, size=(7, 3))
+    for k in range(2):  # axis-aligned and tilted quads (v0, v1, v2, v3 in order)
+        u, v = np.eye(3)[k] * 0.25, np.array([0.0, 0.1 * k, 0.25])
+        m["p"][k, :4] = [c[k], c[k] + u, c[k] + u + v, c[k] + v]
+    for k in (2, 3):
+        m["p"][k, 0] = c[k]
+        m["p"][k, 1, 0] = 0.07 + 0.03 * k
+    for k in (4, 5, 6):
+        m["p"][k, :3] = c[k] + rng.uniform(-0.1, 0.1, size=(3, 3))
+    # template 2: used once (flattened into the top level)
+    once = s[:10].copy()
+    T = np.concatenate([s, m, once])
+    loose = base.prims[base.prims["kind"] == 1][:3]  # Cornell walls, verbatim
+    T = np.concatenate([T, loose])
+    offs0 = [(-0.45, 0.55, -0.3), (0.1, 1 / 3, 0.2), (0.45, 1.2, -0.5), (0.0, 0.0, 0.0), (-0.2, 1.5, 0.4)]
+    offs1 = [(0.3, 0.3, 0.1), (-0.35, 1.0, 0.35), (1e-9, 0.7, -1e-9)]
+    rows = [(0, n_soup, o, 0, 0) for o in offs0[:3]]
+    rows += [(n_soup, 7, o, 0, 0) for o in offs1]
+    rows += [(0, n_soup, o, 0, 0) for o in offs0[3:]]
+    rows += [(n_soup + 7, 10, (0.05, 0.9, 0.0), 0, 0)]
+    rows += [(n_soup + 17, len(loose), (0.0, 0.0, 0.0), MFX_INSTANCE_VERBATIM, 0)]
+    I = np.array(rows, dtype=INSTANCE_DTYPE)
+    W = expand_instances(T, I)
+    return SceneArrays(W, base.albedo, base.light, base.camera, w, h, instancing=(T, I))
+
+
+@pytest.mark.parametrize("seed", [11, 12])
+def test_instanced_closest_and_shadow_exact(gpu, oracle, seed):
+    from mafrixraytracing_amd.native import NativeContext
+    rng = np.random.default_rng(seed)
+    a = instanced_scene(rng)
+    rays = np.concatenate([random_rays(a, 12000, rng), edge_rays(4000, rng, grid=False)])
+    o = oracle.OracleScene(a)
+    ot, op, on = o.closest_hit(rays)
+    tmax = rng.uniform(0.05, 3.0, size=len(rays))
+    occ_o = o.any_hit(rays, tmax)
+    with NativeContext(a) as ctx:
+        info = ctx.instancing_info()
+        gt, gp, gn = ctx.closest_hit(rays)
+        occ_g = ctx.any_hit(rays, tmax)
+    assert info["instances"] == 8 and info["templates"] == 2, info
+    assert np.array_equal(gp, op), f"prim mismatch on {(gp != op).sum()} rays"
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gn, on)
+    assert np.array_equal(occ_g, occ_o), f"occlusion mismatch on {(occ_g != occ_o).sum()} rays"
+    assert (op >= 0).mean() > 0.05
+    # hits land in instances, in loose primitives and on duplicates of both
+    n_inst = 3 * 300 + 3 * 7 + 2 * 300
+    assert (op[op >= 0] < n_inst).any() and (op[op >= 0] >= n_inst).any()
+
+
+def test_instanced_images_exact(gpu, oracle):
+    """Wavefront at 4 spp and the one-sample megakernel call against the oracle on the expansion."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = instanced_scene(np.random.default_rng(21))
+    o = oracle.OracleScene(a)
+    ref4, st4 = o.sample(4, SEED, with_stats=True)
+    ref1, st1 = o.sample(1, SEED, sample_base=4, with_stats=True)
+    with NativeContext(a, seed=SEED) as ctx:
+        img4 = ctx.sample(4)
+        c4 = ctx.ray_counts()[:3].copy()
+        img1 = ctx.sample(1)  # continues at global sample 4: the megakernel call
+        c1 = ctx.ray_counts()[:3].copy()
+    assert tuple(c4) == tuple(st4[:3]) and tuple(c1) == tuple(st1[:3])
+    assert np.array_equal(img4, ref4), np.abs(img4 - ref4).max()
+    assert np.array_equal(img1, ref1), np.abs(img1 - ref1).max()
+
+
+def test_instanced_equals_flattened_and_flat(gpu):
+    from mafrixraytracing_amd.abi import MFX_F_FLATTEN, MFX_F_HOST_BVH, MFX_F_NONE
+    from mafrixraytracing_amd.native import NativeContext
+    a = instanced_scene(np.random.default_rng(31), n_soup=2000, w=96, h=54)
+    out = {}
+    for name, kw in {"two-level": dict(flags=MFX_F_NONE), "two-level host": dict(flags=MFX_F_HOST_BVH),
+                     "flattened": dict(flags=MFX_F_FLATTEN), "flat": dict(instancing=False)}.items():
+        with NativeContext(a, seed=SEED, **kw) as ctx:
+            img = ctx.sample(8)
+            out[name] = (img, ctx.ray_counts()[:3].copy(), ctx.build_info()["digest"])
+    ref = out["flat"]
+    for name, (img, cnt, _) in out.items():
+        assert np.array_equal(cnt, ref[1]), (name, cnt, ref[1])
+        assert np.array_equal(img, ref[0]), name
+    assert out["two-level"][2] == out["two-level host"][2]  # the template BVH: GPU build == host build
+    assert out["flattened"][2] == out["flat"][2]             # MFX_F_FLATTEN builds the flat scene's images
+
+
+def test_c5_instanced_full_size_matches_flat(gpu):
+    """C5 at its 4K film: the two-level context against the flat one, 2 spp through the wavefront
+    and one megakernel call, bit for bit, with identical ray counts."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot16_instanced")
+    res = []
+    for inst in (True, False):
+        with NativeContext(a, seed=SEED, instancing=inst) as ctx:
+            ctx.accum_clear()
+            ctx.trace_accumulate(2, 3)
+            img = ctx.accum_read_mean(2.0)
+            cnt = ctx.ray_counts()[:3].copy()
+            ctx.accum_clear()
+            ctx.trace_accumulate(1, 9)
+            res.append((img, cnt, ctx.accum_read_mean(1.0), ctx.ray_counts()[:3].copy()))
+            if inst:
+                assert ctx.instancing_info()["instances"] == 16
+    (i2, c2, m2, k2), (f2, fc2, fm2, fk2) = res
+    assert np.array_equal(c2, fc2) and np.array_equal(k2, fk2)
+    assert np.array_equal(i2, f2) and np.array_equal(m2, fm2)

@@ -1,0 +1,140 @@
+"""Instanced scenes on the host (row (f3); no GPU): the <Shape type="instances"> loader extension,
+the library's own expansion (mfx_expand_instances) and the two-level traversal images
+(mfx_build_instanced_info).
+
+The reference has no instancing: its scenes are flat primitive lists, and the world list an
+instanced scene expands to is what every result refers to. BASELINE.json's C5 ("spot x16
+instanced") is scenes/spot16_instanced.xml — 16 translated copies of spot.default — and must expand
+to exactly the flat scenes/spot16.xml that scripts/make_scenes.py flattened (same FP64 adds), so
+both describe one scene bit for bit.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SCENES
+
+from mafrixraytracing_amd import abi, scene_io
+from mafrixraytracing_amd.abi import INSTANCE_DTYPE, MFX_F_FLATTEN, MFX_INSTANCE_VERBATIM, PRIM_DTYPE
+
+
+@pytest.fixture(scope="module")
+def c5():
+    flat = scene_io.load_scene_file(os.path.join(SCENES, "spot16.xml"))
+    inst = scene_io.load_scene_file(os.path.join(SCENES, "spot16_instanced.xml"))
+    return flat, inst
+
+
+def test_c5_instanced_scene_is_the_flat_scene(c5):
+    flat, inst = c5
+    assert flat.instancing is None and inst.instancing is not None
+    assert inst.prims.tobytes() == flat.prims.tobytes()  # bit for bit, every primitive in order
+    assert np.array_equal(inst.albedo, flat.albedo)
+    assert inst.light == flat.light and inst.camera == flat.camera
+    assert (inst.width, inst.height) == (flat.width, flat.height) == (3840, 2160)
+    T, I = inst.instancing
+    assert len(I) == 17 and (I["count"][:16] == 5856).all() and (I["first"][:16] == 0).all()
+    assert I["flags"][16] == MFX_INSTANCE_VERBATIM  # the stage floor, copied as it is
+
+
+def test_library_expansion_equals_loader(c5):
+    _, inst = c5
+    T, I = inst.instancing
+    assert abi.expand_instances(T, I).tobytes() == inst.prims.tobytes()
+
+
+def mixed_templates(rng):
+    """Triangles, rects and spheres with awkward coordinates."""
+    n = 40
+    p = np.zeros(n, dtype=PRIM_DTYPE)
+    p["kind"] = rng.integers(0, 3, size=n)
+    p["material"] = rng.integers(0, 2, size=n)
+    p["p"] = rng.uniform(-1, 1, size=(n, 4, 3)) / 3.0
+    sph = p["kind"] == 2
+    p["p"][sph, 1, 0] = rng.uniform(0.01, 0.2, size=sph.sum())
+    p["p"][sph, 1, 1:] = 0.0
+    p["p"][sph, 2:] = 0.0
+    p["p"][p["kind"] == 0, 3] = 0.0
+    p["p"][:3, 0, 0] = -0.0
+    return p
+
+
+def test_expansion_is_fp64_translation():
+    rng = np.random.default_rng(7)
+    T = mixed_templates(rng)
+    offs = [(0.1, 1 / 3, -2.7), (1e-300, -0.0, 12345.678), (0.0, 0.0, 0.0), (-1.8, 0.0, 0.9)]
+    rows = [(0, 30, o, 0, 0) for o in offs] + [(30, 10, (5.0, 5.0, 5.0), MFX_INSTANCE_VERBATIM, 0)]
+    I = np.array(rows, dtype=INSTANCE_DTYPE)
+    W = abi.expand_instances(T, I)
+    assert len(W) == 4 * 30 + 10
+    for k, o in enumerate(offs):
+        part = W[30 * k:30 * (k + 1)]
+        for q in range(30):
+            kind = T[q]["kind"]
+            nv = 1 if kind == 2 else (4 if kind == 1 else 3)
+            want = T[q]["p"].copy()
+            want[:nv] = want[:nv] + np.asarray(o)
+            assert part[q]["p"].tobytes() == want.tobytes()
+            assert part[q]["kind"] == kind and part[q]["material"] == T[q]["material"]
+    assert W[120:].tobytes() == T[30:].tobytes()  # verbatim: copied as they are (the offset ignored)
+    # the loader's Python translation makes the same bits
+    for q in range(30):
+        pr = scene_io.Prim(int(T[q]["kind"]), None, 0)
+        if pr.kind == 2:
+            pr.pts = (tuple(T[q]["p"][0]), float(T[q]["p"][1][0]))
+        else:
+            pr.pts = tuple(tuple(v) for v in T[q]["p"][: (4 if pr.kind == 1 else 3)])
+        t = scene_io.translate(pr, offs[0])
+        got = W[q]["p"]
+        if pr.kind == 2:
+            assert np.asarray(t.pts[0]).tobytes() == got[0].tobytes()
+        else:
+            assert np.asarray(t.pts).tobytes() == got[: len(t.pts)].tobytes()
+
+
+@pytest.mark.parametrize("rows,msg", [
+    ([(0, 41, (0, 0, 0), 0, 0)], "outside"),
+    ([(-1, 2, (0, 0, 0), 0, 0)], "outside"),
+    ([(0, 2, (0, 0, 0), 4, 0)], "flags"),
+    ([(0, 0, (0, 0, 0), 0, 0)], "no primitive"),
+])
+def test_expansion_rejects_bad_instances(rows, msg):
+    T = mixed_templates(np.random.default_rng(1))
+    with pytest.raises(abi.MfxError, match=msg):
+        abi.expand_instances(T, np.array(rows, dtype=INSTANCE_DTYPE))
+
+
+def test_c5_two_level_images(c5):
+    flat, inst = c5
+    two = abi.build_instanced_info(inst)
+    one = abi.build_instanced_info(inst, MFX_F_FLATTEN)
+    _, _, _, finfo = abi.build_leaves(flat)
+    assert two["instances"] == 16 and two["templates"] == 1
+    assert two["template_slots"] == 5856 and two["top_slots"] == 2  # spot's triangles once; the floor rect
+    assert two["world_slots"] == one["world_slots"] == 93698
+    assert one["instances"] == 0 and one["top_slots"] == 93698
+    assert finfo["slots"] == 93698 + 8 and finfo["nodes"] == 28263  # MFX_F_FLATTEN == the flat scene's build
+    assert two["image_bytes"] < 0.5 * one["image_bytes"]
+    # the top level's pushes, the instance-exit marker, the template's own bound
+    assert 2 <= two["stack"] <= 48
+
+
+def test_single_use_ranges_are_flattened():
+    rng = np.random.default_rng(3)
+    T = mixed_templates(rng)
+    base = scene_io.load_scene_file(os.path.join(SCENES, "spot.xml"))
+    rows = [(0, 20, (0.5, 0, 0), 0, 0), (0, 20, (-0.5, 0, 0), 0, 0), (20, 20, (0, 1, 0), 0, 0)]
+    I = np.array(rows, dtype=INSTANCE_DTYPE)
+    W = abi.expand_instances(T, I)
+    a = abi.SceneArrays(W, base.albedo, base.light, base.camera, 32, 18, instancing=(T, I))
+    info = abi.build_instanced_info(a)
+    assert info["instances"] == 2 and info["templates"] == 1
+    slots = lambda p: int((p["kind"] == 1).sum()) * 2 + int((p["kind"] != 1).sum())
+    assert info["template_slots"] == slots(T[:20]) and info["top_slots"] == slots(T[20:40])
+
+
+def test_loader_rejects_bad_offsets(tmp_path):
+    text = open(os.path.join(SCENES, "spot16_instanced.xml")).read().replace("-1.8,0.0,-2.7;", "-1.8,0.0;")
+    with pytest.raises(scene_io.SceneError, match="offset"):
+        scene_io.InitSceneState(text, base_dir=SCENES, manager=scene_io.MaterialManager())
