@@ -156,10 +156,10 @@ int mfx_create_instanced(const mfx_scene_desc* scene, const mfx_instance* instan
 int mfx_expand_instances(const mfx_prim* prims, int64_t nprims, const mfx_instance* instances,
                          int32_t ninstances, mfx_prim* out, int64_t cap, int64_t* nout);
 /* How a context traces instances: out[0] = instances traced two-level, out[1] = template BVHs,
- * out[2] = top-level BVH4 nodes, out[3] = template BVH4 nodes, out[4] = template slots,
- * out[5] = top-level slots, out[6] = world slots (what a flat build would hold), out[7] = bytes of
- * the traversal images (nodes, slots, instance table, per-instance slot records). All 0 but [5..7]
- * for a flat context.                                                                          */
+ * out[2] = top-level BVH4 nodes, out[3] = template BVH4 nodes, out[4] = slots per run of the
+ * templates (each traced instance has its own run of world slots), out[5] = top-level slots,
+ * out[6] = world slots, out[7] = bytes of the traversal images (nodes, slots, instance table).
+ * All 0 but [5..7] for a flat context.                                                         */
 int mfx_instancing_info(mfx_ctx* ctx, double out[8]);
 /* Host-only (no device needed): the same figures for a scene built on the host from an instanced
  * description (MFX_F_FLATTEN honoured), plus the traversal stack bound.                       */

@@ -90,7 +90,6 @@ struct mfx_ctx {
     uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
     MfxInstance* d_inst = nullptr;    // two-level scenes only
-    MfxInstSlot* d_meta = nullptr;
     double* d_accum = nullptr;   // [3][npix] (the active accumulator)
     double* d_accum_own = nullptr;
     double* d_film = nullptr;    // [3][npix]
@@ -126,7 +125,7 @@ struct mfx_ctx {
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
-    int wf_stack_lds = 1;            // traversal stack entries per lane in LDS (the rest spill)
+    int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
@@ -159,7 +158,7 @@ static void free_ctx(mfx_ctx* c) {
     for (hipEvent_t e : c->peer_done)
         if (e) (void)hipEventDestroy(e);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_meta, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -208,9 +207,9 @@ static int ctx_setup(mfx_ctx* c) {
     CK(upload(&c->d_shade, c->host.shade));
     CK(upload(&c->d_albedo, c->host.albedo));
     const bool inst = !c->host.inst.empty();
+    const int ninst = (int)c->host.inst.size();
     if (inst) {
         CK(upload(&c->d_inst, c->host.inst));
-        CK(upload(&c->d_meta, c->host.meta));
     }
     const size_t plane = sizeof(double) * (size_t)c->npix;
     CK(hipMalloc((void**)&c->d_accum_own, 3 * plane));
@@ -243,42 +242,62 @@ static int ctx_setup(mfx_ctx* c) {
     CK(mfx_trace_occupancy(c->stack_size, &bpc, inst));
     bpc = std::max(1, std::min(bpc, 8));
     c->grid = prop.multiProcessorCount * bpc;
-    // Traversal stacks: the whole bound in LDS unless that costs resident blocks. Measured (C2 / C4
-    // / C5): with a deep BVH (C4's bound is 44 entries: k_extend 3 and k_shadow 2 blocks per CU) the
-    // first WF_STACK_LDS entries in LDS and the rest spilled (the kernels' SPILL instances) is
-    // +14 %; when the full stacks already allow k_extend its 4 blocks and k_shadow 3 (C2, C5), the
-    // spilling instances' extra stack arithmetic costs more than k_shadow's fourth block gains.
+    // Traversal stacks, per kernel: the whole bound in LDS unless that costs resident blocks; then
+    // the largest LDS share that keeps them, the deeper entries spilled to a global column (the
+    // kernels' SPILL instances). Measured: with a deep BVH (C4's bound is 44 entries: k_extend 3 and
+    // k_shadow 2 blocks per CU with full stacks) spilling is +14 %; where the full stacks allow
+    // k_extend its 4 blocks and k_shadow 3 (C2, flat C5), k_shadow's fourth block with the largest
+    // share that keeps it is +2 % (C2, C5) to +4 % (C4) (r02y: 16 entries, the round-1 rule, gained
+    // nothing there).
     int ebpc = 0, sbpc = 0;
-    CK(mfx_wf_occupancy(c->stack_size, false, 0, 0, &ebpc, &sbpc, inst));
-    c->wf_stack_lds = c->stack_size;
-    if (c->stack_size > WF_STACK_LDS) {
-        int e2 = 0, s2 = 0;
-        CK(mfx_wf_occupancy(WF_STACK_LDS, true, 0, 0, &e2, &s2, inst));
-        if (e2 > ebpc || (sbpc < 3 && s2 > sbpc)) {
-            c->wf_stack_lds = WF_STACK_LDS;
-            ebpc = e2;
-            sbpc = s2;
+    const int shd_target_max = getenv("MFX_SHADOW_TARGET_BLOCKS") ? atoi(getenv("MFX_SHADOW_TARGET_BLOCKS")) : 8;
+    for (int k = 0; k < 2; ++k) {
+        const bool shd = k == 1;
+        int full = 0;
+        CK(mfx_wf_kernel_occupancy(shd, c->stack_size, false, 0, ninst, &full));
+        int nlds = c->stack_size, blocks = full;
+        if (c->stack_size > WF_STACK_LDS) {
+            int b16 = 0;
+            CK(mfx_wf_kernel_occupancy(shd, WF_STACK_LDS, true, 0, ninst, &b16));
+            const int target = shd ? std::max(full, std::min(shd_target_max, b16)) : b16;
+            if (full < target) {
+                int lo = WF_STACK_LDS, hi = c->stack_size - 1;  // blocks only fall as the share grows
+                while (lo < hi) {
+                    const int mid = (lo + hi + 1) / 2;
+                    int b = 0;
+                    CK(mfx_wf_kernel_occupancy(shd, mid, true, 0, ninst, &b));
+                    if (b >= target) lo = mid;
+                    else hi = mid - 1;
+                }
+                nlds = lo;
+                CK(mfx_wf_kernel_occupancy(shd, nlds, true, 0, ninst, &blocks));
+            }
+            if (c->diag_iter)
+                fprintf(stderr, "wavefront: %s blocks/CU: full %d-entry stacks %d, %d in LDS %d; chosen %d in LDS, %d\n",
+                        shd ? "k_shadow" : "k_extend", c->stack_size, full, WF_STACK_LDS, b16, nlds, blocks);
         }
-    }
-    if (const char* e = getenv("MFX_STACK_LDS")) {
-        c->wf_stack_lds = std::max(1, std::min(c->stack_size, atoi(e)));
-        CK(mfx_wf_occupancy(c->wf_stack_lds, c->wf_stack_lds < c->stack_size, 0, 0, &ebpc, &sbpc, inst));
+        if (const char* e = getenv("MFX_STACK_LDS")) {
+            nlds = std::max(1, std::min(c->stack_size, atoi(e)));
+            CK(mfx_wf_kernel_occupancy(shd, nlds, nlds < c->stack_size, 0, ninst, &blocks));
+        }
+        (shd ? c->wf_stack_lds_shd : c->wf_stack_lds_ext) = nlds;
+        (shd ? sbpc : ebpc) = blocks;
     }
     {  // top BVH nodes in LDS: as many as fit in the LDS the resident blocks leave over
-        const bool spill = c->wf_stack_lds < c->stack_size;
         int cap = std::min((int)c->host.nodes.size(), WF_NTOP_MAX);
         if (const char* e = getenv("MFX_NTOP")) cap = std::max(0, std::min(cap, atoi(e)));
         for (int k = 0; k < 2; ++k) {
-            const int want = k == 0 ? ebpc : sbpc;
+            const bool shd = k == 1;
+            const int nlds = shd ? c->wf_stack_lds_shd : c->wf_stack_lds_ext, want = shd ? sbpc : ebpc;
             int lo = 0, hi = cap;  // resident blocks do not grow with ntop: bisect the largest that keeps them
             while (lo < hi) {
-                const int mid = (lo + hi + 1) / 2, ne = k == 0 ? mid : 0, ns = k == 0 ? 0 : mid;
-                int e3 = 0, s3 = 0;
-                CK(mfx_wf_occupancy(c->wf_stack_lds, spill, ne, ns, &e3, &s3, inst));
-                if ((k == 0 ? e3 : s3) >= want) lo = mid;
+                const int mid = (lo + hi + 1) / 2;
+                int b = 0;
+                CK(mfx_wf_kernel_occupancy(shd, nlds, nlds < c->stack_size, mid, ninst, &b));
+                if (b >= want) lo = mid;
                 else hi = mid - 1;
             }
-            (k == 0 ? c->wf_ntop_ext : c->wf_ntop_shd) = lo;
+            (shd ? c->wf_ntop_shd : c->wf_ntop_ext) = lo;
         }
         // k_shadow with at most 3 resident blocks per CU (its LDS) runs the instance compiled for 3
         // waves per SIMD: more registers, no spills (C2 / C5 +2 %); with 4 it keeps the 4-wave one
@@ -287,9 +306,10 @@ static int ctx_setup(mfx_ctx* c) {
         if (c->wf_shadow_waves == 3) sbpc = std::min(sbpc, 3);
         if (c->diag_iter)
             fprintf(stderr,
-                    "wavefront: stack %d/%d in LDS, blocks/CU extend %d shadow %d (%d-wave build), top nodes in LDS "
-                    "%d / %d\n",
-                    c->wf_stack_lds, c->stack_size, ebpc, sbpc, c->wf_shadow_waves, c->wf_ntop_ext, c->wf_ntop_shd);
+                    "wavefront: stack %d/%d (extend) %d/%d (shadow) in LDS, blocks/CU extend %d shadow %d (%d-wave "
+                    "build), top nodes in LDS %d / %d\n",
+                    c->wf_stack_lds_ext, c->stack_size, c->wf_stack_lds_shd, c->stack_size, ebpc, sbpc,
+                    c->wf_shadow_waves, c->wf_ntop_ext, c->wf_ntop_shd);
     }
     if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
         ebpc = std::min(ebpc, std::max(1, atoi(b)));
@@ -299,7 +319,8 @@ static int ctx_setup(mfx_ctx* c) {
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
     {  // deep traversal-stack entries of every lane of the larger grid
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
-        CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, c->stack_size - c->wf_stack_lds)));
+        const int deep = c->stack_size - std::min(c->wf_stack_lds_ext, c->wf_stack_lds_shd);
+        CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, deep)));
     }
     CK(hipMalloc((void**)&c->d_vscratch, sizeof(double) * 6 * (size_t)(c->host.max_depth + 1) * c->grid * 256));
 #undef CK
@@ -438,10 +459,10 @@ static void instancing_info(const MfxHostScene& h, double out[8]) {
     out[2] = h.inst.empty() ? 0 : h.tlas_nodes;
     out[3] = h.blas_nodes;
     out[4] = h.blas_slots;
-    out[5] = (double)(h.slots.size() - MFX_LEAF_SLOTS_MAX) - h.blas_slots;
+    out[5] = h.top_slots;
     out[6] = h.world_slots;
     out[7] = (double)(h.nodes.size() * sizeof(MfxNode) + h.slots.size() * sizeof(MfxSlot) +
-                      h.inst.size() * sizeof(MfxInstance) + h.meta.size() * sizeof(MfxInstSlot));
+                      h.inst.size() * sizeof(MfxInstance));
 }
 
 int mfx_instancing_info(mfx_ctx* c, double out[8]) {
@@ -499,7 +520,6 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.inst = c->d_inst;
-    P.meta = c->d_meta;
     P.light = c->host.light;
     P.cam = c->host.camera;
     P.accum = c->d_accum;
@@ -532,10 +552,12 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.height = H;
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
-    P.stack_lds = c->wf_stack_lds;
+    P.stack_lds_ext = c->wf_stack_lds_ext;
+    P.stack_lds_shd = c->wf_stack_lds_shd;
     P.ntop_ext = c->wf_ntop_ext;
     P.ntop_shd = c->wf_ntop_shd;
     P.shadow_waves = c->wf_shadow_waves;
+    P.ninst_lds = std::min<int>((int)c->host.inst.size(), WF_INST_LDS);
     P.spill = c->d_spill;
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
@@ -615,7 +637,6 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.ref_blob = c->d_ref_blob;
     P.shade = c->d_shade;
     P.inst = c->d_inst;
-    P.meta = c->d_meta;
     P.accum = c->d_accum;
     P.work_counter = c->d_work;
     P.counters = c->d_counters;
@@ -907,7 +928,6 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         Q.ref_blob = c->d_ref_blob;
         Q.shade = c->d_shade;
         Q.inst = c->d_inst;
-        Q.meta = c->d_meta;
         Q.rays = d_rays;
         Q.tmax_per_ray = d_tmax;
         Q.t_out = d_t;
@@ -979,7 +999,6 @@ int mfx_build_info(mfx_ctx* c, double out[8], uint64_t* digest) {
         mix(h.ref_blob.data(), h.ref_blob.size());
         mix(h.shade.data(), h.shade.size() * sizeof(MfxShade));
         mix(h.inst.data(), h.inst.size() * sizeof(MfxInstance));
-        mix(h.meta.data(), h.meta.size() * sizeof(MfxInstSlot));
         *digest = x;
     }
     return MFX_OK;

@@ -14,7 +14,6 @@ struct TraceParams {
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const MfxInstance* inst;         // two-level scenes (null for a flat scene)
-    const MfxInstSlot* meta;
     double* accum;                   // [3][w*h] FP64 radiance sums, x-major pixels
     unsigned long long* work_counter;
     unsigned long long* counters;    // [8] ray / traversal counters
@@ -37,7 +36,6 @@ struct QueryParams {
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const MfxInstance* inst;
-    const MfxInstSlot* meta;
     const double* rays;
     const double* tmax_per_ray;
     double* t_out;

@@ -36,7 +36,7 @@ __global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TracePa
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
     const MfxLight& LT = P.light;
     const MfxCamera& CAM = P.cam;
     const int W = P.width, H = P.height;
@@ -251,7 +251,7 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, Q.meta};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
@@ -284,7 +284,7 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, Q.meta};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};

@@ -82,11 +82,11 @@ struct alignas(16) MfxShade {
 // The top-level BVH (nodes[0..)) holds the loose primitives' leaves and, as leaf children, the
 // instances: child = ~(MFX_INST_FLAG | instance). Entering one pushes MFX_INST_EXIT onto the
 // traversal stack, moves the ray's FP32 origin into the template's frame (o - off) and continues at
-// the template BVH's root; popping MFX_INST_EXIT returns to the world frame. Template slots hold the
-// template primitive's own vertices (v0, v1, v2: not edges), so the exact FP64 test rebuilds the
-// world triangle exactly as the host flattened it — v = template + off, then e1 = v1 - v0, e2 =
-// v2 - v0 (Trangle.fs:107-119) — and per (instance, template slot) an MfxInstSlot carries what the
-// world primitive's own slot would: its reference leaf's box, `first`, info and ref_blob offset.
+// the template BVH's root, whose boxes are the template primitives' (local coordinates); popping
+// MFX_INST_EXIT returns to the world frame. The template BVH is shared; its leaf codes count slots
+// from the instance's own run of world slots (slot_base), which hold the world primitives exactly
+// as a flat image does (FP64 geometry of the expansion, reference-leaf box, `first`, info), so a
+// template leaf is tested by the same exact leaf test at a per-instance slot base.
 #define MFX_INST_FLAG (1 << 30)                 // leaf codes stay below it (first slot < 2^27)
 #define MFX_INST_EXIT (~(MFX_INST_FLAG | 0x3ffffffe))  // stack marker: leave the instance
 #define MFX_INST_MAX 0x3ffffffe
@@ -94,17 +94,8 @@ struct alignas(16) MfxShade {
 struct alignas(16) MfxInstance {
     double off[3];      // world = template + off, one FP64 rounding per coordinate
     int32_t root;       // its template BVH's root node
-    int32_t meta_base;  // meta[] index of the instance's first template slot
-    int32_t slot_base;  // slots[] index of the template's first slot
-    int32_t pad;
-};
-
-struct alignas(16) MfxInstSlot {
-    double lo[3], hi[3];  // the world primitive's reference leaf FP64 box
-    int32_t first;        // MfxLeaf.first of that leaf
-    int32_t info;         // MFX_INFO_* of the world slot (its shade[] index, position, kind, rect2)
-    int32_t ref16;        // the leaf's 16-byte offset in ref_blob (whole-leaf evaluation)
-    int32_t pad;
+    int32_t slot_base;  // slots[] index of the instance's run of world slots
+    int32_t pad[2];
 };
 
 // Quad light = NewAreaLight (Light.fs:31-64): two sample triangles (v0, e1, e2), normal, color.

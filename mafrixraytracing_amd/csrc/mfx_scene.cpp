@@ -347,9 +347,13 @@ struct Collapse4 {
     const std::vector<Node2>& n2;
     std::vector<MfxNode>& out;
     int max_depth = 0, max_stack = 0;
+    std::vector<int>* leaf_stack = nullptr;  // optional: per leaf, the stack entries when it is reached
 
     int run(int ref, int depth, int pushed, const FBox* leaf_box = nullptr) {
-        if (ref < 0 && depth > 0) return ref;
+        if (ref < 0 && depth > 0) {
+            if (leaf_stack) (*leaf_stack)[~ref] = pushed;
+            return ref;
+        }
         max_depth = std::max(max_depth, depth);
         int ch[4];
         FBox bx[4];
@@ -825,8 +829,8 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
     s.slot_ref.clear();
     s.shade.clear();
     s.inst.clear();
-    s.meta.clear();
     s.tlas_nodes = s.blas_nodes = s.blas_slots = s.ntemplates = 0;
+    s.top_slots = 0;
     // a world primitive's slots at the end of slots[] (the top level / the flat BVH), shade[] in step
     auto emit_world_prim = [&](int p) {
         const MfxLeaf& rl = leaves[ref_leaf_of[p]];
@@ -882,6 +886,7 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             for (int k = 0; k < 4; ++k)
                 if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~code_of[~nd.child[k]];
         s.ntleaves = (int32_t)t.leaves.size();
+        s.top_slots = (int32_t)s.slots.size();
         roots.push_back(root);
     } else {
         // ---- two levels: a top-level BVH over the loose primitives and the instances, one
@@ -920,8 +925,11 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
         Tree tt;
         if (!build_tree(cb, cent, w, &solo, false, max_leaf, c_isect, tt, err)) return false;
         std::vector<MfxNode> top;
+        std::vector<int> at_leaf(tt.leaves.size(), 0);
         Collapse4 ct{tt.nodes2, top};
+        ct.leaf_stack = &at_leaf;
         const int troot = ct.run(tt.root2, 0, 0, &tt.rootbox);
+        if (tt.root2 < 0) at_leaf[~tt.root2] = 0;  // a lone leaf under the root: nothing pushed
         std::vector<int32_t> tcode(tt.leaves.size());
         for (int l : dfs_leaves(top, troot)) {
             const int b = tt.leaves[l].first, e = tt.leaves[l].second;
@@ -938,13 +946,17 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             for (int k = 0; k < 4; ++k)
                 if (nd.child[k] != MFX_CHILD_EMPTY && nd.child[k] < 0) nd.child[k] = ~tcode[~nd.child[k]];
         s.tlas_nodes = (int32_t)top.size();
+        s.top_slots = (int32_t)s.slots.size();
         s.ntleaves = (int32_t)tt.leaves.size();
         roots.push_back(troot);
         s.bvh_depth = ct.max_depth;
-        int blas_stack = 0, blas_depth = 0;
-        // template BVHs: slots hold the template's own vertices (the exact test rebuilds the world
-        // triangle from them, mfx_layout.h); tslot[t][i] = first slot of template primitive i
-        std::vector<int> tmpl_root, tmpl_slot_base;
+        std::vector<int> blas_stack;
+        int blas_depth = 0;
+        s.blas_slots = 0;
+        // template BVHs over the template primitives (local coordinates); their leaf codes count
+        // slots from the instance's own run of world slots: tslot[t][i] = template primitive i's
+        // first slot in such a run (the template's depth-first leaf order)
+        std::vector<int> tmpl_root, tmpl_nslots;
         std::vector<std::vector<int32_t>> tslot;
         for (int tm = 0; tm < (int)templates.size(); ++tm) {
             const int64_t tf = templates[tm].first;
@@ -965,37 +977,23 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             std::vector<MfxNode> bn;
             Collapse4 cbv{bt.nodes2, bn};
             const int broot = cbv.run(bt.root2, 0, 0, &bt.rootbox);
-            blas_stack = std::max(blas_stack, cbv.max_stack);
+            blas_stack.push_back(cbv.max_stack);
             blas_depth = std::max(blas_depth, cbv.max_depth);
             const int base = (int)s.nodes.size();
-            tmpl_slot_base.push_back((int)s.slots.size());
             std::vector<int32_t> ts(tn), bcode(bt.leaves.size());
+            int local = 0;
             for (int l : dfs_leaves(bn, broot)) {
-                const int s0 = (int)s.slots.size();
+                const int s0 = local;
                 for (int k = bt.leaves[l].first; k < bt.leaves[l].second; ++k) {
                     const int i = bt.ids[k];
-                    const mfx_prim& p = d0->prims[tf + i];
-                    ts[i] = (int32_t)s.slots.size();
-                    for (int j = 0; j < (p.kind == MFX_PRIM_RECT ? 2 : 1); ++j) {
-                        MfxSlot sl{};
-                        if (p.kind == MFX_PRIM_SPHERE) {
-                            std::memcpy(sl.a, p.p[0], sizeof(sl.a));
-                            sl.b[0] = p.p[1][0];
-                        } else {  // Rect: (v0, v1, v2) then (v0, v2, v3) (Rect.fs:11-20)
-                            std::memcpy(sl.a, p.p[0], sizeof(sl.a));
-                            std::memcpy(sl.b, p.p[j == 0 ? 1 : 2], sizeof(sl.b));
-                            std::memcpy(sl.c, p.p[j == 0 ? 2 : 3], sizeof(sl.c));
-                        }
-                        const int kind = p.kind == MFX_PRIM_TRIANGLE ? MFX_KIND_TRI
-                                         : p.kind == MFX_PRIM_RECT   ? MFX_KIND_RECT
-                                                                     : MFX_KIND_SPHERE;
-                        sl.first = -1;
-                        sl.info = (kind << MFX_INFO_KIND_SHIFT) | (j == 1 ? MFX_INFO_RECT2 : 0);
-                        s.slots.push_back(sl);
-                        s.slot_ref.push_back(0);
-                    }
+                    ts[i] = local;
+                    local += tw[i];
                 }
-                if (!leaf_code(s0, bcode[l])) return false;
+                if (local - s0 > MFX_LEAF_SLOTS_MAX || s0 >= MFX_SLOTS_MAX) {
+                    err = "scene too large for the traversal image";
+                    return false;
+                }
+                bcode[l] = (s0 << 3) | (local - s0 - 1);
             }
             for (MfxNode nd : bn) {
                 for (int k = 0; k < 4; ++k) {
@@ -1005,46 +1003,56 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
                 s.nodes.push_back(nd);
             }
             tmpl_root.push_back(base + broot);
+            tmpl_nslots.push_back(local);
             roots.push_back(base + broot);
             tslot.push_back(std::move(ts));
             s.ntleaves += (int32_t)bt.leaves.size();
             s.blas_nodes += (int32_t)bn.size();
+            s.blas_slots += local;
         }
-        s.blas_slots = (int32_t)s.slots.size() - tmpl_slot_base[0];
         s.ntemplates = (int32_t)templates.size();
-        // per instance: its world primitives' shade records (template slot order) and slot records
+        // per instance: its own run of world slots (exact world geometry and reference-leaf data, as
+        // a flat image holds them) in its template's slot order; shade[] stays in slots[] order
         for (int k = 0; k < K; ++k) {
             const Use& u = uses[k];
-            const int tm = u.tmpl, sb = tmpl_slot_base[tm];
-            const int nts = (tm + 1 < (int)templates.size() ? tmpl_slot_base[tm + 1] : (int)s.slots.size()) - sb;
+            const int tm = u.tmpl, nts = tmpl_nslots[tm];
             MfxInstance I{};
             std::memcpy(I.off, u.off, sizeof(I.off));
             I.root = tmpl_root[tm];
-            I.meta_base = (int32_t)s.meta.size();
-            I.slot_base = sb;
-            const int32_t shade_base = (int32_t)s.shade.size();
+            I.slot_base = (int32_t)s.slots.size();
+            if ((int64_t)I.slot_base + nts >= MFX_SLOTS_MAX) {
+                err = "scene too large for the traversal image";
+                return false;
+            }
+            s.slots.resize(s.slots.size() + nts);
+            s.slot_ref.resize(s.slot_ref.size() + nts);
             s.shade.resize(s.shade.size() + nts);
-            s.meta.resize(s.meta.size() + nts);
             for (int64_t i = 0; i < u.count; ++i) {
                 const int p = (int)(u.wbase + i);
-                const int local = tslot[tm][i] - sb;
-                shade_of[p] = shade_base + local;
+                const int at = I.slot_base + tslot[tm][i];
+                shade_of[p] = at;
                 const MfxLeaf& rl = leaves[ref_leaf_of[p]];
                 for (int j = 0; j < nslot_of[p]; ++j) {
-                    s.shade[shade_base + local + j] = pshade[slot_of[p] + j];
-                    MfxInstSlot& m = s.meta[I.meta_base + local + j];
-                    std::memcpy(m.lo, rl.lo, sizeof(m.lo));
-                    std::memcpy(m.hi, rl.hi, sizeof(m.hi));
-                    m.first = rl.first;
-                    m.info = slot_info(p, j, shade_base + local + j);
-                    m.ref16 = ref16[ref_leaf_of[p]];
-                    m.pad = 0;
+                    MfxSlot sl = pslots[slot_of[p] + j];
+                    std::memcpy(sl.lo, rl.lo, sizeof(sl.lo));
+                    std::memcpy(sl.hi, rl.hi, sizeof(sl.hi));
+                    sl.first = rl.first;
+                    sl.info = slot_info(p, j, at + j);
+                    s.slots[at + j] = sl;
+                    s.slot_ref[at + j] = ref16[ref_leaf_of[p]];
+                    s.shade[at + j] = pshade[slot_of[p] + j];
                 }
             }
             s.inst.push_back(I);
         }
-        // the top level's pushes before an instance, its exit marker, then the template's own
-        s.stack_entries = std::max(1, ct.max_stack + 1 + blas_stack);
+        // the top level's entries when an instance is reached, its exit marker, then the template's own
+        int bound = ct.max_stack;
+        for (size_t l = 0; l < tt.leaves.size(); ++l) {
+            const int b = tt.leaves[l].first;
+            if (tt.leaves[l].second - b == 1 && tt.ids[b] >= nl)
+                bound = std::max(bound, at_leaf[l] + 1 + blas_stack[uses[tt.ids[b] - nl].tmpl]);
+        }
+        s.stack_entries = std::max(1, bound);
         s.bvh_depth += blas_depth;
     }
     s.ms_bvh = ms_since(t_bvh);

@@ -17,14 +17,12 @@ struct MfxHostScene {
     std::vector<MfxSlot> slots;     // traversal leaves: runs of MfxSlot records, DFS order
     std::vector<int32_t> slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     std::vector<uint8_t> ref_blob;  // reference leaves: MfxLeaf headers + slot copies, heap order
-    std::vector<MfxShade> shade;    // per world slot: top-level / flat slots in slots[] order, then
-                                    // each traced instance's slots in template-slot order
+    std::vector<MfxShade> shade;    // per traversal slot, in slots[] order
     std::vector<MfxInstance> inst;  // two-level scenes: instances traced through a template BVH
-    std::vector<MfxInstSlot> meta;  // [instance][template slot]: the world slot's reference-leaf data
     int32_t nclusters = 0;          // reference leaves
     int32_t ntleaves = 0;           // traversal leaves
     int32_t world_slots = 0;        // slots of the world primitives (what a flat image holds)
-    int32_t tlas_nodes = 0, blas_nodes = 0, blas_slots = 0, ntemplates = 0;  // two-level shape
+    int32_t tlas_nodes = 0, blas_nodes = 0, blas_slots = 0, ntemplates = 0, top_slots = 0;  // two-level shape (blas_slots: one run per template)
     std::vector<double> albedo;  // [nmat][3]
     MfxLight light;
     MfxCamera camera;

@@ -182,8 +182,33 @@ struct SceneView {
     const int32_t* __restrict__ slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
     const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
-    const MfxInstSlot* __restrict__ meta;  // [instance][template slot] reference-leaf data
+    const MfxInstance* inst_lds;           // LDS copy of instances [0, ninst_lds) (wavefront kernels)
+    int ninst_lds;
 };
+
+// An instance's record: from the kernel's LDS copy when it holds it, else from global memory
+struct InstR {
+    DV off;
+    int root, slot_base;
+};
+__device__ __forceinline__ InstR load_inst(const SceneView& S, int k) {
+    InstR r;
+    if (k < S.ninst_lds) {
+        const MfxInstance& I = S.inst_lds[k];
+        r = InstR{ld3(I.off), I.root, I.slot_base};
+    } else {
+        const MfxInstance& I = S.inst[k];
+        r = InstR{ld3(I.off), I.root, I.slot_base};
+    }
+    return r;
+}
+// block-wide copy of the first n instances into LDS at kernel start (ends with a barrier)
+__device__ __forceinline__ void load_inst_lds(MfxInstance* lds, const MfxInstance* __restrict__ g, int n) {
+    const int4* __restrict__ src = (const int4*)g;
+    int4* dst = (int4*)lds;
+    for (int i = threadIdx.x; i < n * (int)(sizeof(MfxInstance) / 16); i += blockDim.x) dst[i] = src[i];
+    __syncthreads();
+}
 
 struct Stats {
     uint32_t nodes, clusters, prims;  // internal-node visits, leaf visits, primitive tests
@@ -331,10 +356,11 @@ __device__ __forceinline__ bool sphere_hit64(const SlotR& s, DV o, DV d, double 
 // tMax, Trangle.fs:148) is where the leaf's minBy can prefer a miss: that reference leaf is then
 // evaluated whole. SHADOW: returns true at the first occluding candidate. Closest: returns true
 // when B improved.
+// base: the slot index the code counts from (an instance's run of world slots; 0 otherwise).
 template <bool SHADOW, bool STATS>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
-                                         Best& B, Stats& st) {
-    const int s0 = code >> 3, n = (code & 7) + 1;
+                                         Best& B, Stats& st, int base = 0) {
+    const int s0 = base + (code >> 3), n = (code & 7) + 1;
     const MfxSlot* __restrict__ sl = S.slots + s0;
     if (STATS) st.clusters++;
     bool improved = false;
@@ -421,77 +447,6 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     return improved;
 }
 
-// One template leaf of instance `inst` (two-level scenes, mfx_layout.h). The world primitive is
-// rebuilt from the template's vertices exactly as the host expanded the scene (mfx_expand: v +
-// off per coordinate) and as the Triangle constructor derives its edges (e1 = v1 - v0, e2 = v2 -
-// v0, Trangle.fs:107-119); a sphere's centre likewise. Everything the reference order and the
-// leaf semantics need — `first`, info, the reference leaf's box and ref_blob offset — is the world
-// slot's, from the instance's MfxInstSlot records, read only for a hit. Otherwise as leaf_hit.
-template <bool SHADOW, bool STATS>
-__device__ __forceinline__ bool leaf_hit_inst(const SceneView& S, int code, int inst, DV o, DV d, double tMin,
-                                              double tMax, Best& B, Stats& st) {
-    const int s0 = code >> 3, n = (code & 7) + 1;
-    const MfxSlot* __restrict__ sl = S.slots + s0;
-    const MfxInstance* __restrict__ I = S.inst + inst;
-    const DV off = ld3(I->off);
-    const MfxInstSlot* __restrict__ meta = S.meta + (I->meta_base + (s0 - I->slot_base));
-    if (STATS) st.clusters++;
-    bool improved = false;
-    for (int k = 0; k < n; ++k) {
-        SlotR r = load_slot(sl + k);
-        const int kind = (r.info >> MFX_INFO_KIND_SHIFT) & 3;
-        if (STATS) st.prims++;
-        double t = 0.0;
-        int hs = k;
-        bool hit;
-        if (kind == MFX_KIND_SPHERE) {
-            r.a = vadd(r.a, off);
-            hit = sphere_hit64(r, o, d, tMin, tMax, t);
-        } else {
-            SlotR w;
-            w.a = vadd(r.a, off);
-            w.b = vsub(vadd(r.b, off), w.a);
-            w.c = vsub(vadd(r.c, off), w.a);
-            hit = tri_hit64(w, o, d, tMin, t);
-            if (kind == MFX_KIND_RECT) {
-                ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
-                if (!hit) {
-                    hs = k;
-                    r = load_slot(sl + k);
-                    w.a = vadd(r.a, off);
-                    w.b = vsub(vadd(r.b, off), w.a);
-                    w.c = vsub(vadd(r.c, off), w.a);
-                    hit = tri_hit64(w, o, d, tMin, t);
-                }
-            }
-        }
-        if (!hit) continue;
-        const MfxInstSlot* __restrict__ m = meta + hs;
-        const int4 fi = *(const int4*)&m->first;  // first, info, ref16
-        if (t >= tMax) {
-            double t2;
-            int info2, first2;
-            if (ref_leaf_hit<SHADOW>(S.ref_blob, fi.z, o, d, tMin, tMax, t2, info2, first2)) {
-                if (SHADOW) return true;
-                if (beats(B, t2, first2, info2)) {
-                    B = Best{t2, info2, first2, true};
-                    improved = true;
-                }
-            }
-            continue;
-        }
-        if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
-        if (!SHADOW && !beats(B, t, fi.x, fi.y)) continue;
-        const double2 bx0 = *(const double2*)m->lo, bx1 = *(const double2*)(m->lo + 2), bx2 = *(const double2*)(m->hi + 1);
-        const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
-        if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
-        if (SHADOW) return true;
-        B = Best{t, fi.y, fi.x, true};
-        improved = true;
-    }
-    return improved;
-}
-
 __device__ __forceinline__ float f_round_up(double x) {
     float f = (float)x;
     if ((double)f < x) f = nextafterf(f, __builtin_inff());
@@ -522,7 +477,7 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 __device__ __forceinline__ bool is_inst_code(int node) { return node > MFX_TRAV_EXIT && node <= ~MFX_INST_FLAG; }
 // the FP32 search ray in the frame of instance `inst` (-1: the world): origin o - off
 __device__ __forceinline__ RayF frame_ray(const SceneView& S, int inst, DV o, DV d) {
-    if (inst >= 0) o = vsub(o, ld3(S.inst[inst].off));
+    if (inst >= 0) o = vsub(o, load_inst(S, inst).off);
     return make_rayf(o, d);
 }
 
@@ -603,7 +558,7 @@ __device__ __forceinline__ int inst_switch(const SceneView& S, int node, int& in
             inst = ~node & ~MFX_INST_FLAG;
             stack.put(sp, MFX_INST_EXIT, stack.deep(sp + 1));
             ++sp;
-            node = S.inst[inst].root;
+            node = load_inst(S, inst).root;
         }
     } while (is_inst_code(node));
     return node;
@@ -702,8 +657,8 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         }
         if (node == MFX_TRAV_EXIT) return B.found;
         // ---- leaf ----
-        const bool better = (INST && inst >= 0) ? leaf_hit_inst<SHADOW, STATS>(S, ~node, inst, o, d, tMin, tMax, B, st)
-                                                : leaf_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, B, st);
+        const int base = (INST && inst >= 0) ? load_inst(S, inst).slot_base : 0;
+        const bool better = leaf_hit<SHADOW, STATS>(S, ~node, o, d, tMin, tMax, B, st, base);
         if (better) {
             if (SHADOW) {
                 B.found = true;

@@ -63,7 +63,6 @@ struct WfParams {
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const MfxInstance* inst;  // two-level scenes: instances (null for a flat scene)
-    const MfxInstSlot* meta;  // [instance][template slot] reference-leaf data
     MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
     MfxCamera cam;
     double* accum;  // [3][w*h]
@@ -90,7 +89,7 @@ struct WfParams {
     int32_t pool;                         // slots scanned (>= total, a multiple of 64)
     int32_t width, height, max_depth;
     int32_t stack_size;                   // traversal stack bound (entries per lane)
-    int32_t stack_lds;                    // of which in LDS; the rest in `spill`
+    int32_t stack_lds_ext, stack_lds_shd; // of which in LDS, per kernel; the rest in `spill`
     int32_t* spill;                       // [stack_size - stack_lds][grid * 256] deep stack entries
     int32_t chunk;                        // slots per chunk fetch of the kernels
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
@@ -98,6 +97,7 @@ struct WfParams {
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
     int32_t ntop_ext, ntop_shd;           // top BVH nodes each trace kernel keeps in LDS (<= nodes)
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
+    int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
@@ -108,13 +108,15 @@ struct WfParams {
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)
 #endif
+#ifndef WF_INST_LDS
+#define WF_INST_LDS 64  // instance records (48 B) a trace kernel keeps in LDS, at most; more stay in global memory
+#endif
 #ifndef WF_NTOP_MAX
 #define WF_NTOP_MAX MFX_TOP_NODES  // top BVH nodes a trace kernel may keep in LDS (mfx_scene.cpp numbers them first)
 #endif
-// resident blocks per CU of each kernel with `stack_lds` stack entries per lane and ntop_* top
-// BVH nodes in LDS
-hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
-                            int* shd_blocks_per_cu, bool inst = false);
+// resident blocks per CU of k_extend / k_shadow with `stack_lds` stack entries per lane (spill: the
+// SpillStack instance), ntop top BVH nodes and min(ninst, WF_INST_LDS) instance records in LDS
+hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

@@ -173,9 +173,10 @@ struct Scanner {
 // the lane's stack: all of it in LDS, or the first P.stack_lds entries (the rest in P.spill)
 template <bool SPILL>
 __device__ __forceinline__ typename std::conditional<SPILL, SpillStack, LdsStack>::type make_stack(int* lds,
-                                                                                                  const WfParams& P) {
+                                                                                                  const WfParams& P,
+                                                                                                  int nlds) {
     if constexpr (SPILL)
-        return SpillStack{lds, P.spill + blockIdx.x * 256 + threadIdx.x, P.stack_lds, (int)gridDim.x * 256};
+        return SpillStack{lds, P.spill + blockIdx.x * 256 + threadIdx.x, nlds, (int)gridDim.x * 256};
     else
         return LdsStack{lds};
 }
@@ -236,9 +237,8 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 #ifdef MFX_DIAG_OCCLUSION
     if (STATS && !SHADOW && T.B.found) st.after_leaves++;
 #endif
-    const bool better = (INST && T.inst >= 0)
-                            ? leaf_hit_inst<SHADOW, STATS>(S, ~T.node, T.inst, T.o, T.d, 1e-6, T.tmax64, T.B, st)
-                            : leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st);
+    const int base = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
+    const bool better = leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
     if (better) {
         if (SHADOW) {
             T.B.found = true;
@@ -295,14 +295,16 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
-    int* lds = lds_all + P.ntop_ext * 32;
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
+    if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
+    int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
-    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds * 64 + lane, P);
-    int* pend = lds + 4 * P.stack_lds * 64 + wave * WF_EXT_PEND;
-    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
+    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
+    int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
+    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -435,15 +437,17 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
-    int* lds = lds_all + P.ntop_shd * 32;
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
+    if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
+    int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
-    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds * 64 + lane, P);
-    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds * 64);
+    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_shd * 64 + lane, P, P.stack_lds_shd);
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, P.meta};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -730,8 +734,9 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 // launchers
 // ------------------------------------------------------------------------------------------------
 // top nodes, stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
-static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop) {
-    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)4 * stack_size * 64 * sizeof(int);
+static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst) {
+    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) +
+                          (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
@@ -745,55 +750,62 @@ static int wf_lds_blocks(size_t bytes) {
     return (int)(per_cu / ((bytes + g - 1) / g * g));
 }
 
-hipError_t mfx_wf_occupancy(int stack_lds, bool spill, int ntop_ext, int ntop_shd, int* ext_blocks_per_cu,
-                            int* shd_blocks_per_cu, bool inst) {
-    const size_t le = wf_lds_bytes(stack_lds, false, ntop_ext), ls = wf_lds_bytes(stack_lds, true, ntop_shd);
-    const void* ke = inst ? (spill ? (const void*)k_extend<false, true, true> : (const void*)k_extend<false, false, true>)
-                          : (spill ? (const void*)k_extend<false, true, false> : (const void*)k_extend<false, false, false>);
-    const void* ks = inst ? (spill ? (const void*)k_shadow<false, true, 4, true> : (const void*)k_shadow<false, false, 4, true>)
-                          : (spill ? (const void*)k_shadow<false, true, 4, false> : (const void*)k_shadow<false, false, 4, false>);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(ext_blocks_per_cu, ke, 256, le);
-    if (e != hipSuccess) return e;
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, ks, 256, ls);
-    *ext_blocks_per_cu = std::min(*ext_blocks_per_cu, wf_lds_blocks(le));
-    *shd_blocks_per_cu = std::min(*shd_blocks_per_cu, wf_lds_blocks(ls));
+hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu) {
+    const bool inst = ninst > 0;
+    const size_t lds = wf_lds_bytes(stack_lds, shadow, ntop, std::min(ninst, WF_INST_LDS));
+    const void* k;
+    if (shadow)
+        k = inst ? (spill ? (const void*)k_shadow<false, true, 4, true> : (const void*)k_shadow<false, false, 4, true>)
+                 : (spill ? (const void*)k_shadow<false, true, 4, false> : (const void*)k_shadow<false, false, 4, false>);
+    else
+        k = inst ? (spill ? (const void*)k_extend<false, true, true> : (const void*)k_extend<false, false, true>)
+                 : (spill ? (const void*)k_extend<false, true, false> : (const void*)k_extend<false, false, false>);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds);
+    *blocks_per_cu = std::min(*blocks_per_cu, wf_lds_blocks(lds));
     return e;
 }
 
+template <bool SPILL, bool INST>
+static void launch_extend(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
+    if (stats)
+        hipLaunchKernelGGL((k_extend<true, SPILL, INST>), dim3(grid), dim3(256), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_extend<false, SPILL, INST>), dim3(grid), dim3(256), lds, st, P);
+}
 template <bool SPILL, int WAVES, bool INST>
-static void launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
-                             hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
+static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (stats)
-        hipLaunchKernelGGL((k_extend<true, SPILL, INST>), dim3(ext_grid), dim3(256), lds_e, st, P);
+        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_extend<false, SPILL, INST>), dim3(ext_grid), dim3(256), lds_e, st, P);
-    if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return;
-    if (stats)
-        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST>), dim3(shd_grid), dim3(256), lds_s, st, P);
-    else
-        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(shd_grid), dim3(256), lds_s, st, P);
+        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
 }
 
 template <bool INST>
-static void launch_iteration_inst(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
-                                  hipEvent_t* ev, size_t lds_e, size_t lds_s, hipError_t& e) {
-    // k_shadow compiled for 3 waves per SIMD (up to 168 VGPRs, no spills) when its LDS allows no
-    // more blocks anyway, else for 4 (128 VGPRs, a few spills)
-    const bool spill = P.stack_lds < P.stack_size, w3 = P.shadow_waves == 3;
-    if (spill && w3) launch_iteration<true, 3, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else if (spill) launch_iteration<true, 4, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else if (w3) launch_iteration<false, 3, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else launch_iteration<false, 4, INST>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
+                                   hipEvent_t* ev, size_t lds_e, size_t lds_s) {
+    // each kernel keeps its own share of the traversal stack in LDS (the rest spills); k_shadow is
+    // compiled for 3 waves per SIMD (up to 168 VGPRs) when its LDS allows no more blocks anyway
+    if (P.stack_lds_ext < P.stack_size) launch_extend<true, INST>(P, ext_grid, stats, st, lds_e);
+    else launch_extend<false, INST>(P, ext_grid, stats, st, lds_e);
+    hipError_t e = hipEventRecord(ev[0], st);
+    if (e != hipSuccess) return e;
+    const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
+    if (spill && w3) launch_shadow<true, 3, INST>(P, shd_grid, stats, st, lds_s);
+    else if (spill) launch_shadow<true, 4, INST>(P, shd_grid, stats, st, lds_s);
+    else if (w3) launch_shadow<false, 3, INST>(P, shd_grid, stats, st, lds_s);
+    else launch_shadow<false, 4, INST>(P, shd_grid, stats, st, lds_s);
+    return hipSuccess;
 }
 
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
-    const size_t lds_e = wf_lds_bytes(P.stack_lds, false, P.ntop_ext);
-    const size_t lds_s = wf_lds_bytes(P.stack_lds, true, P.ntop_shd);
+    const int ni = P.inst ? P.ninst_lds : 0;
+    const size_t lds_e = wf_lds_bytes(P.stack_lds_ext, false, P.ntop_ext, ni);
+    const size_t lds_s = wf_lds_bytes(P.stack_lds_shd, true, P.ntop_shd, ni);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    if (P.inst) launch_iteration_inst<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
-    else launch_iteration_inst<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s, e);
+    e = P.inst ? launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s)
+               : launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }

@@ -32,7 +32,7 @@ def header_layouts(tmp_path):
     """sizeof and every field offset of the header's structs, as gcc lays them out."""
     from mafrixraytracing_amd import abi
     structs = {"mfx_prim": abi.MfxPrim, "mfx_quad_light": abi.MfxQuadLight, "mfx_pinhole": abi.MfxPinhole,
-               "mfx_scene_desc": abi.MfxSceneDesc, "mfx_options": abi.MfxOptions}
+               "mfx_scene_desc": abi.MfxSceneDesc, "mfx_options": abi.MfxOptions, "mfx_instance": abi.MfxInstance}
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void) {"]
     for cname, py in structs.items():
         lines.append(f'printf("{cname} size %zu\\n", sizeof({cname}));')
@@ -56,6 +56,7 @@ def test_struct_layouts_match_header(tmp_path):
         for f in py._fields_:
             assert lay[(cname, f[0])] == getattr(py, f[0]).offset, (cname, f[0])
     assert lay[("mfx_prim", "size")] == 104 and lay[("mfx_options", "size")] == 40
+    assert lay[("mfx_instance", "size")] == 48
 
 
 def test_version_errors_and_no_cpu_fallback():
