@@ -268,8 +268,9 @@ int mfx_build_leaves(const mfx_scene_desc* scene, int32_t* indices_out, int32_t*
 
 /* How mfx_create built the scene (Scene ctor, Scene.fs:298-313; Bvh.Build, BvhNode.fs:24-61):
  * out[0] = ms for the reference leaf grouping (host), out[1] = ms for the traversal BVH2
- * (GPU incl. transfers, or host), out[2] = ms for the whole scene preparation, out[3] = 1 if the
- * BVH2 was built on the GPU, out[4] = BVH4 nodes, out[5] = traversal slots, out[6] = BVH2
+ * (GPU incl. transfers, or host; with the GPU image layout: the whole traversal image), out[2] = ms
+ * for the whole scene preparation, out[3] = 1 if the BVH2 was built on the GPU, 2 if its BVH4
+ * collapse and image layout ran there too (flat scenes), out[4] = BVH4 nodes, out[5] = traversal slots, out[6] = BVH2
  * internal nodes, out[7] = BVH2 build levels. digest (may be NULL) = FNV-1a of the device
  * images (nodes, slots, slot_ref, ref_blob, shade): equal digests mean identical traversal.    */
 int mfx_build_info(mfx_ctx* ctx, double out[8], uint64_t* digest);

@@ -981,7 +981,7 @@ int mfx_build_info(mfx_ctx* c, double out[8], uint64_t* digest) {
         out[0] = h.ms_ref_bvh;
         out[1] = h.ms_bvh;
         out[2] = h.ms_total;
-        out[3] = h.bvh_gpu ? 1.0 : 0.0;
+        out[3] = h.images_gpu ? 2.0 : (h.bvh_gpu ? 1.0 : 0.0);
         out[4] = (double)h.nodes.size();
         out[5] = (double)h.slots.size();
         out[6] = h.nodes2;

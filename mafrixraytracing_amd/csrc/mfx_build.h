@@ -7,6 +7,8 @@
 
 #include <vector>
 
+#include "mfx_layout.h"
+
 // A binned-SAH BVH2 over primitives, as mfx_scene.cpp's host SahBuilder produces it: internal
 // node i has two children (>= 0 internal node, < 0 ~leaf) and their FP32 boxes; leaf l is the
 // range [leaf_b[l], leaf_e[l]) of the primitive permutation `ids`. Node and leaf numbering is the
@@ -26,5 +28,29 @@ struct MfxBvh2 {
 // Same parameters as SahBuilder: leaves of at most max_leaf primitives, intersection cost c_isect.
 hipError_t mfx_gpu_sah_build(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
                              float c_isect, MfxBvh2& out);
+
+// The whole traversal image of a flat scene on the GPU: the BVH2 above, its BVH4 collapse and the
+// layout (nodes renumbered, traversal leaves' slots in depth-first order) — the bytes the host
+// path (mfx_scene.cpp: Collapse4 + layout) produces. Per primitive p the caller gives its slots
+// pslots[slot_of[p] .. slot_of[p + 1]) with the reference-leaf box, `first` and the info bits
+// other than the shade index already set, their shade records and the reference leaf's ref_blob
+// offset.
+struct MfxGpuLayoutIn {
+    const MfxSlot* pslots;
+    const MfxShade* pshade;
+    const int32_t* slot_of;   // [n + 1]
+    const int32_t* ref16_of;  // [n]
+    int32_t nslots;
+};
+struct MfxGpuImages {
+    std::vector<MfxNode> nodes;
+    std::vector<MfxSlot> slots;       // + MFX_LEAF_SLOTS_MAX zero records
+    std::vector<int32_t> slot_ref;
+    std::vector<MfxShade> shade;
+    std::vector<int32_t> shade_of;    // [n] shade index (= slot) of each primitive's first slot
+    int32_t max_depth = 0, max_stack = 0, nodes2 = 0, nleaves = 0, levels = 0;
+};
+hipError_t mfx_gpu_build_images(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
+                                float c_isect, const MfxGpuLayoutIn& in, MfxGpuImages& out);
 
 #endif

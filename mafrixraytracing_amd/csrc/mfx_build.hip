@@ -293,14 +293,252 @@ hipError_t dalloc(T** p, size_t n) {
     return hipMalloc((void**)p, std::max<size_t>(1, n) * sizeof(T));
 }
 
+// ------------------------------------------------------------------------------------------------
+// BVH4 collapse and image layout on the device (the host's Collapse4 + mfx_build_scene layout, the
+// same bytes). Level by level from the root: a BVH4 node is a BVH2 node that adopts the children of
+// its largest-area internal child until it has four (first maximum, children replaced in place);
+// its internal children, in order, form the next level, so the levels' concatenation is the
+// breadth-first order. Subtree node and slot counts go bottom-up, preorder indices, slot offsets
+// and stack depths top-down; then nodes are renumbered (the first MFX_TOP_NODES breadth-first,
+// the rest in preorder) and the traversal leaves' slots scattered in depth-first order.
+// ------------------------------------------------------------------------------------------------
+struct W4 {
+    float box[4][6];
+    int ch[4];  // BVH2 refs: >= 0 internal, < 0 ~leaf
+    int cv[4];  // breadth-first index of an internal child (else -1)
+    int nc;
+};
+
+__device__ __forceinline__ float fbox_area(const float* b) { return box_area(b[0], b[1], b[2], b[3], b[4], b[5]); }
+
+// one BVH4 node per frontier entry (a BVH2 node, or ~leaf for a tree that is one leaf)
+__global__ void k_collapse(const int* __restrict__ F, int nF, const float* __restrict__ node_box,
+                           const int* __restrict__ node_child, const float* __restrict__ root_box, W4* __restrict__ W,
+                           int* __restrict__ cnt) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nF) return;
+    const int r = F[i];
+    W4 w;
+    int nc = 2;
+    if (r < 0) {  // the whole scene is one leaf: a root node with one child
+        nc = 1;
+        w.ch[0] = r;
+        for (int a = 0; a < 6; ++a) w.box[0][a] = root_box[a];
+    } else {
+        for (int k = 0; k < 2; ++k) {
+            w.ch[k] = node_child[2 * r + k];
+            for (int a = 0; a < 6; ++a) w.box[k][a] = node_box[(2 * r + k) * 6 + a];
+        }
+    }
+    while (nc > 1 && nc < 4) {
+        int best = -1;
+        float ba = -1.f;
+        for (int k = 0; k < nc; ++k)
+            if (w.ch[k] >= 0 && fbox_area(w.box[k]) > ba) {
+                ba = fbox_area(w.box[k]);
+                best = k;
+            }
+        if (best < 0) break;
+        const int m = w.ch[best];
+        for (int k = nc; k > best + 1; --k) {  // the children of `best` replace it in place
+            w.ch[k] = w.ch[k - 1];
+            for (int a = 0; a < 6; ++a) w.box[k][a] = w.box[k - 1][a];
+        }
+        for (int q = 0; q < 2; ++q) {
+            w.ch[best + q] = node_child[2 * m + q];
+            for (int a = 0; a < 6; ++a) w.box[best + q][a] = node_box[(2 * m + q) * 6 + a];
+        }
+        ++nc;
+    }
+    w.nc = nc;
+    int c = 0;
+    for (int k = 0; k < 4; ++k) {
+        w.cv[k] = -1;
+        if (k < nc && w.ch[k] >= 0) ++c;
+    }
+    W[i] = w;
+    cnt[i] = c;
+}
+
+// exclusive scan of cnt[0..n) in place (one block), the total in *total
+__global__ void __launch_bounds__(1024) k_scan(int* cnt, int n, int* total) {
+    __shared__ int part[1024];
+    int carry = 0;
+    for (int base = 0; base < n; base += 1024) {
+        const int i = base + threadIdx.x;
+        const int v = i < n ? cnt[i] : 0;
+        part[threadIdx.x] = v;
+        __syncthreads();
+        for (int o = 1; o < 1024; o <<= 1) {
+            const int t = threadIdx.x >= o ? part[threadIdx.x - o] : 0;
+            __syncthreads();
+            part[threadIdx.x] += t;
+            __syncthreads();
+        }
+        if (i < n) cnt[i] = carry + part[threadIdx.x] - v;
+        carry += part[1023];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *total = carry;
+}
+
+// the next level: internal children in order; their breadth-first indices into the parents
+__global__ void k_frontier(W4* __restrict__ W, int nF, const int* __restrict__ pos, int next_base, int* __restrict__ F2) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nF) return;
+    int p = pos[i];
+    for (int k = 0; k < W[i].nc; ++k)
+        if (W[i].ch[k] >= 0) {
+            F2[p] = W[i].ch[k];
+            W[i].cv[k] = next_base + p;
+            ++p;
+        }
+}
+
+struct LArgs {
+    const W4* W;             // [n4] breadth-first
+    const int2* leaves;      // [nleaves] ranges of ids
+    const int* ids;
+    const int* slot_of;      // [n + 1] first slot of each primitive in the per-primitive slot array
+    int* size;               // [n4] BVH4 nodes in the subtree
+    int* nslots;             // [n4] slots in the subtree
+    int* pre;                // [n4] preorder index
+    int* sstart;             // [n4] first slot of the subtree (depth-first leaf order)
+    int* pushed;             // [n4] stack entries when the node is reached
+    int* leaf_start;         // [nleaves] first slot of the traversal leaf
+    int* idx;                // [n4] final node index
+    int* max_stack;
+};
+
+__device__ __forceinline__ int leaf_slots(const LArgs& A, int l) {
+    const int2 r = A.leaves[l];
+    int s = 0;
+    for (int k = r.x; k < r.y; ++k) s += A.slot_of[A.ids[k] + 1] - A.slot_of[A.ids[k]];
+    return s;
+}
+
+__global__ void k_sizes(LArgs A, int lo, int hi) {  // bottom-up, one level [lo, hi)
+    const int v = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= hi) return;
+    const W4& w = A.W[v];
+    int n = 1, s = 0;
+    for (int k = 0; k < w.nc; ++k) {
+        if (w.ch[k] >= 0) {
+            n += A.size[w.cv[k]];
+            s += A.nslots[w.cv[k]];
+        } else {
+            s += leaf_slots(A, ~w.ch[k]);
+        }
+    }
+    A.size[v] = n;
+    A.nslots[v] = s;
+}
+
+__global__ void k_preorder(LArgs A, int lo, int hi) {  // top-down, one level [lo, hi)
+    const int v = lo + blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= hi) return;
+    const W4& w = A.W[v];
+    int next = A.pre[v] + 1, slot = A.sstart[v];
+    const int push = A.pushed[v] + w.nc - 1;  // node_step writes stack[pushed .. pushed + nc - 2]
+    atomicMax(A.max_stack, push);
+    for (int k = 0; k < w.nc; ++k) {
+        if (w.ch[k] >= 0) {
+            const int c = w.cv[k];
+            A.pre[c] = next;
+            A.sstart[c] = slot;
+            A.pushed[c] = push;
+            next += A.size[c];
+            slot += A.nslots[c];
+        } else {
+            A.leaf_start[~w.ch[k]] = slot;
+            slot += leaf_slots(A, ~w.ch[k]);
+        }
+    }
+}
+
+// final index: the first MFX_TOP_NODES breadth-first, the rest by preorder rank among the others
+__global__ void k_index(LArgs A, int n4) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n4) return;
+    const int ntop = min(n4, MFX_TOP_NODES);
+    if (v < ntop) {
+        A.idx[v] = v;
+        return;
+    }
+    const int p = A.pre[v];
+    int below = 0;
+    for (int u = 0; u < ntop; ++u) below += A.pre[u] < p ? 1 : 0;
+    A.idx[v] = ntop + p - below;
+}
+
+__global__ void k_nodes(LArgs A, int n4, MfxNode* __restrict__ out) {
+    const int v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= n4) return;
+    const W4& w = A.W[v];
+    MfxNode nd;
+    for (int k = 0; k < 4; ++k) {
+        const bool e = k < w.nc;
+        nd.lox[k] = e ? w.box[k][0] : FLT_MAX;
+        nd.loy[k] = e ? w.box[k][1] : FLT_MAX;
+        nd.loz[k] = e ? w.box[k][2] : FLT_MAX;
+        nd.hix[k] = e ? w.box[k][3] : FLT_MAX;
+        nd.hiy[k] = e ? w.box[k][4] : FLT_MAX;
+        nd.hiz[k] = e ? w.box[k][5] : FLT_MAX;
+        int c = MFX_CHILD_EMPTY;
+        if (e && w.ch[k] >= 0) c = A.idx[w.cv[k]];
+        else if (e) c = ~((A.leaf_start[~w.ch[k]] << 3) | (leaf_slots(A, ~w.ch[k]) - 1));
+        nd.child[k] = c;
+        nd.pad[k] = 0;
+    }
+    out[A.idx[v]] = nd;
+}
+
+// one traversal leaf: its primitives' slots at its offset, in its order; a slot's shade[] index
+// is its own index (the info field's low bits)
+__global__ void k_slots(LArgs A, int nleaves, const MfxSlot* __restrict__ pslots, const MfxShade* __restrict__ pshade,
+                        const int32_t* __restrict__ ref16_of, MfxSlot* __restrict__ slots, int32_t* __restrict__ slot_ref,
+                        MfxShade* __restrict__ shade, int32_t* __restrict__ shade_of) {
+    const int l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= nleaves) return;
+    const int2 r = A.leaves[l];
+    int at = A.leaf_start[l];
+    for (int k = r.x; k < r.y; ++k) {
+        const int p = A.ids[k];
+        shade_of[p] = at;
+        for (int q = A.slot_of[p]; q < A.slot_of[p + 1]; ++q, ++at) {
+            MfxSlot sl = pslots[q];
+            sl.info |= at;
+            slots[at] = sl;
+            slot_ref[at] = ref16_of[p];
+            shade[at] = pshade[q];
+        }
+    }
+}
+
 }  // namespace
 
-hipError_t mfx_gpu_sah_build(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
-                             float c_isect, MfxBvh2& out) {
+// The BVH2 build on the device; its arrays stay there for the collapse and layout
+struct DevBvh2 {
     BArgs A{};
-    float *d_box = nullptr, *d_cent = nullptr;
+    float* d_box = nullptr;
+    float* d_cent = nullptr;
     int* d_weight = nullptr;
-    BTask *t0 = nullptr, *t1 = nullptr;
+    BTask* t0 = nullptr;
+    BTask* t1 = nullptr;
+    int nodes = 0, nleaves = 0, levels = 0, root = 0;
+};
+
+static void bvh2_free(DevBvh2& D) {
+    void* bufs[] = {D.d_box, D.d_cent, D.d_weight, D.A.ids, D.A.tmp, D.A.node_box, D.A.node_child, D.A.leaves,
+                    D.A.counters, D.A.root_box, D.A.root_ref, D.t0, D.t1};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    D = DevBvh2{};
+}
+
+static hipError_t bvh2_build(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
+                             float c_isect, DevBvh2& D) {
+    BArgs& A = D.A;
     hipError_t e = hipSuccess;
     auto ok = [&](hipError_t r) {
         if (e == hipSuccess) e = r;
@@ -308,9 +546,9 @@ hipError_t mfx_gpu_sah_build(const float* prim_box, const float* cent, const int
     };
     std::vector<int32_t> iota(n);
     std::iota(iota.begin(), iota.end(), 0);
-    ok(dalloc(&d_box, 6 * (size_t)n));
-    ok(dalloc(&d_cent, 3 * (size_t)n));
-    ok(dalloc(&d_weight, (size_t)n));
+    ok(dalloc(&D.d_box, 6 * (size_t)n));
+    ok(dalloc(&D.d_cent, 3 * (size_t)n));
+    ok(dalloc(&D.d_weight, (size_t)n));
     ok(dalloc(&A.ids, (size_t)n));
     ok(dalloc(&A.tmp, (size_t)n));
     ok(dalloc(&A.node_box, 12 * (size_t)n));
@@ -319,56 +557,179 @@ hipError_t mfx_gpu_sah_build(const float* prim_box, const float* cent, const int
     ok(dalloc(&A.counters, 4));
     ok(dalloc(&A.root_box, 6));
     ok(dalloc(&A.root_ref, 1));
-    ok(dalloc(&t0, (size_t)n));
-    ok(dalloc(&t1, (size_t)n));
+    ok(dalloc(&D.t0, (size_t)n));
+    ok(dalloc(&D.t1, (size_t)n));
     if (e == hipSuccess) {
-        ok(hipMemcpy(d_box, prim_box, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice));
-        ok(hipMemcpy(d_cent, cent, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice));
-        ok(hipMemcpy(d_weight, weight, sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
+        ok(hipMemcpy(D.d_box, prim_box, sizeof(float) * 6 * (size_t)n, hipMemcpyHostToDevice));
+        ok(hipMemcpy(D.d_cent, cent, sizeof(float) * 3 * (size_t)n, hipMemcpyHostToDevice));
+        ok(hipMemcpy(D.d_weight, weight, sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
         ok(hipMemcpy(A.ids, iota.data(), sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
         ok(hipMemset(A.counters, 0, 4 * sizeof(int)));
         const BTask root{0, n, -1, 0};
-        ok(hipMemcpy(t0, &root, sizeof(BTask), hipMemcpyHostToDevice));
+        ok(hipMemcpy(D.t0, &root, sizeof(BTask), hipMemcpyHostToDevice));
     }
-    A.box = d_box;
-    A.cent = d_cent;
-    A.weight = d_weight;
+    A.box = D.d_box;
+    A.cent = D.d_cent;
+    A.weight = D.d_weight;
     A.max_leaf = max_leaf;
     A.c_isect = c_isect;
-    int ntasks = 1, levels = 0;
+    int ntasks = 1;
     while (e == hipSuccess && ntasks > 0) {
         ok(hipMemset(A.counters + 2, 0, sizeof(int)));
-        hipLaunchKernelGGL(k_sah_level, dim3((ntasks + 3) / 4), dim3(256), 0, 0, A, t0, ntasks, t1);
+        hipLaunchKernelGGL(k_sah_level, dim3((ntasks + 3) / 4), dim3(256), 0, 0, A, D.t0, ntasks, D.t1);
         ok(hipGetLastError());
         ok(hipMemcpy(&ntasks, A.counters + 2, sizeof(int), hipMemcpyDeviceToHost));
-        std::swap(t0, t1);
-        ++levels;
-        if (levels > 4 * 64 + n) ok(hipErrorUnknown);  // cannot happen: every level splits ranges
+        std::swap(D.t0, D.t1);
+        ++D.levels;
+        if (D.levels > 4 * 64 + n) ok(hipErrorUnknown);  // cannot happen: every level splits ranges
     }
     int cnt[2] = {0, 0};
+    ok(hipMemcpy(cnt, A.counters, 2 * sizeof(int), hipMemcpyDeviceToHost));
+    ok(hipMemcpy(&D.root, A.root_ref, sizeof(int), hipMemcpyDeviceToHost));
+    D.nodes = cnt[0];
+    D.nleaves = cnt[1];
+    return e;
+}
+
+hipError_t mfx_gpu_sah_build(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
+                             float c_isect, MfxBvh2& out) {
+    DevBvh2 D;
+    hipError_t e = bvh2_build(prim_box, cent, weight, n, max_leaf, c_isect, D);
+    auto ok = [&](hipError_t r) {
+        if (e == hipSuccess) e = r;
+        return e == hipSuccess;
+    };
     if (e == hipSuccess) {
-        ok(hipMemcpy(cnt, A.counters, 2 * sizeof(int), hipMemcpyDeviceToHost));
-        out.box.resize(12 * (size_t)cnt[0]);
-        out.child.resize(2 * (size_t)cnt[0]);
-        std::vector<int2> lv(cnt[1]);
+        const BArgs& A = D.A;
+        out.box.resize(12 * (size_t)D.nodes);
+        out.child.resize(2 * (size_t)D.nodes);
+        std::vector<int2> lv(D.nleaves);
         out.ids.resize(n);
         ok(hipMemcpy(out.box.data(), A.node_box, sizeof(float) * out.box.size(), hipMemcpyDeviceToHost));
         ok(hipMemcpy(out.child.data(), A.node_child, sizeof(int) * out.child.size(), hipMemcpyDeviceToHost));
         ok(hipMemcpy(lv.data(), A.leaves, sizeof(int2) * lv.size(), hipMemcpyDeviceToHost));
         ok(hipMemcpy(out.ids.data(), A.ids, sizeof(int) * (size_t)n, hipMemcpyDeviceToHost));
-        ok(hipMemcpy(&out.root, A.root_ref, sizeof(int), hipMemcpyDeviceToHost));
         ok(hipMemcpy(out.root_box, A.root_box, sizeof(float) * 6, hipMemcpyDeviceToHost));
+        out.root = D.root;
         out.leaf_b.resize(lv.size());
         out.leaf_e.resize(lv.size());
         for (size_t l = 0; l < lv.size(); ++l) {
             out.leaf_b[l] = lv[l].x;
             out.leaf_e[l] = lv[l].y;
         }
-        out.levels = levels;
+        out.levels = D.levels;
     }
-    void* bufs[] = {d_box, d_cent, d_weight, A.ids, A.tmp, A.node_box, A.node_child, A.leaves, A.counters,
-                    A.root_box, A.root_ref, t0, t1};
+    bvh2_free(D);
+    return e;
+}
+
+hipError_t mfx_gpu_build_images(const float* prim_box, const float* cent, const int32_t* weight, int n, int max_leaf,
+                                float c_isect, const MfxGpuLayoutIn& in, MfxGpuImages& out) {
+    DevBvh2 D;
+    hipError_t e = bvh2_build(prim_box, cent, weight, n, max_leaf, c_isect, D);
+    auto ok = [&](hipError_t r) {
+        if (e == hipSuccess) e = r;
+        return e == hipSuccess;
+    };
+    const int n4max = D.nodes + 1;
+    W4* W = nullptr;
+    int *F = nullptr, *cnt = nullptr, *total = nullptr, *slot_of = nullptr, *ref16 = nullptr, *shade_of = nullptr;
+    int *size = nullptr, *nsl = nullptr, *pre = nullptr, *sstart = nullptr, *pushed = nullptr, *lstart = nullptr,
+        *idx = nullptr, *mstack = nullptr;
+    MfxSlot *pslots = nullptr, *slots = nullptr;
+    MfxShade *pshade = nullptr, *shade = nullptr;
+    MfxNode* nodes = nullptr;
+    int32_t* slot_ref = nullptr;
+    const size_t ns = (size_t)in.nslots;
+    ok(dalloc(&W, n4max));
+    ok(dalloc(&F, n4max));
+    ok(dalloc(&cnt, n4max));
+    ok(dalloc(&total, 1));
+    ok(dalloc(&size, n4max));
+    ok(dalloc(&nsl, n4max));
+    ok(dalloc(&pre, n4max));
+    ok(dalloc(&sstart, n4max));
+    ok(dalloc(&pushed, n4max));
+    ok(dalloc(&idx, n4max));
+    ok(dalloc(&mstack, 1));
+    ok(dalloc(&lstart, (size_t)std::max(1, D.nleaves)));
+    ok(dalloc(&slot_of, (size_t)n + 1));
+    ok(dalloc(&ref16, (size_t)n));
+    ok(dalloc(&shade_of, (size_t)n));
+    ok(dalloc(&pslots, ns));
+    ok(dalloc(&pshade, ns));
+    ok(dalloc(&slots, ns + MFX_LEAF_SLOTS_MAX));
+    ok(dalloc(&slot_ref, ns));
+    ok(dalloc(&shade, ns));
+    ok(dalloc(&nodes, n4max));
+    if (e == hipSuccess) {
+        ok(hipMemcpy(slot_of, in.slot_of, sizeof(int) * ((size_t)n + 1), hipMemcpyHostToDevice));
+        ok(hipMemcpy(ref16, in.ref16_of, sizeof(int) * (size_t)n, hipMemcpyHostToDevice));
+        ok(hipMemcpy(pslots, in.pslots, sizeof(MfxSlot) * ns, hipMemcpyHostToDevice));
+        ok(hipMemcpy(pshade, in.pshade, sizeof(MfxShade) * ns, hipMemcpyHostToDevice));
+        ok(hipMemset(slots + ns, 0, sizeof(MfxSlot) * MFX_LEAF_SLOTS_MAX));  // speculative loads stay in bounds
+        ok(hipMemcpy(F, &D.root, sizeof(int), hipMemcpyHostToDevice));
+        ok(hipMemset(pre, 0, sizeof(int)));
+        ok(hipMemset(sstart, 0, sizeof(int)));
+        ok(hipMemset(pushed, 0, sizeof(int)));
+        ok(hipMemset(mstack, 0, sizeof(int)));
+    }
+    // collapse, level by level: frontier [base, base + nF) of F is a level in breadth-first order
+    std::vector<int> lo;
+    int base = 0, nF = 1;
+    while (e == hipSuccess && nF > 0) {
+        if (base + nF > n4max) {
+            ok(hipErrorUnknown);
+            break;
+        }
+        lo.push_back(base);
+        const dim3 g((nF + 255) / 256);
+        hipLaunchKernelGGL(k_collapse, g, dim3(256), 0, 0, F + base, nF, D.A.node_box, D.A.node_child, D.A.root_box,
+                           W + base, cnt + base);
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, 0, cnt + base, nF, total);
+        hipLaunchKernelGGL(k_frontier, g, dim3(256), 0, 0, W + base, nF, cnt + base, base + nF, F + base + nF);
+        ok(hipGetLastError());
+        int t = 0;
+        ok(hipMemcpy(&t, total, sizeof(int), hipMemcpyDeviceToHost));
+        base += nF;
+        nF = t;
+    }
+    const int n4 = base;
+    lo.push_back(n4);
+    const int nlev = (int)lo.size() - 1;
+    LArgs A{W, D.A.leaves, D.A.ids, slot_of, size, nsl, pre, sstart, pushed, lstart, idx, mstack};
+    for (int L = nlev - 1; L >= 0 && e == hipSuccess; --L)
+        hipLaunchKernelGGL(k_sizes, dim3((lo[L + 1] - lo[L] + 255) / 256), dim3(256), 0, 0, A, lo[L], lo[L + 1]);
+    for (int L = 0; L < nlev && e == hipSuccess; ++L)
+        hipLaunchKernelGGL(k_preorder, dim3((lo[L + 1] - lo[L] + 255) / 256), dim3(256), 0, 0, A, lo[L], lo[L + 1]);
+    if (e == hipSuccess && n4 > 0) {
+        hipLaunchKernelGGL(k_index, dim3((n4 + 255) / 256), dim3(256), 0, 0, A, n4);
+        hipLaunchKernelGGL(k_nodes, dim3((n4 + 255) / 256), dim3(256), 0, 0, A, n4, nodes);
+        hipLaunchKernelGGL(k_slots, dim3((D.nleaves + 255) / 256), dim3(256), 0, 0, A, D.nleaves, pslots, pshade, ref16,
+                           slots, slot_ref, shade, shade_of);
+        ok(hipGetLastError());
+    }
+    if (e == hipSuccess) {
+        out.nodes.resize(n4);
+        out.slots.resize(ns + MFX_LEAF_SLOTS_MAX);
+        out.slot_ref.resize(ns);
+        out.shade.resize(ns);
+        out.shade_of.resize(n);
+        ok(hipMemcpy(out.nodes.data(), nodes, sizeof(MfxNode) * n4, hipMemcpyDeviceToHost));
+        ok(hipMemcpy(out.slots.data(), slots, sizeof(MfxSlot) * out.slots.size(), hipMemcpyDeviceToHost));
+        ok(hipMemcpy(out.slot_ref.data(), slot_ref, sizeof(int32_t) * ns, hipMemcpyDeviceToHost));
+        ok(hipMemcpy(out.shade.data(), shade, sizeof(MfxShade) * ns, hipMemcpyDeviceToHost));
+        ok(hipMemcpy(out.shade_of.data(), shade_of, sizeof(int32_t) * (size_t)n, hipMemcpyDeviceToHost));
+        ok(hipMemcpy(&out.max_stack, mstack, sizeof(int), hipMemcpyDeviceToHost));
+        out.max_depth = nlev - 1;
+        out.nodes2 = D.nodes;
+        out.nleaves = D.nleaves;
+        out.levels = D.levels;
+    }
+    void* bufs[] = {W, F, cnt, total, size, nsl, pre, sstart, pushed, idx, mstack, lstart, slot_of, ref16, shade_of,
+                    pslots, pshade, slots, slot_ref, shade, nodes};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    bvh2_free(D);
     return e;
 }

@@ -831,6 +831,7 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
     s.inst.clear();
     s.tlas_nodes = s.blas_nodes = s.blas_slots = s.ntemplates = 0;
     s.top_slots = 0;
+    s.images_gpu = false;
     // a world primitive's slots at the end of slots[] (the top level / the flat BVH), shade[] in step
     auto emit_world_prim = [&](int p) {
         const MfxLeaf& rl = leaves[ref_leaf_of[p]];
@@ -867,8 +868,60 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             for (int a = 0; a < 3; ++a) cent[3 * i + a] = 0.5f * (cb[i].lo[a] + cb[i].hi[a]);
             w[i] = nslot_of[i];
         }
+        if (gpu_bvh) {
+            // the whole image on the GPU: BVH2, BVH4 collapse, renumbering, slots in depth-first
+            // order (mfx_build.hip; the host path's bytes)
+            std::vector<MfxSlot> ps(pslots.size());
+            std::vector<int32_t> so(n + 1), r16(n);
+            for (int p = 0; p < n; ++p) {
+                so[p] = slot_of[p];
+                r16[p] = ref16[ref_leaf_of[p]];
+                const MfxLeaf& rl = leaves[ref_leaf_of[p]];
+                for (int j = 0; j < nslot_of[p]; ++j) {
+                    MfxSlot sl = pslots[slot_of[p] + j];
+                    std::memcpy(sl.lo, rl.lo, sizeof(sl.lo));
+                    std::memcpy(sl.hi, rl.hi, sizeof(sl.hi));
+                    sl.first = rl.first;
+                    sl.info = slot_info(p, j, 0);
+                    ps[slot_of[p] + j] = sl;
+                }
+            }
+            so[n] = (int32_t)pslots.size();
+            if (pslots.size() >= (size_t)MFX_SLOTS_MAX) {
+                err = "scene too large for the traversal image";
+                return false;
+            }
+            std::vector<float> pbox(6 * (size_t)n);
+            for (int i = 0; i < n; ++i)
+                for (int a = 0; a < 3; ++a) {
+                    pbox[6 * (size_t)i + a] = cb[i].lo[a];
+                    pbox[6 * (size_t)i + 3 + a] = cb[i].hi[a];
+                }
+            MfxGpuImages g;
+            const hipError_t he = mfx_gpu_build_images(
+                pbox.data(), cent.data(), w.data(), n, max_leaf, c_isect,
+                MfxGpuLayoutIn{ps.data(), pshade.data(), so.data(), r16.data(), (int32_t)pslots.size()}, g);
+            if (he != hipSuccess) {
+                err = std::string("GPU BVH build: ") + hipGetErrorString(he);
+                return false;
+            }
+            s.nodes.swap(g.nodes);
+            s.slots.swap(g.slots);
+            s.slots.resize(pslots.size());
+            s.slot_ref.swap(g.slot_ref);
+            s.shade.swap(g.shade);
+            shade_of.swap(g.shade_of);
+            s.bvh_levels = g.levels;
+            s.nodes2 = g.nodes2;
+            s.bvh_depth = g.max_depth;
+            s.stack_entries = std::max(1, g.max_stack);
+            s.ntleaves = g.nleaves;
+            s.top_slots = (int32_t)s.slots.size();
+            s.images_gpu = true;
+            roots.push_back(0);  // already numbered: the renumbering below is the identity
+        } else {
         Tree t;
-        if (!build_tree(cb, cent, w, nullptr, gpu_bvh, max_leaf, c_isect, t, err)) return false;
+        if (!build_tree(cb, cent, w, nullptr, false, max_leaf, c_isect, t, err)) return false;
         s.bvh_levels = t.levels;
         s.nodes2 = (int32_t)t.nodes2.size();
         s.nodes.clear();
@@ -888,6 +941,7 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
         s.ntleaves = (int32_t)t.leaves.size();
         s.top_slots = (int32_t)s.slots.size();
         roots.push_back(root);
+        }
     } else {
         // ---- two levels: a top-level BVH over the loose primitives and the instances, one
         //      template BVH per distinct template range (local coordinates) ---------------------

@@ -32,6 +32,7 @@ struct MfxHostScene {
     float eps = 0.f;           // conservative box widening
     // build record (mfx_build_info)
     bool bvh_gpu = false;      // traversal BVH2 built on the GPU (mfx_build.hip)
+    bool images_gpu = false;   // and its BVH4 collapse and image layout too (flat scenes)
     int32_t bvh_levels = 0;    // its breadth-first levels (GPU) / depth + 1 (host)
     int32_t nodes2 = 0;        // its internal nodes
     double ms_ref_bvh = 0, ms_bvh = 0, ms_total = 0;

@@ -25,8 +25,10 @@ def both(a):
 
 @pytest.mark.parametrize("name", SCENES)
 def test_gpu_bvh_equals_host_bvh(gpu, name):
-    bg, bh = both(scene(name, 16, 16))
+    a = scene(name, 16, 16)
+    bg, bh = both(a)
     assert bg["gpu_bvh"] and not bh["gpu_bvh"]
+    assert bg["gpu_images"] == (a.instancing is None)  # flat scenes: collapse and layout on the GPU too
     for k in ("nodes2", "nodes4", "slots"):
         assert bg[k] == bh[k], (k, bg[k], bh[k])
     assert bg["digest"] == bh["digest"]
