@@ -41,6 +41,7 @@ struct MfxGpuLayoutIn {
     const int32_t* slot_of;   // [n + 1]
     const int32_t* ref16_of;  // [n]
     int32_t nslots;
+    int32_t top_nodes;        // nodes numbered breadth-first first (MFX_TOP_NODES), the rest in preorder
 };
 struct MfxGpuImages {
     std::vector<MfxNode> nodes;

@@ -457,10 +457,10 @@ __global__ void k_preorder(LArgs A, int lo, int hi) {  // top-down, one level [l
 }
 
 // final index: the first MFX_TOP_NODES breadth-first, the rest by preorder rank among the others
-__global__ void k_index(LArgs A, int n4) {
+__global__ void k_index(LArgs A, int n4, int top_nodes) {
     const int v = blockIdx.x * blockDim.x + threadIdx.x;
     if (v >= n4) return;
-    const int ntop = min(n4, MFX_TOP_NODES);
+    const int ntop = min(n4, top_nodes);
     if (v < ntop) {
         A.idx[v] = v;
         return;
@@ -703,7 +703,7 @@ hipError_t mfx_gpu_build_images(const float* prim_box, const float* cent, const 
     for (int L = 0; L < nlev && e == hipSuccess; ++L)
         hipLaunchKernelGGL(k_preorder, dim3((lo[L + 1] - lo[L] + 255) / 256), dim3(256), 0, 0, A, lo[L], lo[L + 1]);
     if (e == hipSuccess && n4 > 0) {
-        hipLaunchKernelGGL(k_index, dim3((n4 + 255) / 256), dim3(256), 0, 0, A, n4);
+        hipLaunchKernelGGL(k_index, dim3((n4 + 255) / 256), dim3(256), 0, 0, A, n4, in.top_nodes);
         hipLaunchKernelGGL(k_nodes, dim3((n4 + 255) / 256), dim3(256), 0, 0, A, n4, nodes);
         hipLaunchKernelGGL(k_slots, dim3((D.nleaves + 255) / 256), dim3(256), 0, 0, A, D.nleaves, pslots, pshade, ref16,
                            slots, slot_ref, shade, shade_of);

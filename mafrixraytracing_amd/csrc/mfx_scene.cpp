@@ -900,7 +900,8 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             MfxGpuImages g;
             const hipError_t he = mfx_gpu_build_images(
                 pbox.data(), cent.data(), w.data(), n, max_leaf, c_isect,
-                MfxGpuLayoutIn{ps.data(), pshade.data(), so.data(), r16.data(), (int32_t)pslots.size()}, g);
+                MfxGpuLayoutIn{ps.data(), pshade.data(), so.data(), r16.data(), (int32_t)pslots.size(), MFX_TOP_NODES},
+                g);
             if (he != hipSuccess) {
                 err = std::string("GPU BVH build: ") + hipGetErrorString(he);
                 return false;
@@ -1024,43 +1025,77 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
                 for (int a = 0; a < 3; ++a) tc[3 * i + a] = 0.5f * (tb[i].lo[a] + tb[i].hi[a]);
                 tw[i] = p.kind == MFX_PRIM_RECT ? 2 : 1;
             }
-            Tree bt;
-            if (!build_tree(tb, tc, tw, nullptr, gpu_bvh, max_leaf, c_isect, bt, err)) return false;
-            s.bvh_levels = std::max(s.bvh_levels, bt.levels);
-            s.nodes2 += (int32_t)bt.nodes2.size();
-            std::vector<MfxNode> bn;
-            Collapse4 cbv{bt.nodes2, bn};
-            const int broot = cbv.run(bt.root2, 0, 0, &bt.rootbox);
-            blas_stack.push_back(cbv.max_stack);
-            blas_depth = std::max(blas_depth, cbv.max_depth);
             const int base = (int)s.nodes.size();
-            std::vector<int32_t> ts(tn), bcode(bt.leaves.size());
-            int local = 0;
-            for (int l : dfs_leaves(bn, broot)) {
-                const int s0 = local;
-                for (int k = bt.leaves[l].first; k < bt.leaves[l].second; ++k) {
-                    const int i = bt.ids[k];
-                    ts[i] = local;
-                    local += tw[i];
-                }
-                if (local - s0 > MFX_LEAF_SLOTS_MAX || s0 >= MFX_SLOTS_MAX) {
-                    err = "scene too large for the traversal image";
+            std::vector<int32_t> ts(tn);
+            std::vector<MfxNode> bn;
+            int broot = 0, local = 0, nleaves = 0;
+            if (gpu_bvh) {  // BVH2, collapse and layout on the GPU, nodes in preorder (as Collapse4 emits them)
+                std::vector<int32_t> so(tn + 1), r16(tn, 0);
+                for (int i = 0; i <= tn; ++i) so[i] = i == 0 ? 0 : so[i - 1] + tw[i - 1];
+                std::vector<MfxSlot> ps(so[tn]);
+                std::vector<MfxShade> psh(so[tn]);
+                std::vector<float> pbox(6 * (size_t)tn);
+                for (int i = 0; i < tn; ++i)
+                    for (int a = 0; a < 3; ++a) {
+                        pbox[6 * (size_t)i + a] = tb[i].lo[a];
+                        pbox[6 * (size_t)i + 3 + a] = tb[i].hi[a];
+                    }
+                MfxGpuImages g;
+                const hipError_t he = mfx_gpu_build_images(pbox.data(), tc.data(), tw.data(), tn, max_leaf, c_isect,
+                                                           MfxGpuLayoutIn{ps.data(), psh.data(), so.data(), r16.data(),
+                                                                          so[tn], 0},
+                                                           g);
+                if (he != hipSuccess) {
+                    err = std::string("GPU BVH build: ") + hipGetErrorString(he);
                     return false;
                 }
-                bcode[l] = (s0 << 3) | (local - s0 - 1);
-            }
-            for (MfxNode nd : bn) {
-                for (int k = 0; k < 4; ++k) {
-                    if (nd.child[k] == MFX_CHILD_EMPTY) continue;
-                    nd.child[k] = nd.child[k] >= 0 ? nd.child[k] + base : ~bcode[~nd.child[k]];
+                bn.swap(g.nodes);
+                ts.swap(g.shade_of);  // a template primitive's first slot in the run
+                local = so[tn];
+                nleaves = g.nleaves;
+                blas_stack.push_back(g.max_stack);
+                blas_depth = std::max(blas_depth, g.max_depth);
+                s.bvh_levels = std::max(s.bvh_levels, g.levels);
+                s.nodes2 += g.nodes2;
+                for (MfxNode& nd : bn)
+                    for (int k = 0; k < 4; ++k)
+                        if (nd.child[k] >= 0) nd.child[k] += base;
+            } else {
+                Tree bt;
+                if (!build_tree(tb, tc, tw, nullptr, false, max_leaf, c_isect, bt, err)) return false;
+                s.bvh_levels = std::max(s.bvh_levels, bt.levels);
+                s.nodes2 += (int32_t)bt.nodes2.size();
+                Collapse4 cbv{bt.nodes2, bn};
+                broot = cbv.run(bt.root2, 0, 0, &bt.rootbox);
+                blas_stack.push_back(cbv.max_stack);
+                blas_depth = std::max(blas_depth, cbv.max_depth);
+                std::vector<int32_t> bcode(bt.leaves.size());
+                for (int l : dfs_leaves(bn, broot)) {
+                    const int s0 = local;
+                    for (int k = bt.leaves[l].first; k < bt.leaves[l].second; ++k) {
+                        const int i = bt.ids[k];
+                        ts[i] = local;
+                        local += tw[i];
+                    }
+                    if (local - s0 > MFX_LEAF_SLOTS_MAX || s0 >= MFX_SLOTS_MAX) {
+                        err = "scene too large for the traversal image";
+                        return false;
+                    }
+                    bcode[l] = (s0 << 3) | (local - s0 - 1);
                 }
-                s.nodes.push_back(nd);
+                for (MfxNode& nd : bn)
+                    for (int k = 0; k < 4; ++k) {
+                        if (nd.child[k] == MFX_CHILD_EMPTY) continue;
+                        nd.child[k] = nd.child[k] >= 0 ? nd.child[k] + base : ~bcode[~nd.child[k]];
+                    }
+                nleaves = (int)bt.leaves.size();
             }
+            s.nodes.insert(s.nodes.end(), bn.begin(), bn.end());
             tmpl_root.push_back(base + broot);
             tmpl_nslots.push_back(local);
             roots.push_back(base + broot);
             tslot.push_back(std::move(ts));
-            s.ntleaves += (int32_t)bt.leaves.size();
+            s.ntleaves += nleaves;
             s.blas_nodes += (int32_t)bn.size();
             s.blas_slots += local;
         }
