@@ -218,7 +218,7 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipMalloc((void**)&c->d_frame, 4 * plane));
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
-    CK(hipMalloc((void**)&c->d_counters, 16 * WF_SHARDS * sizeof(unsigned long long)));
+    CK(hipMalloc((void**)&c->d_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
     CK(hipMalloc((void**)&c->d_wfctl, WF_NCTL * sizeof(unsigned long long)));
     {
         size_t mfree = 0, mtotal = 0;
@@ -235,7 +235,7 @@ static int ctx_setup(mfx_ctx* c) {
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
-    CK(hipMemset(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long)));
+    CK(hipMemset(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, c->device));
     int bpc = 0;
@@ -586,18 +586,19 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
             HIPCHECK(hipEventRecord(ev[2], c->stream));
             if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
                 HIPCHECK(hipStreamSynchronize(c->stream));
-                unsigned long long h[16 * WF_SHARDS];
+                unsigned long long h[WF_NCTR * WF_SHARDS];
                 HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-                double r[16] = {0};
+                double r[WF_NCTR] = {0};
                 for (int k = 0; k < WF_SHARDS; ++k)
-                    for (int q = 0; q < 16; ++q) r[q] += (double)h[16 * k + q];
+                    for (int q = 0; q < WF_NCTR; ++q) r[q] += (double)h[WF_NCTR * k + q];
                 float fe = 0.f, fs = 0.f;
                 HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
                 fprintf(stderr, "gen %lld iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
                         " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g; cumulative traversal closest %.0f %.0f %.0f"
-                        " shadow %.0f %.0f %.0f\n", (long long)g, d + 1,
-                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9]);
+                        " shadow %.0f %.0f %.0f; scan %.4g shade %.4g\n", (long long)g, d + 1,
+                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9],
+                        r[16], r[17]);
             }
         }
         HIPCHECK(mfx_wf_resolve(P, c->stream));
@@ -614,7 +615,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(hipSetDevice(c->device));
     const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
     HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
-    HIPCHECK(hipMemsetAsync(c->d_counters, 0, 16 * WF_SHARDS * sizeof(unsigned long long), c->stream));
+    HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
     // One sample per pixel on this device (Scene.Render's call): the megakernel, unless the caller
     // pins the wavefront. With one path per pixel its FP64 atomic add onto the zeroed accumulator
     // is exact, and its per-path arithmetic is the wavefront's, so the bits are the same; it does
@@ -814,12 +815,12 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
     for (int k = 0; k < 16; ++k) out[k] = 0.0;
     for (mfx_ctx* d : devs_of(c)) {  // summed over the context's devices
         HIPCHECK(hipSetDevice(d->device));
-        unsigned long long h[16 * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
+        unsigned long long h[WF_NCTR * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
         HIPCHECK(hipMemcpyAsync(h, d->d_counters, sizeof(h), hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipStreamSynchronize(d->stream));
         for (int k = 0; k < 16; ++k) {
             double v = 0;
-            for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[16 * g + k];
+            for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[WF_NCTR * g + k];
             out[k] += v;
         }
     }

@@ -38,6 +38,7 @@
 #define WF_DONE 8   // finished with a lit vertex: k_resolve folds its vertices and adds them to its pixel
 #define WF_STATE_MASK 15
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
+#define WF_OCT_SHIFT 28   // WF_NEED_EXT state word: the ray's direction octant << WF_OCT_SHIFT (MFX_OCTANT_SORT)
 // depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
 // shadow ray reached the light); so at most WF_MAX_VERTS vertices (max_depth < WF_MAX_VERTS)
 #define WF_MAX_VERTS 16
@@ -50,6 +51,7 @@
 #ifndef WF_LOOKAHEAD
 #define WF_LOOKAHEAD 4  // windows whose state words a scan loads in one round
 #endif
+#define WF_NCTR 24  // counters per shard: [0..2] rays, [4..9] traversal statistics, [10..17] diagnostics
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
 #define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
@@ -80,7 +82,7 @@ struct WfParams {
     int32_t* state;
     // control
     unsigned long long* ctl;              // [WF_NCTL]
-    unsigned long long* counters;         // [WF_SHARDS][16] ray / traversal counters
+    unsigned long long* counters;         // [WF_SHARDS][WF_NCTR] ray / traversal counters
     int64_t total;                        // paths of this generation (edge-tile padding included)
     int64_t path_base;                    // first path index of this generation
     uint64_t seed;

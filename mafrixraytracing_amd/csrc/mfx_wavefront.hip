@@ -46,6 +46,14 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define MFX_SHADOW_ORDER 1  // shadow rays' child order: 0 near-first, 1 far-first (by exit distance)
 #endif
 
+#ifndef MFX_OCTANT_SORT
+#define MFX_OCTANT_SORT 0  // 1: k_extend's pending extension rays grouped by direction octant (r02ae: -1 to -2 %)
+#endif
+
+#ifndef MFX_SPECULATIVE
+#define MFX_SPECULATIVE 0  // 1: postpone a lane's first leaf and keep stepping (trav_step)
+#endif
+
 #ifndef MFX_NODE_LANES_MIN
 #define MFX_NODE_LANES_MIN 16  // node-loop early exit: fewer lanes than this still stepping
 #endif
@@ -57,7 +65,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow
 #endif
 struct DiagAcc {
-    uint64_t fetch, node, leaf, fin, last;
+    uint64_t fetch, node, leaf, fin, last, scan, shade;
     uint32_t outer, node_iters, windows;
 };
 __device__ __forceinline__ uint64_t stamp() {
@@ -190,7 +198,9 @@ struct Trav {
     double tmax64;
     Best B;
     int node, sp;
-    int inst;  // two-level scenes: the instance whose template the lane is in (-1: the world)
+    int inst;   // two-level scenes: the instance whose template the lane is in (-1: the world)
+    int pleaf;  // MFX_SPECULATIVE: a postponed leaf's code (-1: none)
+    int pbase;  // and the slot base of its frame (two-level scenes)
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
@@ -201,6 +211,8 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.sp = 0;
     T.node = 0;
     T.inst = -1;
+    T.pleaf = -1;
+    T.pbase = 0;
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
@@ -216,6 +228,49 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
     RayF rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
     const float tlim = f_round_up(T.B.t);  // the query's tMax until the first hit, then the best t
+#if MFX_SPECULATIVE
+    // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps
+    // stepping nodes until it reaches a second one, so the node loop and the leaf tests run with
+    // more lanes busy. Results are unchanged: the leaf semantics are order-independent (beats()),
+    // the postponed leaf only culls later (closest hits: a few more node visits). Measured (r02ad):
+    // C2 -5 %, C4 -4 %, C3 +2.5 %; off.
+    while (true) {
+        if (T.node >= 0) {
+            if (STATS) st.nodes++;
+            if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;
+            T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, rf, tlim, stack, T.sp, tn);
+            if (INST && is_inst_code(T.node)) {
+                T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
+                rf = frame_ray(S, T.inst, T.o, T.d);
+            }
+        }
+        if (T.node < 0 && T.node != MFX_TRAV_EXIT && T.pleaf < 0) {  // postpone the leaf, pop the next entry
+            T.pleaf = ~T.node;
+            T.pbase = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
+            if (T.sp == 0) {
+                T.node = MFX_TRAV_EXIT;
+            } else {
+                T.node = stack.get(T.sp - 1, stack.deep(T.sp));
+                --T.sp;
+            }
+            if (INST && is_inst_code(T.node)) {
+                T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
+                rf = frame_ray(S, T.inst, T.o, T.d);
+            }
+        }
+        if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
+    }
+    DIAG_MARK(dg, node, diag);
+    if (T.pleaf >= 0) {
+        const bool better = leaf_hit<SHADOW, STATS>(S, T.pleaf, T.o, T.d, 1e-6, T.tmax64, T.B, st, T.pbase);
+        T.pleaf = -1;
+        if (SHADOW && better) {
+            T.B.found = true;
+            return true;
+        }
+    }
+    return T.node == MFX_TRAV_EXIT;
+#else
     while (T.node >= 0) {
         if (STATS) st.nodes++;
 #ifdef MFX_DIAG_OCCLUSION
@@ -249,6 +304,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     T.node = stack.get(T.sp - 1, stack.deep(T.sp));
     --T.sp;
     return false;
+#endif
 }
 
 // Path index of this generation -> (sample, 8x8 pixel tile, pixel), sample-major and
@@ -317,7 +373,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
     constexpr bool DG = MFX_DIAG_STAMPS == 1;
-    DiagAcc dg{0, 0, 0, 0, 0, 0, 0, 0};
+    DiagAcc dg{};
     if (DG) dg.last = stamp();
 
     while (true) {
@@ -333,7 +389,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
-                    bool take = sj == WF_NEED_EXT;
+                    bool take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
                     if (P.start && sj == WF_FREE && j < P.total) {
                         int x, y;
                         int64_t smp;
@@ -341,11 +397,33 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                         take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
                     }
                     const uint64_t tm = __ballot(take);
-                    if (take) pend[n + __popcll(tm & lanes_below())] = sj == WF_FREE ? (j | (int)0x80000000) : j;
+                    // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
+                    if (take)
+                        pend[n + __popcll(tm & lanes_below())] =
+                            sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
                     n += __popcll(tm);
                     sc.advance(P.state);
                 }
                 wave_lds_sync();
+#if MFX_OCTANT_SORT
+                // extension rays grouped by direction octant (a stable counting sort of the list):
+                // lanes that take entries together trace rays of one octant
+                if (!P.start) {
+                    const int e0 = lane < n ? pend[lane] : 0, e1 = lane + 64 < n ? pend[lane + 64] : 0;
+                    const int k0 = (e0 >> 28) & 7, k1 = (e1 >> 28) & 7;
+                    int d0 = 0, d1 = 0, off = 0;
+                    for (int k = 0; k < 8; ++k) {
+                        const uint64_t b0 = __ballot(lane < n && k0 == k), b1 = __ballot(lane + 64 < n && k1 == k);
+                        if (k0 == k) d0 = off + __popcll(b0 & lanes_below());
+                        if (k1 == k) d1 = off + __popcll(b0) + __popcll(b1 & lanes_below());
+                        off += __popcll(b0) + __popcll(b1);
+                    }
+                    wave_lds_sync();
+                    if (lane < n) pend[d0] = e0;
+                    if (lane + 64 < n) pend[d1] = e1;
+                    wave_lds_sync();
+                }
+#endif
                 pend_lo = 0;
                 pend_hi = n;
                 if (n == 0) break;  // every chunk scanned
@@ -354,7 +432,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
                 const int e = pend[pend_lo + rank];
-                s = e & 0x7fffffff;
+                s = e & 0x0fffffff;
                 fresh = e < 0;
                 DV o, d;
                 if (fresh) {
@@ -407,7 +485,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         }
         DIAG_MARK(dg, fin, DG);
     }
-    unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
+    unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 0, c_primary, red);
     block_add<4>(cnt + 1, c_ext, red);
     if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
@@ -467,7 +545,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint32_t dg_occ = 0, dg_occ_nodes = 0, dg_occ_leaves = 0;
 #endif
     constexpr bool DG = MFX_DIAG_STAMPS == 2;
-    DiagAcc dg{0, 0, 0, 0, 0, 0, 0, 0};
+    DiagAcc dg{};
     if (DG) dg.last = stamp();
 
     while (true) {
@@ -496,6 +574,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     sc.advance(P.state);
                 }
                 wave_lds_sync();
+                DIAG_MARK(dg, scan, DG);
                 if (nshade == 0) break;  // every chunk scanned, every hit shaded, every ray handed out
                 // ---- shade up to 64 listed hits with all lanes: one vertex of PathIntegrator.TraceRay
                 //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
@@ -570,7 +649,9 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
                     pd.slot[lane] = j;
-                    pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
+                    // bits 24..26: the next ray's direction octant (MFX_OCTANT_SORT)
+                    const int oct = (wi.x < 0. ? 1 : 0) | (wi.y < 0. ? 2 : 0) | (wi.z < 0. ? 4 : 0);
+                    pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff) | (oct << 24);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
                     pd.v[4 * 64 + lane] = cs; pd.v[5 * 64 + lane] = solid;
@@ -586,6 +667,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 nshade = rest;
                 pend_lo = 0;
                 pend_hi = cnt;
+                DIAG_MARK(dg, shade, DG);
                 continue;
             }
             const int avail = pend_hi - pend_lo;
@@ -642,12 +724,12 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             // continue with the next vertex's remaining depth; or finished: k_resolve folds the
             // recorded vertices (none lit: nothing to add, FREE)
             if (cont || mask) P.depth[s] = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-            P.state[s] = cont ? WF_NEED_EXT : (mask ? WF_DONE : WF_FREE);
+            P.state[s] = cont ? (WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT)) : (mask ? WF_DONE : WF_FREE);
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
     }
-    unsigned long long* cnt = P.counters + 16 * (blockIdx.x & (WF_SHARDS - 1));
+    unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
     if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
@@ -656,6 +738,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
+        atomicAdd(cnt + 16, (unsigned long long)dg.scan);
+        atomicAdd(cnt + 17, (unsigned long long)dg.shade);
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);
