@@ -80,15 +80,14 @@ struct alignas(16) MfxShade {
 
 // ---- two-level scenes (mfx_create_instanced) ----------------------------------------------------
 // The top-level BVH (nodes[0..)) holds the loose primitives' leaves and, as leaf children, the
-// instances: child = ~(MFX_INST_FLAG | instance). Entering one pushes MFX_INST_EXIT onto the
-// traversal stack, moves the ray's FP32 origin into the template's frame (o - off) and continues at
-// the template BVH's root, whose boxes are the template primitives' (local coordinates); popping
-// MFX_INST_EXIT returns to the world frame. The template BVH is shared; its leaf codes count slots
+// instances: child = ~(MFX_INST_FLAG | instance). Entering one records the traversal stack depth,
+// moves the ray's FP32 origin into the template's frame (o - off) and continues at the template
+// BVH's root, whose boxes are the template primitives' (local coordinates); a pop below the
+// recorded depth returns to the world frame. The template BVH is shared; its leaf codes count slots
 // from the instance's own run of world slots (slot_base), which hold the world primitives exactly
 // as a flat image does (FP64 geometry of the expansion, reference-leaf box, `first`, info), so a
 // template leaf is tested by the same exact leaf test at a per-instance slot base.
 #define MFX_INST_FLAG (1 << 30)                 // leaf codes stay below it (first slot < 2^27)
-#define MFX_INST_EXIT (~(MFX_INST_FLAG | 0x3ffffffe))  // stack marker: leave the instance
 #define MFX_INST_MAX 0x3ffffffe
 
 struct alignas(16) MfxInstance {

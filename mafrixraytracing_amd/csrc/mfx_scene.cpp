@@ -1134,12 +1134,12 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
             }
             s.inst.push_back(I);
         }
-        // the top level's entries when an instance is reached, its exit marker, then the template's own
+        // the top level's entries when an instance is reached, then the template's own
         int bound = ct.max_stack;
         for (size_t l = 0; l < tt.leaves.size(); ++l) {
             const int b = tt.leaves[l].first;
             if (tt.leaves[l].second - b == 1 && tt.ids[b] >= nl)
-                bound = std::max(bound, at_leaf[l] + 1 + blas_stack[uses[tt.ids[b] - nl].tmpl]);
+                bound = std::max(bound, at_leaf[l] + blas_stack[uses[tt.ids[b] - nl].tmpl]);
         }
         s.stack_entries = std::max(1, bound);
         s.bvh_depth += blas_depth;

@@ -472,8 +472,8 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
 
-// two-level scenes: a node value that enters an instance (~(MFX_INST_FLAG | instance)) or leaves
-// one (MFX_INST_EXIT); leaf codes stay below MFX_INST_FLAG
+// two-level scenes: a node value that enters an instance (~(MFX_INST_FLAG | instance)); leaf codes
+// stay below MFX_INST_FLAG
 __device__ __forceinline__ bool is_inst_code(int node) { return node > MFX_TRAV_EXIT && node <= ~MFX_INST_FLAG; }
 // the FP32 search ray in the frame of instance `inst` (-1: the world): origin o - off
 __device__ __forceinline__ RayF frame_ray(const SceneView& S, int inst, DV o, DV d) {
@@ -543,24 +543,23 @@ __device__ __forceinline__ void load_top_nodes(float4* lds, const MfxNode* __res
     __syncthreads();
 }
 
-// Enter / leave instances until `node` is a node, a leaf or MFX_TRAV_EXIT: entering pushes the
-// exit marker and continues at the template's root in the instance's frame; the marker restores
-// the world frame and pops the next entry. The caller recomputes the FP32 ray (frame_ray).
-template <typename ST>
-__device__ __forceinline__ int inst_switch(const SceneView& S, int node, int& inst, const ST& stack, int& sp) {
-    do {
-        if (node == MFX_INST_EXIT) {
-            inst = -1;
-            if (sp == 0) return MFX_TRAV_EXIT;
-            node = stack.get(sp - 1, stack.deep(sp));
-            --sp;
-        } else {
-            inst = ~node & ~MFX_INST_FLAG;
-            stack.put(sp, MFX_INST_EXIT, stack.deep(sp + 1));
-            ++sp;
-            node = load_inst(S, inst).root;
-        }
-    } while (is_inst_code(node));
+// Two-level frame bookkeeping after a step or a pop. A lane in an instance remembers the stack
+// depth at which it entered (inst_sp): entries below it belong to the world frame, so a pop below
+// it leaves the instance (world FP32 ray). An instance code is entered: its template's root, the
+// ray moved into its frame (origin o - off), from one read of its record.
+__device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& inst, int& inst_sp, int sp, DV o, DV d,
+                                          RayF& rf) {
+    if (inst >= 0 && sp < inst_sp) {
+        inst = -1;
+        rf = make_rayf(o, d);
+    }
+    if (is_inst_code(node)) {
+        inst = ~node & ~MFX_INST_FLAG;
+        inst_sp = sp;
+        const InstR r = load_inst(S, inst);
+        rf = make_rayf(vsub(o, r.off), d);
+        node = r.root;
+    }
     return node;
 }
 
@@ -634,7 +633,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
 // (the reference's combine returns a hit iff some visited leaf does). Otherwise: the closest hit
 // under the reference's order (Best). The stack lives in LDS, one column per lane (stride 64
 // dwords: conflict-free).
-// INST: a two-level scene (instances entered and left through inst_switch).
+// INST: a two-level scene (instances entered and left through inst_frame).
 template <bool SHADOW, bool STATS, bool INST = false>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
                          Best& B, Stats& st) {
@@ -643,17 +642,14 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
     float tlim = f_round_up(tMax);
     int sp = 0;
     int node = 0;
-    int inst = -1;
+    int inst = -1, inst_sp = 0;
     const LdsStack stk{stack};
     while (true) {
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
             node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
-            if (INST && is_inst_code(node)) {
-                node = inst_switch(S, node, inst, stk, sp);
-                rf = frame_ray(S, inst, o, d);
-            }
+            if (INST) node = inst_frame(S, node, inst, inst_sp, sp, o, d, rf);
         }
         if (node == MFX_TRAV_EXIT) return B.found;
         // ---- leaf ----
@@ -668,10 +664,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         }
         if (sp == 0) return B.found;
         node = stack[(--sp) * 64];
-        if (INST && is_inst_code(node)) {
-            node = inst_switch(S, node, inst, stk, sp);
-            rf = frame_ray(S, inst, o, d);
-        }
+        if (INST) node = inst_frame(S, node, inst, inst_sp, sp, o, d, rf);
     }
 }
 

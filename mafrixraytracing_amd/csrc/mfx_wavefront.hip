@@ -199,6 +199,7 @@ struct Trav {
     Best B;
     int node, sp;
     int inst;   // two-level scenes: the instance whose template the lane is in (-1: the world)
+    int inst_sp;  // and the stack depth at which it entered (entries below belong to the world)
     int pleaf;  // MFX_SPECULATIVE: a postponed leaf's code (-1: none)
     int pbase;  // and the slot base of its frame (two-level scenes)
 };
@@ -211,6 +212,7 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.sp = 0;
     T.node = 0;
     T.inst = -1;
+    T.inst_sp = 0;
     T.pleaf = -1;
     T.pbase = 0;
 }
@@ -218,15 +220,16 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
-// INST: a two-level scene; a lane enters and leaves instances inside the node loop (inst_switch).
+// INST: a two-level scene; a lane enters and leaves instances inside the node loop (inst_frame).
 template <bool SHADOW, bool STATS, bool INST, typename ST>
 __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
                                           DiagAcc& dg, bool diag) {
-    // an instance exit (or entry) popped at the end of the last round
-    if (INST && is_inst_code(T.node)) T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
+    // the frame of the entry popped at the end of the last round (an instance left or entered)
+    RayF rf;
+    if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
     // the FP32 ray and the node-test limit are recomputed each round (the same values) rather than
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
-    RayF rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
+    rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
     const float tlim = f_round_up(T.B.t);  // the query's tMax until the first hit, then the best t
 #if MFX_SPECULATIVE
     // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps
@@ -239,10 +242,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
             if (STATS) st.nodes++;
             if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;
             T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, rf, tlim, stack, T.sp, tn);
-            if (INST && is_inst_code(T.node)) {
-                T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
-                rf = frame_ray(S, T.inst, T.o, T.d);
-            }
+            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         }
         if (T.node < 0 && T.node != MFX_TRAV_EXIT && T.pleaf < 0) {  // postpone the leaf, pop the next entry
             T.pleaf = ~T.node;
@@ -253,10 +253,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
                 T.node = stack.get(T.sp - 1, stack.deep(T.sp));
                 --T.sp;
             }
-            if (INST && is_inst_code(T.node)) {
-                T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
-                rf = frame_ray(S, T.inst, T.o, T.d);
-            }
+            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         }
         if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
     }
@@ -278,10 +275,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
         T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, T.node, rf, tlim, stack, T.sp, tn);
-        if (INST && is_inst_code(T.node)) {
-            T.node = inst_switch(S, T.node, T.inst, stack, T.sp);
-            rf = frame_ray(S, T.inst, T.o, T.d);
-        }
+        if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
         if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
