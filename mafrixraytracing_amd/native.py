@@ -166,7 +166,7 @@ class NativeContext:
         dig = C.c_uint64()
         check(self.lib.mfx_build_info(self._h, dptr(out), C.byref(dig)), "mfx_build_info")
         return {"ref_bvh_ms": out[0], "bvh_ms": out[1], "scene_ms": out[2], "gpu_bvh": bool(out[3]),
-                "gpu_images": out[3] == 2,
+                "gpu_images": bool(out[3] == 2),
                 "nodes4": int(out[4]), "slots": int(out[5]), "nodes2": int(out[6]), "levels": int(out[7]),
                 "digest": dig.value}
 
