@@ -125,6 +125,7 @@ struct mfx_ctx {
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
+    int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
@@ -239,7 +240,10 @@ static int ctx_setup(mfx_ctx* c) {
     hipDeviceProp_t prop;
     CK(hipGetDeviceProperties(&prop, c->device));
     int bpc = 0;
-    CK(mfx_trace_occupancy(c->stack_size, &bpc, inst));
+    // the megakernel's register budget: 4 waves per SIMD unless the stack is deep (its spills)
+    c->mega_waves = c->stack_size <= 36 ? 4 : 1;
+    if (const char* e = getenv("MFX_MEGA_WAVES")) c->mega_waves = atoi(e) == 4 ? 4 : 1;
+    CK(mfx_trace_occupancy(c->stack_size, &bpc, inst, c->mega_waves));
     bpc = std::max(1, std::min(bpc, 8));
     c->grid = prop.multiProcessorCount * bpc;
     // Traversal stacks, per kernel: the whole bound in LDS unless that costs resident blocks; then
@@ -653,6 +657,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.max_depth = c->host.max_depth;
     P.stack_size = c->stack_size;
     P.vscratch = c->d_vscratch;
+    P.waves = c->mega_waves;
     // paths per chunk: 256, halved while fewer than 16 chunks per wave remain (a 1-spp frame:
     // 64, one path per lane per fetch; r02g/r02i A/B at 1 spp: 256 -> 64 is +21 %)
     if (c->mega_chunk > 0) {

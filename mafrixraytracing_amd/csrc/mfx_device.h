@@ -27,6 +27,7 @@ struct TraceParams {
     int32_t stack_size;              // LDS traversal stack entries per lane
     int32_t chunk;                   // path indices a wave takes per atomic
     double* vscratch;                // [max_depth + 1][6][grid * 256] per-lane vertex records (a_v, c_v)
+    int32_t waves;                   // the kernel instance: 4 (128-VGPR budget) or 1 (unbounded)
 };
 
 struct QueryParams {
@@ -48,7 +49,7 @@ struct QueryParams {
 };
 
 hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st);
-hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst = false);
+hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst = false, int waves = 1);
 hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st);
 hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st);
 hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h, double spp, double frame_count,

@@ -24,12 +24,11 @@
 // ----------------------------------------------------------------------------------------------
 // The integrator megakernel
 // ----------------------------------------------------------------------------------------------
-#ifndef MFX_TRACE_MIN_WAVES
-#define MFX_TRACE_MIN_WAVES 1  // __launch_bounds__ 2nd arg: minimum waves per SIMD
-#endif
-
-template <bool STATS, bool INST>
-__global__ void __launch_bounds__(256, MFX_TRACE_MIN_WAVES) trace_kernel(TraceParams P) {
+// WAVES: the register budget, as minimum waves per SIMD: 1 (no limit: ~152 VGPRs, 3 waves) or 4
+// (128 VGPRs, ~90 B of spills per lane). Measured at one sample per pixel (r02as): 4 waves C2
+// +2.4 %, C5 +9.8 %, C4 -3.4 % (the deep stack: bound 44); mfx_api picks 4 for bounds <= 36.
+template <bool STATS, bool INST, int WAVES>
+__global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
     // one traversal-stack column per lane in LDS. (The top BVH levels in LDS, as the wavefront
     // kernels keep them, measured -21 % here at 1 spp, r02i: the per-node LDS/global branch.)
     extern __shared__ int lds[];
@@ -364,20 +363,31 @@ static size_t trace_lds_bytes(int stack_size) { return (size_t)4 * stack_size * 
 
 hipError_t mfx_launch_trace(const TraceParams& P, bool stats, int grid, hipStream_t st) {
     const size_t lds = trace_lds_bytes(P.stack_size);
-    if (P.inst) {
-        if (stats) hipLaunchKernelGGL((trace_kernel<true, true>), dim3(grid), dim3(256), lds, st, P);
-        else hipLaunchKernelGGL((trace_kernel<false, true>), dim3(grid), dim3(256), lds, st, P);
+    if (P.waves == 4) {
+        if (P.inst) {
+            if (stats) hipLaunchKernelGGL((trace_kernel<true, true, 4>), dim3(grid), dim3(256), lds, st, P);
+            else hipLaunchKernelGGL((trace_kernel<false, true, 4>), dim3(grid), dim3(256), lds, st, P);
+        } else {
+            if (stats) hipLaunchKernelGGL((trace_kernel<true, false, 4>), dim3(grid), dim3(256), lds, st, P);
+            else hipLaunchKernelGGL((trace_kernel<false, false, 4>), dim3(grid), dim3(256), lds, st, P);
+        }
     } else {
-        if (stats) hipLaunchKernelGGL((trace_kernel<true, false>), dim3(grid), dim3(256), lds, st, P);
-        else hipLaunchKernelGGL((trace_kernel<false, false>), dim3(grid), dim3(256), lds, st, P);
+        if (P.inst) {
+            if (stats) hipLaunchKernelGGL((trace_kernel<true, true, 1>), dim3(grid), dim3(256), lds, st, P);
+            else hipLaunchKernelGGL((trace_kernel<false, true, 1>), dim3(grid), dim3(256), lds, st, P);
+        } else {
+            if (stats) hipLaunchKernelGGL((trace_kernel<true, false, 1>), dim3(grid), dim3(256), lds, st, P);
+            else hipLaunchKernelGGL((trace_kernel<false, false, 1>), dim3(grid), dim3(256), lds, st, P);
+        }
     }
     return hipGetLastError();
 }
 
-hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst) {
+hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst, int waves) {
     const size_t lds = trace_lds_bytes(stack_size);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        blocks_per_cu, inst ? (const void*)trace_kernel<false, true> : (const void*)trace_kernel<false, false>, 256, lds);
+    const void* k = waves == 4 ? (inst ? (const void*)trace_kernel<false, true, 4> : (const void*)trace_kernel<false, false, 4>)
+                               : (inst ? (const void*)trace_kernel<false, true, 1> : (const void*)trace_kernel<false, false, 1>);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds);
     // gfx950 allocates LDS in 1,280-byte granules of its 160 KB (the API counts finer ones)
     const size_t g = 1280;
     *blocks_per_cu = std::min(*blocks_per_cu, (int)(160 * 1024 / ((lds + g - 1) / g * g)));
