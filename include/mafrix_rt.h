@@ -280,6 +280,14 @@ int mfx_build_info(mfx_ctx* ctx, double out[8], uint64_t* digest);
 int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* b,
                       double* div_out, double* sqrt_out);
 
+/* Device self-test of the exact shortcuts the traversal puts in front of AABB.hit
+ * (IHitable.fs:18-54): rec = n records of 24 doubles (lo[3], hi[3], origin[3], direction[3],
+ * tMin, tMax, a triangle's v0[3], e1[3], e2[3] whose vertex box lies inside [lo, hi], one pad);
+ * out = 3 int32 per record: the FP64 test's answer (0/1), the FP32 screen's (1 hit, 0 miss, -1
+ * left to the FP64 test) and the vertex-box proof's (1 proved to pass, 0 not proved). Wherever a
+ * shortcut decides it must agree with the FP64 answer.                                         */
+int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out);
+
 /* ---- misc -------------------------------------------------------------------------------- */
 const char* mfx_last_error(void);
 int mfx_abi_version(void);

@@ -1049,4 +1049,21 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
     return MFX_OK;
 }
 
+int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out) {
+    if (n <= 0 || !rec || !out) return fail(MFX_E_INVALID, "bad selftest arguments");
+    HIPCHECK(hipSetDevice(device));
+    double* dr = nullptr;
+    int32_t* dout = nullptr;
+    hipError_t e = hipMalloc((void**)&dr, sizeof(double) * 24 * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(int32_t) * 3 * n);
+    if (e == hipSuccess) e = hipMemcpy(dr, rec, sizeof(double) * 24 * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mfx_launch_aabb_selftest(dr, n, dout, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(int32_t) * 3 * n, hipMemcpyDeviceToHost);
+    if (dr) (void)hipFree(dr);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("aabb selftest: ") + hipGetErrorString(e));
+    return MFX_OK;
+}
+
 }  // extern "C"

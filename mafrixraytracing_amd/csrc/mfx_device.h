@@ -58,5 +58,6 @@ hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_c
 hipError_t mfx_launch_accum_add(double* dst, const double* src, int64_t n, hipStream_t st);
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo,
                                     hipStream_t st);
+hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st);
 
 #endif

@@ -354,6 +354,21 @@ __global__ void fp64_selftest_kernel(const double* a, const double* b, int64_t n
     sq_out[k] = sqrt(a[k]);
 }
 
+// The exact shortcuts in front of the reference-leaf box test against aabb_hit64 (AABB.hit,
+// IHitable.fs:18-54): rec = 24 doubles per case (lo, hi, o, d, tMin, tMax, then a triangle v0, e1,
+// e2 whose vertex box lies in [lo, hi], one pad); out = 3 per case: the FP64 test's answer (0/1),
+// aabb_screen32's (1, 0 or -1 when it leaves the case to the FP64 test) and tri_box_pass's (1
+// proved to pass, 0 not proved)
+__global__ void aabb_selftest_kernel(const double* rec, int64_t n, int32_t* out) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n) return;
+    const double* r = rec + 24 * k;
+    const DV o = ld3(r + 6), d = ld3(r + 9);
+    out[3 * k] = aabb_hit64(r, r + 3, o, d, r[12], r[13]) ? 1 : 0;
+    out[3 * k + 1] = aabb_screen32(r, r + 3, o, d, r[12], r[13]);
+    out[3 * k + 2] = tri_box_pass(ld3(r + 14), ld3(r + 17), ld3(r + 20), o, d, r[12], r[13]) ? 1 : 0;
+}
+
 // ----------------------------------------------------------------------------------------------
 // Host-side launchers (called from mfx_api.cpp)
 // ----------------------------------------------------------------------------------------------
@@ -427,6 +442,11 @@ hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_c
 
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo, hipStream_t st) {
     hipLaunchKernelGGL(fp64_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, a, b, n, dvo, sqo);
+    return hipGetLastError();
+}
+
+hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(aabb_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, out);
     return hipGetLastError();
 }
 

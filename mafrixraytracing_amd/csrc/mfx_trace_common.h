@@ -140,6 +140,63 @@ __device__ __forceinline__ bool aabb_hit64(const double* lo, const double* hi, D
     return tmin < tMax && tmax > tMin;
 }
 
+// AABB.hit decided in FP32 where that is provably the FP64 answer (1 hit, 0 miss; -1: undecided,
+// take aabb_hit64). For non-NaN slab values the reference's test (early-outs included) is the
+// conjunction of: every axis's entry value <= every other axis's exit value, every entry < tMax,
+// every exit > tMin (an axis's own entry <= exit holds for lo <= hi). Each slab value is the
+// reference's FP64 difference b - o, rounded to FP32 and multiplied by rcp_f32(d): relative error
+// < 2^-21 against the FP64 quotient (three roundings of 2^-24 and v_rcp_f32's 1 ulp). A condition
+// counts as decided when its two sides are apart by more than 2^-18 of the larger magnitude taking
+// part (S, or |tMax|, |tMin|) — more than twice their combined error — so only grazing rays,
+// out-of-range values and zero direction components fall back to the divisions.
+__device__ __forceinline__ int aabb_screen32(const double* lo, const double* hi, DV o, DV d, double tMin, double tMax) {
+    const double dd[3] = {d.x, d.y, d.z}, oo[3] = {o.x, o.y, o.z};
+    float mn[3], mx[3];
+    bool ok = true;
+    float S = 0.f;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        const float df = (float)dd[a];
+        const float al = (float)(lo[a] - oo[a]), ah = (float)(hi[a] - oo[a]);  // the reference's FP64 differences
+        const float adf = fabsf(df), aal = fabsf(al), aah = fabsf(ah);
+        ok = ok && adf >= 0x1p-60f && adf <= 0x1p60f && aal <= 0x1p60f && aah <= 0x1p60f &&
+             (aal >= 0x1p-60f || al == 0.f) && (aah >= 0x1p-60f || ah == 0.f);
+        const float r = __builtin_amdgcn_rcpf(df);
+        const float ql = al * r, qh = ah * r;
+        mn[a] = dd[a] >= 0. ? ql : qh;  // the reference's branch on d >= 0 (-0.0 counts as >= 0)
+        mx[a] = dd[a] >= 0. ? qh : ql;
+        S = fmaxf(S, fmaxf(fabsf(ql), fabsf(qh)));
+    }
+    if (!ok) return -1;
+    const float m = S * 0x1p-18f;
+    int res = 1;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            if (i == j) continue;
+            if (mn[i] - mx[j] > m) return 0;   // an entry past another axis's exit: certainly a miss
+            if (!(mx[j] - mn[i] > m)) res = -1;
+        }
+    const float tx = (float)tMax, tn = (float)tMin;
+    const float mX = fmaxf(S, fabsf(tx)) * 0x1p-18f, mN = fmaxf(S, fabsf(tn)) * 0x1p-18f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        if (mn[i] - tx > mX) return 0;  // an entry at or beyond tMax
+        if (!(tx - mn[i] > mX)) res = -1;
+        if (tn - mx[i] > mN) return 0;  // an exit at or before tMin
+        if (!(mx[i] - tn > mN)) res = -1;
+    }
+    return res;
+}
+__device__ __forceinline__ bool aabb_hit(const double* lo, const double* hi, DV o, DV d, double tMin, double tMax) {
+#if MFX_AABB_SCREEN
+    const int r = aabb_screen32(lo, hi, o, d, tMin, tMax);
+    if (r >= 0) return r == 1;
+#endif
+    return aabb_hit64(lo, hi, o, d, tMin, tMax);
+}
+
 // Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148); fields
 // loaded where used (the rare whole-reference-leaf evaluation)
 __device__ __forceinline__ bool tri_hit64(const MfxSlot& s, DV o, DV d, double tMin, double& t) {
@@ -286,8 +343,17 @@ __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV
     return true;
 }
 
+#ifndef MFX_AABB_SCREEN
+#define MFX_AABB_SCREEN 1  // the winning candidate's reference-leaf box test screened in FP32 (exact)
+#endif
+
+#ifndef MFX_TRI_BOX_PROOF
+#define MFX_TRI_BOX_PROOF 1  // a triangle winner's leaf-box test proved from its own vertices (tri_box_pass)
+#endif
 #ifndef MFX_LEAF_PRELOAD
-#define MFX_LEAF_PRELOAD 2  // 0: fields loaded where used; 1: a slot's 80-B test prefix in one round; 2: + its box (+5 % on C2)
+// 0: fields loaded where used; 1: a slot's 80-B test prefix in one round; 2: + its box (+5 % on C2
+// when every winner read it; with MFX_TRI_BOX_PROOF few do)
+#define MFX_LEAF_PRELOAD (MFX_TRI_BOX_PROOF ? 1 : 2)
 #endif
 #ifndef MFX_SHADOW_PRELOAD
 #define MFX_SHADOW_PRELOAD MFX_LEAF_PRELOAD  // the same for shadow queries (a hit ends them: the box is rarely needed)
@@ -344,6 +410,49 @@ __device__ __forceinline__ bool sphere_hit64(const SlotR& s, DV o, DV d, double 
         if (tmx > tMin && tmx < tMax) { t = tmx; return true; }
     }
     return false;
+}
+
+// The reference leaf's box test (AABB.hit, IHitable.fs:18-54) for a triangle candidate, proved to
+// pass without reading the box: the leaf box contains the triangle's vertex box (InitNode unions
+// the primitives' bounds, BvhNode.fs:32-37; Triangle's bound is its vertices', Trangle.fs:113) and
+// the rounded slab test is monotone in the bounds, so an upper bound on every axis's entry value
+// and a lower bound on every exit value that satisfy aabb_screen32's conjunction (entries <= other
+// axes' exits, entries < tMax, exits > tMin) prove the FP64 test passes. The bounds are the vertex
+// box's slab values in FP32 — vertices relative to the origin from the FP64 difference v0 - o and
+// the stored edges — whose error against the FP64 values is below 2^-21 (R / |d| + |q|), R =
+// |v0 - o| + |e1| + |e2| per axis; each comparison needs a gap of 2^-18 of that on both sides.
+// false: not proved (grazing rays, hits within ~1e-5 of the vertex box's faces, zero or tiny
+// direction components, t next to tMin/tMax): the caller runs the FP64 test on the loaded box.
+__device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, double tMin, double tMax) {
+    const double aa[3] = {a.x, a.y, a.z}, b1[3] = {e1.x, e1.y, e1.z}, b2[3] = {e2.x, e2.y, e2.z};
+    const double oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
+    float U[3], L[3], E[3];
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float A = (float)(aa[k] - oo[k]), p = (float)b1[k], q = (float)b2[k];
+        const float x1 = A + p, x2 = A + q;
+        const float mn = fminf(A, fminf(x1, x2)), mx = fmaxf(A, fmaxf(x1, x2));
+        const float R = fabsf(A) + fabsf(p) + fabsf(q);
+        const float df = (float)dd[k], adf = fabsf(df);
+        ok = ok && adf >= 0x1p-60f && adf <= 0x1p60f && R >= 0x1p-60f && R <= 0x1p60f;
+        const float rc = __builtin_amdgcn_rcpf(df);
+        const float qm = mn * rc, qM = mx * rc;
+        U[k] = dd[k] >= 0. ? qm : qM;  // entry <= the vertex box's entry value
+        L[k] = dd[k] >= 0. ? qM : qm;  // exit >= the vertex box's exit value
+        E[k] = (R * fabsf(rc) + fmaxf(fabsf(qm), fabsf(qM))) * 0x1p-18f;
+    }
+    if (!ok) return false;
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+            if (i != j) ok = ok && L[j] - U[i] > E[i] + E[j];
+    const float tx = (float)tMax, tn = (float)tMin;
+    const float ex = fabsf(tx) * 0x1p-22f, en = fabsf(tn) * 0x1p-22f;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) ok = ok && tx - U[i] > E[i] + ex && L[i] - tn > E[i] + en;
+    return ok;
 }
 
 // One traversal leaf (1..4 primitives of possibly different reference leaves; child code = first
@@ -434,11 +543,18 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         }
         if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
         if (!SHADOW && !beats(B, t, first, info)) continue;
+#if MFX_TRI_BOX_PROOF && MFX_LEAF_PRELOAD
+        if (kind != MFX_KIND_SPHERE && tri_box_pass(r.a, r.b, r.c, o, d, tMin, tMax)) {
+            // the reference leaf's box test passes (proved; its box is not read)
+        } else
+#endif
         if (PRE == 2) {
             const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
-            if (!aabb_hit64(blo, bhi, o, d, tMin, tMax)) continue;
+#ifndef MFX_DIAG_NO_LEAFBOX  // timing experiment only: the reference leaf's box test assumed to pass
+            if (!aabb_hit(blo, bhi, o, d, tMin, tMax)) continue;
+#endif
         } else {
-            if (!aabb_hit64(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
+            if (!aabb_hit(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
         }
         if (SHADOW) return true;
         B = Best{t, info, first, true};

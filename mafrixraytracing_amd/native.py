@@ -196,6 +196,16 @@ def fp64_selftest(a: np.ndarray, b: np.ndarray, device: int = 0):
     return dv, sq
 
 
+def aabb_selftest(rec: np.ndarray, device: int = 0):
+    """(FP64 AABB.hit answers, FP32-screen answers: 1, 0 or -1 = left to FP64, vertex-box proofs:
+    1 or 0) for n x 24 records (mfx_aabb_selftest)."""
+    lib = load_library()
+    rec = np.ascontiguousarray(rec, dtype=np.float64).reshape(-1, 24)
+    out = np.zeros((len(rec), 3), dtype=np.int32)
+    check(lib.mfx_aabb_selftest(device, len(rec), dptr(rec), iptr(out)), "mfx_aabb_selftest")
+    return out[:, 0], out[:, 1], out[:, 2]
+
+
 # ---- the reference's object model -----------------------------------------------------------
 class Film:
     """Film (Film.fs:13-34): progressive accumulation; here the accumulator lives on the GPU."""
