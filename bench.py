@@ -76,6 +76,8 @@ def parse():
                     help="weak: config spp per GPU; strong: config spp per job, split over the GPUs")
     ap.add_argument("--single-process", action="store_true",
                     help="N > 1 from one process: one library context over N devices (its own RCCL reduce)")
+    ap.add_argument("--render-ahead", type=int, default=0,
+                    help="--api render: mfx_options.render_ahead (one-sample calls served from batches of K samples)")
     ap.add_argument("--api", default="batch", choices=["batch", "render"],
                     help="batch: mfx_trace_accumulate of the frame's spp; render: spp x mfx_render_rgba8(1)")
     ap.add_argument("--no-render-api", action="store_true", help="skip the render_api sub-measurement")
@@ -157,18 +159,23 @@ def cpu_baseline(arrays, spp, seed, budget_s):
                       f"per-thread rate x nproc (linear, not measured)"}
 
 
-def render_api(arrays, seed, calls, devices=None):
+def render_api(arrays, seed, calls, devices=None, render_ahead=0):
     """Scene.Render's call pattern (Scene.fs:331-333): `calls` x mfx_render_rgba8(ctx, 1, buf), each
     one 1-spp frame into the film, ACES/sqrt/RGBA8 post and the RGBA8 readback to host memory.
-    Rays from the kernels' counters of every call; wall time per call by the host clock."""
+    Rays from the kernels' counters of every call; wall time per call by the host clock.
+    render_ahead = K > 1: the context serves one-sample calls from batches of K samples
+    (mfx_options.render_ahead); the warmup is one whole batch and `calls` a multiple of K, so the
+    timed calls trace exactly the samples they consume."""
     import numpy as np
     from mafrixraytracing_amd.native import NativeContext
-    ctx = NativeContext(arrays, seed=seed, devices=devices)
+    ctx = NativeContext(arrays, seed=seed, devices=devices, render_ahead=render_ahead)
+    if render_ahead > 1:
+        calls = max(1, calls // render_ahead) * render_ahead
     buf = np.empty(arrays.width * arrays.height * 4, dtype=np.uint8)
     import ctypes as C
     bp = buf.ctypes.data_as(C.POINTER(C.c_uint8))
     from mafrixraytracing_amd.abi import check
-    for _ in range(3):
+    for _ in range(render_ahead if render_ahead > 1 else 3):
         check(ctx.lib.mfx_render_rgba8(ctx._h, 1, bp), "mfx_render_rgba8")
     wall, dev, rays = [], [], 0.0
     for _ in range(calls):
@@ -183,9 +190,12 @@ def render_api(arrays, seed, calls, devices=None):
     return {"value": round(rays / total / 1e6, 2), "unit": "Mrays/s", "calls": calls,
             "ms_per_call": round(total / calls * 1e3, 4), "ms_per_call_min": round(min(wall) * 1e3, 4),
             "trace_device_ms_per_call": round(sum(dev) / calls * 1e3, 4),
-            "rays_per_call": round(rays / calls, 1),
+            "rays_per_call": round(rays / calls, 1), "render_ahead": render_ahead,
+            "ms_per_call_max": round(max(wall) * 1e3, 4),
             "includes": "per call: mfx_render_rgba8(ctx, 1, buf) = trace of 1 spp (all bounces), film add, "
-                        "ACES/sqrt/RGBA8 post, 8 MB RGBA8 copy to pageable host memory, synchronize"}
+                        "ACES/sqrt/RGBA8 post, 8 MB RGBA8 copy to pageable host memory, synchronize" +
+                        (f"; render-ahead: one call in {render_ahead} traces the next {render_ahead} samples "
+                         "in one wavefront batch, the others add their held sample plane" if render_ahead > 1 else "")}
 
 
 def main():
@@ -229,7 +239,7 @@ def main():
     mode = MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE
     devices = list(range(args.gpus)) if args.single_process else None
     ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world,
-                        devices=devices)
+                        devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
     pr = None
     if world > 1:
         acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
@@ -391,6 +401,10 @@ def main():
         if ngpu == 1 and args.api == "batch" and not args.no_render_api and not args.megakernel:
             rapi = render_api(arrays, DEFAULT_SEED, args.spp)
             rapi["vs_batch"] = round(rapi["value"] / value, 4)
+            # the same calls with render-ahead over the config's spp (one batch per `spp` calls)
+            ra = render_api(arrays, DEFAULT_SEED, args.spp, render_ahead=args.spp)
+            ra["vs_batch"] = round(ra["value"] / value, 4)
+            rapi["with_render_ahead"] = ra
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)

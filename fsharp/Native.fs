@@ -104,7 +104,7 @@ type MfxSceneDesc =
     val mutable light : MfxQuadLight
     val mutable camera : MfxPinhole
 
-/// mfx_options (40 B): seed, device, flags, part_index, part_count, ndevices, reserved, devices
+/// mfx_options (40 B): seed, device, flags, part_index, part_count, ndevices, render_ahead, devices
 [<Struct; StructLayout(LayoutKind.Sequential)>]
 type MfxOptions =
     val mutable seed : uint64
@@ -113,7 +113,7 @@ type MfxOptions =
     val mutable partIndex : int32
     val mutable partCount : int32
     val mutable ndevices : int32
-    val mutable reserved : int32
+    val mutable renderAhead : int32
     val mutable devices : nativeint
 
 // ---- entry points --------------------------------------------------------------------------------

@@ -30,8 +30,9 @@
 extern "C" {
 #endif
 
-#define MFX_ABI_VERSION 3
+#define MFX_ABI_VERSION 4
 #define MFX_MAX_DEVICES 64
+#define MFX_MAX_RENDER_AHEAD 1024
 
 /* error codes */
 #define MFX_OK 0
@@ -100,14 +101,16 @@ typedef struct mfx_scene_desc {
  * (a communicator the library owns, ncclCommInitAll over the list) sums the FP64 accumulators
  * into devices[0], where film and post run. A list that repeats a device (e.g. {0,0}) adds the
  * accumulators in device order instead (RCCL needs distinct devices).                        */
-typedef struct mfx_options {
+typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ahead (0 = off) */
     uint64_t seed;      /* counter-RNG seed; the reference uses unseeded System.Random */
     int32_t device;     /* HIP device ordinal when ndevices == 0 */
     int32_t flags;      /* MFX_F_* */
     int32_t part_index; /* this context renders sample partition part_index of part_count */
     int32_t part_count; /* (multi-process: one context per rank; partitions are disjoint sample sets) */
     int32_t ndevices;   /* 0: one device (`device`); 1..MFX_MAX_DEVICES: the device list below */
-    int32_t reserved;
+    int32_t render_ahead; /* 0 or 1: off. K in 2..MFX_MAX_RENDER_AHEAD: one-sample mfx_render_rgba8
+                             calls (Scene.Render) on a one-device context take their sample from a
+                             batch of the next K samples traced at once (see mfx_render_rgba8)    */
     const int32_t* devices; /* [ndevices] HIP device ordinals; devices[0] is the primary */
 } mfx_options; /* 40 bytes */
 
@@ -179,7 +182,14 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * (Film.fs:18-34, Scene.fs:315-333): adds spp samples per pixel to the film, then writes the
  * progressive mean through ACES -> sqrt -> int(255.99 c) as RGBA8, y-major:
  * rgba[(y*w + x)*4 + {0,1,2,3}]. `Scene.Render(delta, buffer)` is this call with spp = 1.
- * rgba may be NULL (accumulate only).                                                      */
+ * rgba may be NULL (accumulate only).
+ * Render-ahead (mfx_options.render_ahead = K > 1, one device, part_count 1): a call with spp = 1
+ * whose global sample is not held traces the next K samples in one batched pass (each sample's
+ * 1-spp image kept in its own FP64 plane, K x 24 B per pixel of HBM) and the following K - 1
+ * calls only add their plane to the film and post it. Every frame's bytes equal the one-sample
+ * path's (a sample's image depends only on the seed and its global index); the cost is one call
+ * in K taking the batch's time. mfx_stats: the batch call reports the K samples' rays and device
+ * time, the others 0 rays in 0 s.                                                          */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
 /* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */

@@ -24,7 +24,7 @@ MFX_F_WAVEFRONT = 8
 MFX_F_FLATTEN = 16
 MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
-MFX_ABI_VERSION = 3
+MFX_ABI_VERSION = 4
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -55,7 +55,7 @@ class MfxSceneDesc(C.Structure):
 class MfxOptions(C.Structure):
     _fields_ = [("seed", C.c_uint64), ("device", C.c_int32), ("flags", C.c_int32),
                 ("part_index", C.c_int32), ("part_count", C.c_int32),
-                ("ndevices", C.c_int32), ("reserved", C.c_int32), ("devices", C.POINTER(C.c_int32))]
+                ("ndevices", C.c_int32), ("render_ahead", C.c_int32), ("devices", C.POINTER(C.c_int32))]
 
 
 class MfxInstance(C.Structure):

@@ -132,6 +132,12 @@ struct mfx_ctx {
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     double* d_vscratch = nullptr;    // megakernel: per-lane vertex records [max_depth + 1][6][grid * 256]
     double* d_albedo = nullptr;      // [nmat][3]
+    // render-ahead (mfx_options.render_ahead): one-sample render calls take their sample's image
+    // from planes a batched wavefront trace filled for the next render_ahead samples
+    int render_ahead = 0;
+    double* d_ahead = nullptr;       // [ahead_cap][3][npix]
+    int ahead_cap = 0;               // planes allocated
+    int64_t ahead_base = 0, ahead_n = 0;  // global samples [ahead_base, ahead_base + ahead_n) held
     bool diag_iter = false;
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
@@ -160,7 +166,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_ahead};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     for (hipEvent_t e : c->it_ev)
@@ -339,6 +345,8 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         return fail(MFX_E_INVALID, "mfx_create: bad sample partition");
     if (opt->ndevices < 0 || opt->ndevices > MFX_MAX_DEVICES || (opt->ndevices > 0 && !opt->devices))
         return fail(MFX_E_INVALID, "mfx_create: bad device list");
+    if (opt->render_ahead < 0 || opt->render_ahead > MFX_MAX_RENDER_AHEAD)
+        return fail(MFX_E_INVALID, "mfx_create: render_ahead out of range");
     int ndev = 0;
     HIPCHECK(hipGetDeviceCount(&ndev));
     std::vector<int> devlist;
@@ -369,6 +377,7 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         d->api_part_count = opt->part_count;
     };
     init(c, 0);
+    c->render_ahead = opt->render_ahead;
     int rc = ctx_setup(c);
     if (rc) {
         free_ctx(c);
@@ -536,7 +545,7 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
 // max_depth extension rays of PathIntegrator.TraceRay (Integrators.fs:107-137), one bounce of
 // every live path per iteration — then k_resolve adds its finished paths to their pixels. Every
 // launch count is known up front, so the whole call is enqueued without a host round trip.
-static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
+static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes = nullptr) {
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
@@ -565,6 +574,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base) {
     P.spill = c->d_spill;
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
+    P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
@@ -852,20 +862,77 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     return mfx_sync(c);
 }
 
+// Render-ahead (mfx_options.render_ahead = K > 1, one device, whole sample set): a one-sample
+// render call whose global sample is not held traces the next K samples in one batched wavefront
+// pass, k_resolve writing each sample's 1-spp image to its own plane; that call and the next K - 1
+// take their plane. A sample's image depends only on (seed, global sample index), so the film and
+// every RGBA8 frame are the bits the one-sample-per-call path gives (tests/test_gpu_render_ahead.py);
+// mfx_reset clears the film, not the sample sequence, so held planes stay valid across it. The
+// batch's rays and device time are reported by the call that traced it; the others trace nothing
+// and report 0 rays in 0 device time.
+static int ahead_plane(mfx_ctx* c, double** plane) {
+    const int64_t s = c->next_sample;
+    if (!(c->ahead_n > 0 && s >= c->ahead_base && s < c->ahead_base + c->ahead_n)) {
+        const size_t pb = 3 * sizeof(double) * (size_t)c->npix;
+        int k = c->render_ahead;
+        if (k > c->ahead_cap) {
+            if (c->d_ahead) (void)hipFree(c->d_ahead);
+            c->d_ahead = nullptr;
+            c->ahead_cap = 0;
+            c->ahead_n = 0;
+            size_t fr = 0, tot = 0;
+            HIPCHECK(hipMemGetInfo(&fr, &tot));
+            const int fit = (int)std::min<size_t>((size_t)k, fr / 4 / pb);  // at most a quarter of the free HBM
+            if (fit < 2) return fail(MFX_E_NOMEM, "render_ahead: no room for two sample planes");
+            HIPCHECK(hipMalloc((void**)&c->d_ahead, (size_t)fit * pb));
+            c->ahead_cap = fit;
+        }
+        k = std::min(k, c->ahead_cap);
+        HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
+        HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
+        c->mega_last = false;
+        const int rc = wf_trace(c, k, s, c->d_ahead);
+        if (rc) return rc;
+        c->ahead_base = s;
+        c->ahead_n = k;
+    } else {  // held: nothing traced by this call
+        HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
+        HIPCHECK(hipEventRecord(c->ev0, c->stream));
+        HIPCHECK(hipEventRecord(c->ev1, c->stream));
+        c->ev_valid = true;
+        c->it_recorded = 0;
+        c->generations = 0;
+        c->mega_last = false;
+    }
+    *plane = c->d_ahead + (s - c->ahead_base) * 3 * c->npix;
+    return MFX_OK;
+}
+
 int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     if (!c) return fail(MFX_E_INVALID, "null context");
     if (c->api_part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
-    int rc = mfx_accum_clear(c);
-    if (rc) return rc;
-    rc = mfx_trace_accumulate(c, spp, c->next_sample);
-    if (rc) return rc;
-    c->next_sample += spp;
-    if (!c->peers.empty() || !c->comms.empty()) {
-        rc = mfx_accum_reduce(c);
+    if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
+    const double* frame = c->d_accum;
+    if (spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty()) {
+        HIPCHECK(hipSetDevice(c->device));
+        double* plane = nullptr;
+        const int rc = ahead_plane(c, &plane);
         if (rc) return rc;
+        frame = plane;
+        c->next_sample += 1;
+    } else {
+        int rc = mfx_accum_clear(c);
+        if (rc) return rc;
+        rc = mfx_trace_accumulate(c, spp, c->next_sample);
+        if (rc) return rc;
+        c->next_sample += spp;
+        if (!c->peers.empty() || !c->comms.empty()) {
+            rc = mfx_accum_reduce(c);
+            if (rc) return rc;
+        }
     }
     c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
-    HIPCHECK(mfx_launch_film_post(c->d_accum, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
+    HIPCHECK(mfx_launch_film_post(frame, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
                                   rgba ? c->d_rgba : nullptr, c->stream));
     if (rgba)
         HIPCHECK(hipMemcpyAsync(rgba, c->d_rgba, 4 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));

@@ -569,9 +569,18 @@ __device__ __forceinline__ float f_round_up(double x) {
     return f;
 }
 
+#ifndef MFX_NEAR_FAR_PLANES
+#define MFX_NEAR_FAR_PLANES 0  // 1: node steps read each axis's near / far planes by the ray's direction signs
+#endif
+
 // FP32 ray for the cluster-BVH slab tests
 struct RayF {
     float ix, iy, iz, oix, oiy, oiz;
+#if MFX_NEAR_FAR_PLANES
+    // byte offsets in an MfxNode of each axis's near-plane column (lo if the direction component
+    // is >= +0, else hi); the far plane's column is the other one (offset ^ 16)
+    uint32_t px, py, pz;
+#endif
 };
 __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
     // tiny direction components clamped so 1/d stays finite (no 0*inf NaNs)
@@ -583,6 +592,12 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
     RayF r;
     r.ix = 1.0f / dx; r.iy = 1.0f / dy; r.iz = 1.0f / dz;
     r.oix = (float)o.x * r.ix; r.oiy = (float)o.y * r.iy; r.oiz = (float)o.z * r.iz;
+#if MFX_NEAR_FAR_PLANES
+    // the sign of 1/d is the sign of the clamped d (-0.0 -> -tiny: hi is near)
+    r.px = (__float_as_uint(r.ix) >> 31) << 4;
+    r.py = 32u | ((__float_as_uint(r.iy) >> 31) << 4);
+    r.pz = 64u | ((__float_as_uint(r.iz) >> 31) << 4);
+#endif
     return r;
 }
 
@@ -684,6 +699,61 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
+#if MFX_NEAR_FAR_PLANES
+    // Each axis's slab values are read in (near, far) order: the near plane is lo for a direction
+    // component >= 0, hi otherwise, chosen by the load's per-lane column offset (RayF::px..pz).
+    // For a box with lo <= hi the rounded values keep that order (fma is monotone in the plane,
+    // the factor's sign fixed), so near = min(a0, a1) and far = max(a0, a1) bit for bit and the
+    // per-axis min / max pairs disappear; the empty child (lo = hi = FLT_MAX) still never hits.
+    // The slab FMAs run two children per v_pk_fma_f32.
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    float4 nxv, fxv, nyv, fyv, nzv, fzv;
+    int4 ch;
+    const uint32_t nb = (uint32_t)node * 128u;
+    if (TOP && node < tn.ntop) {
+        // LDS column c of node n sits at byte n * 128 + ((c ^ sw) << 4) (top_col)
+        const uint32_t sw = (((uint32_t)node >> 1) & 7u) << 4;
+        const char* t = (const char*)tn.lds + nb;
+        nxv = *(const float4*)(t + (r.px ^ sw)); fxv = *(const float4*)(t + (r.px ^ 16u ^ sw));
+        nyv = *(const float4*)(t + (r.py ^ sw)); fyv = *(const float4*)(t + (r.py ^ 16u ^ sw));
+        nzv = *(const float4*)(t + (r.pz ^ sw)); fzv = *(const float4*)(t + (r.pz ^ 16u ^ sw));
+        const float4 c4 = *(const float4*)(t + (96u ^ sw));
+        ch = make_int4(__float_as_int(c4.x), __float_as_int(c4.y), __float_as_int(c4.z), __float_as_int(c4.w));
+    } else {
+        const char* __restrict__ g = (const char*)nodes;
+        nxv = *(const float4*)(g + (nb | r.px)); fxv = *(const float4*)(g + (nb | (r.px ^ 16u)));
+        nyv = *(const float4*)(g + (nb | r.py)); fyv = *(const float4*)(g + (nb | (r.py ^ 16u)));
+        nzv = *(const float4*)(g + (nb | r.pz)); fzv = *(const float4*)(g + (nb | (r.pz ^ 16u)));
+        ch = *(const int4*)(g + nb + 96u);
+    }
+    const f2 ix2 = {r.ix, r.ix}, iy2 = {r.iy, r.iy}, iz2 = {r.iz, r.iz};
+    const f2 ox2 = {-r.oix, -r.oix}, oy2 = {-r.oiy, -r.oiy}, oz2 = {-r.oiz, -r.oiz};
+    f2 An[3][2], Af[3][2];
+    An[0][0] = __builtin_elementwise_fma((f2){nxv.x, nxv.y}, ix2, ox2);
+    An[0][1] = __builtin_elementwise_fma((f2){nxv.z, nxv.w}, ix2, ox2);
+    Af[0][0] = __builtin_elementwise_fma((f2){fxv.x, fxv.y}, ix2, ox2);
+    Af[0][1] = __builtin_elementwise_fma((f2){fxv.z, fxv.w}, ix2, ox2);
+    An[1][0] = __builtin_elementwise_fma((f2){nyv.x, nyv.y}, iy2, oy2);
+    An[1][1] = __builtin_elementwise_fma((f2){nyv.z, nyv.w}, iy2, oy2);
+    Af[1][0] = __builtin_elementwise_fma((f2){fyv.x, fyv.y}, iy2, oy2);
+    Af[1][1] = __builtin_elementwise_fma((f2){fyv.z, fyv.w}, iy2, oy2);
+    An[2][0] = __builtin_elementwise_fma((f2){nzv.x, nzv.y}, iz2, oz2);
+    An[2][1] = __builtin_elementwise_fma((f2){nzv.z, nzv.w}, iz2, oz2);
+    Af[2][0] = __builtin_elementwise_fma((f2){fzv.x, fzv.y}, iz2, oz2);
+    Af[2][1] = __builtin_elementwise_fma((f2){fzv.z, fzv.w}, iz2, oz2);
+    float d[4];
+    int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    int nh = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const int p = k >> 1, e = k & 1;
+        const float n = fmaxf(fmaxf(An[0][p][e], An[1][p][e]), fmaxf(An[2][p][e], 0.0f));
+        const float f = fminf(fminf(Af[0][p][e], Af[1][p][e]), fminf(Af[2][p][e], tlim));
+        const bool h = n <= f;
+        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
+        nh += h ? 1 : 0;
+    }
+#else
     float4 lx, hx, ly, hy, lz, hz;
     int4 ch;
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
@@ -729,6 +799,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         d[k] = h ? (FAR ? -f : n) : __builtin_inff();
         nh += h ? 1 : 0;
     }
+#endif
     cswap(d[0], c[0], d[1], c[1]);
     cswap(d[2], c[2], d[3], c[3]);
     cswap(d[0], c[0], d[2], c[2]);

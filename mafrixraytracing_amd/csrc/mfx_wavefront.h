@@ -68,6 +68,8 @@ struct WfParams {
     MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
     MfxCamera cam;
     double* accum;  // [3][w*h]
+    double* planes; // non-null: k_resolve writes each sample's 1-spp image to its own [3][w*h] plane
+                    // (plane = the sample's index in the call) instead of adding to accum
     // path slots (SoA)
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
     double *dx, *dy, *dz;  // ray direction

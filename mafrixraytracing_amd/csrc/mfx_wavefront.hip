@@ -747,6 +747,35 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     }
 }
 
+// One finished path's radiance: its recorded vertices folded from the deepest lit one back to the
+// camera (f starts as TraceRay below the deepest lit vertex: Color(), black). False: no lit vertex,
+// the path's radiance is black and nothing is added.
+__device__ __forceinline__ bool resolve_path(const WfParams& P, int64_t j, double& fx, double& fy, double& fz) {
+    const int mask = (P.depth[j] >> WF_LIT_SHIFT) & 0xffff;
+    if (mask == 0) return false;
+    const MfxLight& LT = P.light;
+    for (int v = 31 - __builtin_clz(mask); v >= 0; --v) {
+        const double ei = P.vei[v * P.vstride + j];
+        const double* al = P.albedo + 3 * P.vmat[v * P.vstride + j];
+        // c_v = col = TwoPi * (ei * (INVPI * a)) (Material.fs:36, the expression k_shadow had)
+        const double cx = TWOPI * (ei * (INVPI * al[0]));
+        const double cy = TWOPI * (ei * (INVPI * al[1]));
+        const double cz = TWOPI * (ei * (INVPI * al[2]));
+        double ax = 0.0, ay = 0.0, az = 0.0;
+        if ((mask >> v) & 1) {  // a_v = (cs * (solid * I)) / pdf_li (Integrators.fs:52, Light.fs:52-53)
+            const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
+            const double cs = vl[0], solid = vl[P.vstride];
+            ax = (cs * (solid * LT.color[0])) / LT.pdf;
+            ay = (cs * (solid * LT.color[1])) / LT.pdf;
+            az = (cs * (solid * LT.color[2])) / LT.pdf;
+        }
+        fx = (ax + fx) * cx;
+        fy = (ay + fy) * cy;
+        fz = (az + fz) * cz;
+    }
+    return true;
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_resolve: after a generation, every pixel adds its finished paths' radiance in sample order
 // (PixelIntegrator.Sample: color <- color + TraceRay(...), Integrators.fs:169). A path's radiance
@@ -769,40 +798,35 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     const int64_t npix = (int64_t)P.width * P.height;
     const int64_t pixel = (int64_t)x * P.height + y;
     const int64_t end = P.path_base + P.total;
-    double ax = P.accum[pixel], ay = P.accum[npix + pixel], az = P.accum[2 * npix + pixel];
+    double ax = 0.0, ay = 0.0, az = 0.0;
+    if (!P.planes) {
+        ax = P.accum[pixel];
+        ay = P.accum[npix + pixel];
+        az = P.accum[2 * npix + pixel];
+    }
     for (int64_t smp = P.path_base / per_sample; smp * per_sample < end; ++smp) {
         const int64_t p = smp * per_sample + q;
         if (p < P.path_base || p >= end) continue;
         const int64_t j = p - P.path_base;
+        if (P.planes) {  // render-ahead: this sample's own 1-spp image, 0.0 + its path (as a 1-spp call adds it)
+            double fx = 0.0, fy = 0.0, fz = 0.0;
+            if ((P.state[j] & WF_STATE_MASK) == WF_DONE) resolve_path(P, j, fx, fy, fz);
+            double* pl = P.planes + smp * 3 * npix;
+            pl[pixel] = 0.0 + fx;
+            pl[npix + pixel] = 0.0 + fy;
+            pl[2 * npix + pixel] = 0.0 + fz;
+            continue;
+        }
         if ((P.state[j] & WF_STATE_MASK) == WF_DONE) {
-            const int mask = (P.depth[j] >> WF_LIT_SHIFT) & 0xffff;
-            if (mask == 0) continue;  // no lit vertex: the path's radiance is black
-            const MfxLight& LT = P.light;
-            double fx = 0.0, fy = 0.0, fz = 0.0;  // TraceRay below the deepest lit vertex: Color()
-            for (int v = 31 - __builtin_clz(mask); v >= 0; --v) {
-                const double ei = P.vei[v * P.vstride + j];
-                const double* al = P.albedo + 3 * P.vmat[v * P.vstride + j];
-                // c_v = col = TwoPi * (ei * (INVPI * a)) (Material.fs:36, the expression k_shadow had)
-                const double cx = TWOPI * (ei * (INVPI * al[0]));
-                const double cy = TWOPI * (ei * (INVPI * al[1]));
-                const double cz = TWOPI * (ei * (INVPI * al[2]));
-                double ax = 0.0, ay = 0.0, az = 0.0;
-                if ((mask >> v) & 1) {  // a_v = (cs * (solid * I)) / pdf_li (Integrators.fs:52, Light.fs:52-53)
-                    const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
-                    const double cs = vl[0], solid = vl[P.vstride];
-                    ax = (cs * (solid * LT.color[0])) / LT.pdf;
-                    ay = (cs * (solid * LT.color[1])) / LT.pdf;
-                    az = (cs * (solid * LT.color[2])) / LT.pdf;
-                }
-                fx = (ax + fx) * cx;
-                fy = (ay + fy) * cy;
-                fz = (az + fz) * cz;
+            double fx = 0.0, fy = 0.0, fz = 0.0;
+            if (resolve_path(P, j, fx, fy, fz)) {
+                ax += fx;
+                ay += fy;
+                az += fz;
             }
-            ax += fx;
-            ay += fy;
-            az += fz;
         }
     }
+    if (P.planes) return;
     P.accum[pixel] = ax;
     P.accum[npix + pixel] = ay;
     P.accum[2 * npix + pixel] = az;

@@ -20,11 +20,13 @@ class NativeContext:
 
     def __init__(self, arrays: SceneArrays, seed: int = DEFAULT_SEED, device: int = 0, flags: int = MFX_F_NONE,
                  part_index: int = 0, part_count: int = 1, devices: list[int] | None = None,
-                 instancing: bool = True):
+                 instancing: bool = True, render_ahead: int = 0):
         """devices: drive this list of HIP devices from one context (mfx_options.devices; the
         library's own RCCL reduce sums them into devices[0]); None: the single `device`.
         instancing: a scene with instancing data is created through mfx_create_instanced (two-level
-        traversal; MFX_F_FLATTEN flattens it in the library); False: mfx_create on the world list."""
+        traversal; MFX_F_FLATTEN flattens it in the library); False: mfx_create on the world list.
+        render_ahead: mfx_options.render_ahead (one-sample render calls served from batches of K
+        samples; 0 = off)."""
         self.lib = load_library()
         self.arrays = arrays
         self.w, self.h = arrays.width, arrays.height
@@ -33,7 +35,7 @@ class NativeContext:
         self.devices = list(devices) if devices else [device]
         self._devs = (C.c_int32 * len(self.devices))(*self.devices)
         opt = MfxOptions(seed=seed, device=device, flags=flags, part_index=part_index, part_count=part_count,
-                         ndevices=len(devices) if devices else 0,
+                         ndevices=len(devices) if devices else 0, render_ahead=render_ahead,
                          devices=C.cast(self._devs, C.POINTER(C.c_int32)) if devices else None)
         h = C.c_void_p()
         if inst:

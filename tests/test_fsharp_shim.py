@@ -52,7 +52,7 @@ def _mutated(tmp_path, fname, old, new):
     # an extern whose parameter count differs from the header
     ("Native.fs", "extern int mfx_reset(nativeint ctx)", "extern int mfx_reset(nativeint ctx, int spp)", "parameters"),
     # a struct whose fields do not follow the C layout
-    ("Native.fs", "    val mutable ndevices : int32\n    val mutable reserved : int32\n",
+    ("Native.fs", "    val mutable ndevices : int32\n    val mutable renderAhead : int32\n",
      "    val mutable ndevices : int32\n", "C layout"),
 ])
 def test_checker_catches_binding_errors(tmp_path, fname, old, new, expect):

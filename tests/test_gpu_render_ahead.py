@@ -1,0 +1,85 @@
+"""Render-ahead (mfx_options.render_ahead; DESIGN.md §7 "Scene.Render"): one-sample render calls
+served from a batch of the next K samples traced at once by the wavefront, each sample's 1-spp
+image in its own plane. Every frame must be the bytes of the one-sample-per-call path, which the
+oracle pins (test_gpu_parity.test_film_render_rgba8_matches_oracle_post); here both contexts run
+side by side, and the first frames are also checked against the oracle's film directly."""
+import numpy as np
+import pytest
+
+from conftest import SEED, scene
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("name,w,h,K", [("spot", 67, 37, 4), ("cube_cornell", 48, 27, 5),
+                                         ("spot16_instanced", 40, 24, 3), ("two_spheres_plane", 32, 32, 2)])
+def test_render_ahead_frames_are_the_one_sample_frames(gpu, name, w, h, K):
+    """12 Scene.Render calls with a reset after the 7th and an spp = 2 call in between (traced by
+    the plain path; the next one-sample call still takes its plane from the held batch): identical
+    RGBA8 bytes every call and an identical film."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, w, h)
+    rays_plain = rays_ahead = 0.0
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, render_ahead=K) as c2:
+        for k in range(12):
+            spp = 2 if k == 4 else 1
+            assert np.array_equal(c1.render_rgba8(spp), c2.render_rgba8(spp)), (name, k)
+            rays_plain += c1.stats()[0]
+            rays_ahead += c2.stats()[0]
+            if k == 6:
+                c1.reset()
+                c2.reset()
+        assert np.array_equal(c1.film_mean(), c2.film_mean())
+    assert rays_plain > 0 and rays_ahead > 0
+
+
+def test_render_ahead_stats_account_for_whole_batches(gpu):
+    """The batch call reports K samples' rays and device time; held calls report 0 rays in 0 s;
+    over K calls the rays equal K one-sample calls'."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 64, 36)
+    K = 4
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, render_ahead=K) as c2:
+        plain = []
+        for _ in range(2 * K):
+            c1.render_rgba8(1, want_pixels=False)
+            plain.append(c1.stats()[0])
+        ahead = []
+        for k in range(2 * K):
+            c2.render_rgba8(1, want_pixels=False)
+            r, sec = c2.stats()
+            ahead.append(r)
+            if k % K:
+                assert r == 0 and sec < 1e-4  # events recorded back to back
+            else:
+                assert r > 0 and sec > 0.0
+        assert ahead[0] == sum(plain[:K]) and ahead[K] == sum(plain[K:])
+
+
+def test_render_ahead_matches_oracle_film(gpu, oracle):
+    """Frames 1..5 of a render-ahead context (K = 3: a batch boundary inside) against the oracle's
+    Film.AddSample + PostProcessAndToScreenBuffer, bit for bit."""
+    from mafrixraytracing_amd.abi import dptr
+    from mafrixraytracing_amd.native import NativeContext
+    w, h = 40, 30
+    a = scene("two_spheres_plane", w, h)
+    o = oracle.OracleScene(a)
+    npix = w * h
+    accum, target, fc = np.zeros((npix, 4)), np.zeros((npix, 4)), np.zeros(1)
+    with NativeContext(a, seed=SEED, render_ahead=3) as ctx:
+        for k in range(5):
+            rgba = ctx.render_rgba8(1)
+            fr = o.sample(1, SEED, sample_base=k)
+            oracle.lib().oracle_film_add(dptr(accum), dptr(target), dptr(fc), dptr(fr), npix)
+            assert np.array_equal(rgba, oracle.post_rgba8(target, w, h)), k
+        assert np.array_equal(ctx.film_mean()[:, :3], target[:, :3])
+
+
+def test_render_ahead_option_validated(gpu):
+    from mafrixraytracing_amd.abi import MfxError
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 16, 16)
+    with pytest.raises(MfxError):
+        NativeContext(a, seed=SEED, render_ahead=-1)
+    with pytest.raises(MfxError):
+        NativeContext(a, seed=SEED, render_ahead=1 << 20)
