@@ -264,6 +264,7 @@ type NativePixelIntegrator(shapes : IHitable[], light : INewLight, camera : ICam
             o.partIndex <- 0
             o.partCount <- 1
             o.ndevices <- devices.Length
+            o.renderAhead <- 0  // K > 1: Scene.Render's one-sample calls served from batches of K samples
             o.devices <- (if devices.Length > 0 then hd.AddrOfPinnedObject() else 0n)
             let mutable c = 0n
             check (Api.mfx_create(&d, &o, &c)) "mfx_create"   // deep copy: the arrays are unpinned after
