@@ -12,9 +12,9 @@ OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o run -- \
-    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline "$@" > $OUT/bench_trace.log 2>&1
+    python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-render-api "$@" > $OUT/bench_trace.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o run -- \
-    python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats "$@" > $OUT/bench_fetch.log 2>&1
+    python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats --no-render-api "$@" > $OUT/bench_fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o run -- \
-    python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats "$@" > $OUT/bench_write.log 2>&1
+    python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats --no-render-api "$@" > $OUT/bench_write.log 2>&1
 python3 $R/scripts/summarize_profile.py $OUT "$@"
