@@ -537,6 +537,7 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.cam = c->host.camera;
     P.accum = c->d_accum;
     P.albedo = c->d_albedo;
+    P.nmat = (int32_t)(c->host.albedo.size() / 3);
 }
 
 // The wavefront pipeline. The frame's path indices (sample-major, 8x8 tiles) are cut into

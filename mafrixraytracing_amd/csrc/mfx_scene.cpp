@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <thread>
 
 namespace {
 
@@ -156,11 +157,13 @@ struct NetSort {
 };
 
 // ---- reference heap BVH: leaf grouping only ------------------------------------------------
+// Subtrees are independent: each sorts only its own index range (keys / tmp are indexed by the
+// range, not from 0), so the two halves of the top splits run on their own host threads and their
+// leaves are concatenated left to right — the same leaves, in the same order, as the sequential
+// recursion (the introsort of every range is unchanged).
 struct RefBvh {
     const std::vector<Box>& pb;
     std::vector<int32_t>& idx;
-    std::vector<int32_t>& lf;
-    std::vector<int32_t>& lc;
     std::vector<double> keys;
     std::vector<int32_t> tmp;
 
@@ -169,8 +172,9 @@ struct RefBvh {
         for (int k = 1; k < count; ++k) b = join(b, pb[idx[first + k]]);
         return b;
     }
-    // Subdivide (BvhNode.fs:42-61), visiting leaves left to right
-    void subdivide(int first, int count, Box b) {
+    // Subdivide (BvhNode.fs:42-61), visiting leaves left to right; `par` more levels split onto
+    // a second thread (ranges of at least 8,192 primitives)
+    void subdivide(int first, int count, Box b, std::vector<int32_t>& lf, std::vector<int32_t>& lc, int par) {
         if (count <= 3) {
             lf.push_back(first);
             lc.push_back(count);
@@ -178,19 +182,30 @@ struct RefBvh {
         }
         D3 d = sub(b.hi, b.lo);  // MaximumExtent, Aggregate.fs:29-36
         int axis = (d.x > d.y && d.x > d.z) ? 0 : (d.y > d.z ? 1 : 2);
+        double* kk = keys.data() + first;
+        int32_t* tt = tmp.data() + first;
         for (int k = 0; k < count; ++k) {
             int p = idx[first + k];
             const Box& q = pb[p];
             D3 c = add(q.lo, scale(sub(q.hi, q.lo), 0.5));
-            keys[k] = comp(c, axis);
-            tmp[k] = p;
+            kk[k] = comp(c, axis);
+            tt[k] = p;
         }
-        NetSort::sort(keys.data(), tmp.data(), count);
-        std::memcpy(&idx[first], tmp.data(), sizeof(int32_t) * count);
+        NetSort::sort(kk, tt, count);
+        std::memcpy(&idx[first], tt, sizeof(int32_t) * count);
         int left = count / 2;
         Box bl = bound(first, left), br = bound(first + left, count - left);
-        subdivide(first, left, bl);
-        subdivide(first + left, count - left, br);
+        if (par > 0 && count >= 8192) {
+            std::vector<int32_t> lf2, lc2;
+            std::thread t([&] { subdivide(first + left, count - left, br, lf2, lc2, par - 1); });
+            subdivide(first, left, bl, lf, lc, par - 1);
+            t.join();
+            lf.insert(lf.end(), lf2.begin(), lf2.end());
+            lc.insert(lc.end(), lc2.begin(), lc2.end());
+        } else {
+            subdivide(first, left, bl, lf, lc, 0);
+            subdivide(first + left, count - left, br, lf, lc, 0);
+        }
     }
 };
 
@@ -707,9 +722,9 @@ bool mfx_build_scene(const mfx_scene_desc* d0, MfxHostScene& s, std::string& err
     s.leaf_count.clear();
     {
         const auto t0 = clock::now();
-        RefBvh rb{pb, s.ref_indices, s.leaf_first, s.leaf_count, std::vector<double>(n), std::vector<int32_t>(n)};
+        RefBvh rb{pb, s.ref_indices, std::vector<double>(n), std::vector<int32_t>(n)};
         Box root = rb.bound(0, n);
-        rb.subdivide(0, n, root);
+        rb.subdivide(0, n, root, s.leaf_first, s.leaf_count, 3);  // up to 8 host threads
         s.ms_ref_bvh = ms_since(t0);
     }
     const int nc = (int)s.leaf_first.size();

@@ -78,6 +78,7 @@ struct WfParams {
     double* vls;           // [vertex][2][stride] a lit vertex's cs = unit . n and solid = |cos_o| A / dist^2
     int64_t vstride;       // slots per vertex-record row (the allocated pool)
     const double* albedo;  // [nmat][3] Lambert albedo per material (Material.fs:29-37)
+    int32_t nmat;
     uint64_t* key;         // RNG key of the path
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)

@@ -747,33 +747,79 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     }
 }
 
-// One finished path's radiance: its recorded vertices folded from the deepest lit one back to the
-// camera (f starts as TraceRay below the deepest lit vertex: Color(), black). False: no lit vertex,
-// the path's radiance is black and nothing is added.
-__device__ __forceinline__ bool resolve_path(const WfParams& P, int64_t j, double& fx, double& fy, double& fz) {
-    const int mask = (P.depth[j] >> WF_LIT_SHIFT) & 0xffff;
-    if (mask == 0) return false;
-    const MfxLight& LT = P.light;
-    for (int v = 31 - __builtin_clz(mask); v >= 0; --v) {
-        const double ei = P.vei[v * P.vstride + j];
-        const double* al = P.albedo + 3 * P.vmat[v * P.vstride + j];
-        // c_v = col = TwoPi * (ei * (INVPI * a)) (Material.fs:36, the expression k_shadow had)
-        const double cx = TWOPI * (ei * (INVPI * al[0]));
-        const double cy = TWOPI * (ei * (INVPI * al[1]));
-        const double cz = TWOPI * (ei * (INVPI * al[2]));
-        double ax = 0.0, ay = 0.0, az = 0.0;
-        if ((mask >> v) & 1) {  // a_v = (cs * (solid * I)) / pdf_li (Integrators.fs:52, Light.fs:52-53)
-            const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
-            const double cs = vl[0], solid = vl[P.vstride];
-            ax = (cs * (solid * LT.color[0])) / LT.pdf;
-            ay = (cs * (solid * LT.color[1])) / LT.pdf;
-            az = (cs * (solid * LT.color[2])) / LT.pdf;
+#ifndef WF_RES_VERTS
+#define WF_RES_VERTS 4  // vertices k_resolve loads in one round (max_depth 3 paths); deeper ones in a loop
+#endif
+#ifndef WF_RES_MAT_LDS
+#define WF_RES_MAT_LDS 256  // materials whose albedo k_resolve keeps in LDS (more: read from global memory)
+#endif
+#ifndef WF_RES_SAMPLES
+#define WF_RES_SAMPLES 1  // samples of a pixel whose path records k_resolve loads together
+#endif
+
+// One path's vertex records as loaded by k_resolve: for the first WF_RES_VERTS vertices up to its
+// deepest lit one, ei and the material; cs and solid for the lit ones. Loaded in one round of
+// independent loads (the state and depth words came in the rounds before), so a path costs three
+// dependent memory round trips instead of one per vertex and field.
+struct PathRec {
+    int mask;  // lit-vertex mask (0: black path, or not a finished path of this generation)
+    double ei[WF_RES_VERTS], cs[WF_RES_VERTS], so[WF_RES_VERTS];
+    int mat[WF_RES_VERTS];
+};
+__device__ __forceinline__ void load_path(const WfParams& P, int64_t j, int mask, PathRec& R) {
+    R.mask = mask;
+    if (mask == 0) return;
+    const int top = 31 - __builtin_clz(mask);
+#pragma unroll
+    for (int v = 0; v < WF_RES_VERTS; ++v) {
+        R.ei[v] = 0.0; R.cs[v] = 0.0; R.so[v] = 0.0; R.mat[v] = 0;
+        if (v <= top) {
+            R.ei[v] = P.vei[v * P.vstride + j];
+            R.mat[v] = P.vmat[v * P.vstride + j];
+            if ((mask >> v) & 1) {
+                const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
+                R.cs[v] = vl[0];
+                R.so[v] = vl[P.vstride];
+            }
         }
-        fx = (ax + fx) * cx;
-        fy = (ay + fy) * cy;
-        fz = (az + fz) * cz;
     }
-    return true;
+}
+// The path's radiance: its vertices folded from the deepest lit one back to the camera, f starting
+// as TraceRay below the deepest lit vertex (Color(), black):
+//   c_v = col = TwoPi * (ei * (INVPI * a))            (Material.fs:36, the expression k_shadow had)
+//   a_v = (cs * (solid * I)) / pdf_li, 0 if unlit     (Integrators.fs:52, Light.fs:52-53)
+//   f  <- (a_v + f) * c_v                             (Integrators.fs:135-136, pdf = 1)
+__device__ __forceinline__ void fold_vertex(const WfParams& P, bool lit, double ei, int mat, double cs, double so,
+                                            const double* alb_lds, double& fx, double& fy, double& fz) {
+    const MfxLight& LT = P.light;
+    const double* al = mat < WF_RES_MAT_LDS ? alb_lds + 3 * mat : P.albedo + 3 * mat;
+    const double cx = TWOPI * (ei * (INVPI * al[0]));
+    const double cy = TWOPI * (ei * (INVPI * al[1]));
+    const double cz = TWOPI * (ei * (INVPI * al[2]));
+    double ax = 0.0, ay = 0.0, az = 0.0;
+    if (lit) {
+        ax = (cs * (so * LT.color[0])) / LT.pdf;
+        ay = (cs * (so * LT.color[1])) / LT.pdf;
+        az = (cs * (so * LT.color[2])) / LT.pdf;
+    }
+    fx = (ax + fx) * cx;
+    fy = (ay + fy) * cy;
+    fz = (az + fz) * cz;
+}
+__device__ __forceinline__ void fold_path(const WfParams& P, int64_t j, const PathRec& R, const double* alb_lds,
+                                          double& fx, double& fy, double& fz) {
+    const int top = 31 - __builtin_clz(R.mask);
+    // vertices deeper than the batched records (max_depth >= WF_RES_VERTS), read here
+    for (int v = top; v >= WF_RES_VERTS; --v) {
+        const bool lit = (R.mask >> v) & 1;
+        const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
+        fold_vertex(P, lit, P.vei[v * P.vstride + j], P.vmat[v * P.vstride + j], lit ? vl[0] : 0.0,
+                    lit ? vl[P.vstride] : 0.0, alb_lds, fx, fy, fz);
+    }
+    // the batched ones, indices known at compile time (the records stay in registers)
+#pragma unroll
+    for (int v = WF_RES_VERTS - 1; v >= 0; --v)
+        if (v <= top) fold_vertex(P, (R.mask >> v) & 1, R.ei[v], R.mat[v], R.cs[v], R.so[v], alb_lds, fx, fy, fz);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -784,8 +830,16 @@ __device__ __forceinline__ bool resolve_path(const WfParams& P, int64_t j, doubl
 // exact), black below the last lit vertex, and l = 0 at an occluded or unlit one. One thread per
 // tile-ordered pixel position q; for a fixed sample, consecutive q are consecutive slots, so the
 // loads are coalesced. No atomics: one thread owns each pixel, generations are stream-ordered.
+// The records of WF_RES_SAMPLES samples are loaded together (state words, then depth words, then
+// vertex records: three rounds of independent loads), then folded and added in sample order.
+// Render-ahead (P.planes): each sample's 1-spp image goes to its own plane, 0.0 + its path (what a
+// one-sample call adds to its zeroed accumulator), 0.0 for a black one.
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
+    __shared__ double alb[3 * WF_RES_MAT_LDS];
+    const int nm = P.nmat < WF_RES_MAT_LDS ? P.nmat : WF_RES_MAT_LDS;
+    for (int i = threadIdx.x; i < 3 * nm; i += blockDim.x) alb[i] = P.albedo[i];
+    __syncthreads();
     const int tiles_x = (P.width + 7) >> 3;
     const int64_t per_sample = (int64_t)tiles_x * ((P.height + 7) >> 3) * 64;
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -804,22 +858,36 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         ay = P.accum[npix + pixel];
         az = P.accum[2 * npix + pixel];
     }
-    for (int64_t smp = P.path_base / per_sample; smp * per_sample < end; ++smp) {
-        const int64_t p = smp * per_sample + q;
-        if (p < P.path_base || p >= end) continue;
-        const int64_t j = p - P.path_base;
-        if (P.planes) {  // render-ahead: this sample's own 1-spp image, 0.0 + its path (as a 1-spp call adds it)
-            double fx = 0.0, fy = 0.0, fz = 0.0;
-            if ((P.state[j] & WF_STATE_MASK) == WF_DONE) resolve_path(P, j, fx, fy, fz);
-            double* pl = P.planes + smp * 3 * npix;
-            pl[pixel] = 0.0 + fx;
-            pl[npix + pixel] = 0.0 + fy;
-            pl[2 * npix + pixel] = 0.0 + fz;
-            continue;
+    constexpr int U = WF_RES_SAMPLES;
+    for (int64_t smp0 = P.path_base / per_sample; smp0 * per_sample < end; smp0 += U) {
+        int64_t jv[U];
+        bool in[U];
+        int sw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t p = (smp0 + u) * per_sample + q;
+            in[u] = p >= P.path_base && p < end;
+            jv[u] = in[u] ? p - P.path_base : 0;
+            sw[u] = in[u] ? P.state[jv[u]] : 0;
         }
-        if ((P.state[j] & WF_STATE_MASK) == WF_DONE) {
+        int mask[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            mask[u] = (sw[u] & WF_STATE_MASK) == WF_DONE ? (P.depth[jv[u]] >> WF_LIT_SHIFT) & 0xffff : 0;
+        PathRec R[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) load_path(P, jv[u], mask[u], R[u]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if (!in[u]) continue;
             double fx = 0.0, fy = 0.0, fz = 0.0;
-            if (resolve_path(P, j, fx, fy, fz)) {
+            if (R[u].mask) fold_path(P, jv[u], R[u], alb, fx, fy, fz);
+            if (P.planes) {
+                double* pl = P.planes + (smp0 + u) * 3 * npix;
+                pl[pixel] = 0.0 + fx;
+                pl[npix + pixel] = 0.0 + fy;
+                pl[2 * npix + pixel] = 0.0 + fz;
+            } else if (R[u].mask) {  // a path with no lit vertex adds nothing
                 ax += fx;
                 ay += fy;
                 az += fz;

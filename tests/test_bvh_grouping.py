@@ -168,7 +168,23 @@ def test_all_equal_keys_follow_dotnet_order(oracle):
     assert np.array_equal(gi, pi)
 
 
-@pytest.mark.parametrize("name", ["cornell", "cube_cornell", "spot", "two_spheres_plane"])
+@pytest.mark.parametrize("n,quant", [(20000, 0), (40000, 6)])
+def test_threaded_grouping_matches_oracle(oracle, n, quant):
+    """Ranges of >= 8,192 primitives split onto host threads (mfx_scene.cpp RefBvh): the leaves and
+    their order equal the oracle's sequential recursion, with and without tied keys."""
+    from mafrixraytracing_amd.abi import build_leaves
+    rng = np.random.default_rng(n + quant)
+    c = rng.uniform(-1, 1, (n, 1, 3))
+    if quant:
+        c = np.round(c * quant) / quant
+    verts = c + rng.uniform(-0.05, 0.05, (n, 3, 3))
+    a = tri_scene(verts)
+    oi, of, oc = oracle.OracleScene(a).bvh_leaves()
+    gi, gf, gc, _ = build_leaves(a)
+    assert np.array_equal(gi, oi) and np.array_equal(gf, of) and np.array_equal(gc, oc)
+
+
+@pytest.mark.parametrize("name", ["cornell", "cube_cornell", "spot", "two_spheres_plane", "renault", "spot16"])
 def test_scene_grouping_matches_oracle(oracle, name):
     from mafrixraytracing_amd.abi import build_leaves
     a = scene(name, 8, 8)
