@@ -189,7 +189,8 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * calls only add their plane to the film and post it. Every frame's bytes equal the one-sample
  * path's (a sample's image depends only on the seed and its global index); the cost is one call
  * in K taking the batch's time. mfx_stats: the batch call reports the K samples' rays and device
- * time, the others 0 rays in 0 s.                                                          */
+ * time, the others 0 rays in 0 s. K is cut to the planes that fit in a quarter of the free HBM;
+ * when not even two fit, the context renders one sample per call as without render-ahead.  */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
 /* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */

@@ -871,7 +871,8 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
 // mfx_reset clears the film, not the sample sequence, so held planes stay valid across it. The
 // batch's rays and device time are reported by the call that traced it; the others trace nothing
 // and report 0 rays in 0 device time.
-static int ahead_plane(mfx_ctx* c, double** plane) {
+// Makes the context hold the plane of sample next_sample (tracing the next batch if needed).
+static int ahead_ensure(mfx_ctx* c) {
     const int64_t s = c->next_sample;
     if (!(c->ahead_n > 0 && s >= c->ahead_base && s < c->ahead_base + c->ahead_n)) {
         const size_t pb = 3 * sizeof(double) * (size_t)c->npix;
@@ -884,8 +885,11 @@ static int ahead_plane(mfx_ctx* c, double** plane) {
             size_t fr = 0, tot = 0;
             HIPCHECK(hipMemGetInfo(&fr, &tot));
             const int fit = (int)std::min<size_t>((size_t)k, fr / 4 / pb);  // at most a quarter of the free HBM
-            if (fit < 2) return fail(MFX_E_NOMEM, "render_ahead: no room for two sample planes");
-            HIPCHECK(hipMalloc((void**)&c->d_ahead, (size_t)fit * pb));
+            if (fit < 2 || hipMalloc((void**)&c->d_ahead, (size_t)fit * pb) != hipSuccess) {
+                c->d_ahead = nullptr;
+                (void)hipGetLastError();
+                return MFX_E_NOMEM;  // the caller renders this call (and the later ones) one sample at a time
+            }
             c->ahead_cap = fit;
         }
         k = std::min(k, c->ahead_cap);
@@ -905,7 +909,6 @@ static int ahead_plane(mfx_ctx* c, double** plane) {
         c->generations = 0;
         c->mega_last = false;
     }
-    *plane = c->d_ahead + (s - c->ahead_base) * 3 * c->npix;
     return MFX_OK;
 }
 
@@ -914,12 +917,15 @@ int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     if (c->api_part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
     const double* frame = c->d_accum;
-    if (spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty()) {
+    const bool ahead = spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty();
+    if (ahead) {
         HIPCHECK(hipSetDevice(c->device));
-        double* plane = nullptr;
-        const int rc = ahead_plane(c, &plane);
-        if (rc) return rc;
-        frame = plane;
+        const int rc = ahead_ensure(c);
+        if (rc == MFX_E_NOMEM) c->render_ahead = 0;  // no room for the planes: render-ahead off for this context
+        else if (rc) return rc;
+    }
+    if (ahead && c->render_ahead > 1) {
+        frame = c->d_ahead + (c->next_sample - c->ahead_base) * 3 * c->npix;
         c->next_sample += 1;
     } else {
         int rc = mfx_accum_clear(c);
