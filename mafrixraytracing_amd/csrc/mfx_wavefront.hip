@@ -38,9 +38,6 @@
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
-#ifndef MFX_HEMI_FP32_SCREEN
-#define MFX_HEMI_FP32_SCREEN 1  // rejection trials decided in FP32 away from the boundary (exact)
-#endif
 
 #ifndef MFX_SHADOW_ORDER
 #define MFX_SHADOW_ORDER 1  // shadow rays' child order: 0 near-first, 1 far-first (by exit distance)
@@ -337,6 +334,85 @@ struct PendShd {
     }
 };
 
+#ifndef MFX_HEMI_WAVE
+#define MFX_HEMI_WAVE 1  // k_shadow: the rejection sampler's stragglers' trials spread over the whole wave
+#endif
+#ifndef MFX_HEMI_WAVE_FIRST
+#define MFX_HEMI_WAVE_FIRST 1  // trials each owner makes alone before the wave shares them (r02bi: 1 vs 2, C3 +0.8 %, C4 +0.6 %, C2 -0.5 %)
+#endif
+
+// GetRandomInUnitSphere(nm) (Material.fs:9-14) for the wave's shading lanes (`own`), the same
+// accepted trial, point and draw count as hemisphere_ball. A lane's loop runs until its first
+// accepted trial (3.8 trials on average), but the wave runs until its slowest lane's (about 16):
+// after a first round in which every owner tries its own first MFX_HEMI_WAVE_FIRST trials, the owners
+// still rejecting share the wave's 64 lanes, m = 2^k consecutive trials each (np * m <= 64), and
+// each owner takes the lowest accepted trial of its round (all lower ones were rejected before).
+// A worker lane draws from the owner's key and draw count (the trial's three draws at their
+// counter positions) and decides with hemi_trial, so p is the owner's own computation's bits.
+// scratch: 64 ints of the wave's LDS (owner lane ids in rank order).
+__device__ __forceinline__ DV hemisphere_ball_wave(bool own, DV nm, uint64_t key, uint32_t& rn, int* scratch) {
+    const int lane = lane_id();
+    DV p = dv(0, 0, 0);
+    bool done = !own;
+    const uint32_t base = rn;  // draws used before trial 0
+    if (own) {  // round 0: the owner's own first MFX_HEMI_WAVE_FIRST trials
+        const float nx = (float)nm.x, ny = (float)nm.y, nz = (float)nm.z;
+        uint32_t r = base;
+        uint64_t z[3 * MFX_HEMI_WAVE_FIRST];
+#pragma unroll
+        for (int i = 0; i < 3 * MFX_HEMI_WAVE_FIRST; ++i) z[i] = rng_bits(key, r);
+        for (int i = 0; i < MFX_HEMI_WAVE_FIRST; ++i)
+            if (hemi_trial(nm, nx, ny, nz, z[3 * i], z[3 * i + 1], z[3 * i + 2], p)) {
+                rn = base + 3 * (i + 1);
+                done = true;
+                break;
+            }
+    }
+    uint32_t next = MFX_HEMI_WAVE_FIRST;  // the owner's next trial index
+    while (true) {
+        const uint64_t pend = __ballot(!done);
+        if (pend == 0) break;
+        const int np = __popcll(pend);
+        int sh = 0;  // trials per pending owner: m = 2^sh, np * m <= 64
+        while ((np << (sh + 1)) <= 64) ++sh;
+        const int rank = __popcll(pend & lanes_below());
+        if (!done) scratch[rank] = lane;
+        wave_lds_sync();
+        const int slot = lane >> sh, t = lane & ((1 << sh) - 1);
+        const bool work = slot < np;
+        const int owner = work ? scratch[slot] : lane;
+        wave_lds_sync();
+        const uint64_t k = __shfl(key, owner);
+        const uint32_t b = (uint32_t)__shfl((int)base, owner);
+        const uint32_t nt = (uint32_t)__shfl((int)next, owner);
+        const DV q = dv(__shfl(nm.x, owner), __shfl(nm.y, owner), __shfl(nm.z, owner));
+        bool acc = false;
+        DV pt = dv(0, 0, 0);
+        if (work) {
+            uint32_t r = b + 3 * (nt + (uint32_t)t);
+            const uint64_t zx = rng_bits(k, r);
+            const uint64_t zy = rng_bits(k, r);
+            const uint64_t zz = rng_bits(k, r);
+            acc = hemi_trial(q, (float)q.x, (float)q.y, (float)q.z, zx, zy, zz, pt);
+        }
+        const uint64_t A = __ballot(acc);
+        const int first_lane = done ? lane : (rank << sh);
+        const uint64_t seg = done ? 0 : (A >> first_lane) & (sh == 6 ? ~0ULL : ((1ULL << (1 << sh)) - 1));
+        const int src = done ? lane : first_lane + (seg ? __builtin_ctzll(seg) : 0);
+        const DV ps = dv(__shfl(pt.x, src), __shfl(pt.y, src), __shfl(pt.z, src));
+        if (!done) {
+            if (seg) {
+                p = ps;
+                rn = base + 3 * (next + (uint32_t)__builtin_ctzll(seg) + 1);
+                done = true;
+            } else {
+                next += 1u << sh;
+            }
+        }
+    }
+    return p;
+}
+
 // ------------------------------------------------------------------------------------------------
 // k_extend: closest hit for NEED_EXT slots; in a generation's first iteration FREE slots start paths
 // ------------------------------------------------------------------------------------------------
@@ -573,35 +649,38 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // ---- shade up to 64 listed hits with all lanes: one vertex of PathIntegrator.TraceRay
                 //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
                 const int cnt = nshade < 64 ? nshade : 64;
-                if (lane < cnt) {
-                    const int j = shl[lane] & 0x7fffffff;
-                    const bool first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
+                const bool own = lane < cnt;
+                int j = 0, mat = 0;
+                bool first = false;
+                DV hp = dv(0, 0, 0), nm = dv(0, 0, 0);
+                uint64_t key = 0;
+                uint32_t rn = 0;
+                if (own) {
+                    j = shl[lane] & 0x7fffffff;
+                    first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
                     const int slot = shl[WF_SHD_LIST + lane];
-                    const DV hp = dv(P.ox[j], P.oy[j], P.oz[j]);
+                    hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
-                    DV nm;
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
                     else nm = ld3(sh.n);
-                    const uint64_t key = P.key[j];
-                    uint32_t rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
-                    // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
+                    mat = sh.material;
+                    key = P.key[j];
+                    rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
+                }
+                // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
+#if MFX_HEMI_WAVE && !defined(MFX_DIAG_ONE_TRIAL)
+                wave_lds_sync();  // every owner has read its shl entries: shl[0, 64) is the sampler's scratch
+                const DV p = hemisphere_ball_wave(own, nm, key, rn, shl);
+#endif
+                if (own) {
 #if defined(MFX_DIAG_ONE_TRIAL)  // timing experiment only: the first trial, mirrored into the hemisphere
                     DV p = dv(rng_next(key, rn) * 2.0 - 1.0, rng_next(key, rn) * 2.0 - 1.0, rng_next(key, rn) * 2.0 - 1.0);
                     if (vdot(nm, p) <= 0.) p = vmul(p, -1.0);
-#elif MFX_HEMI_FP32_SCREEN
+#elif !MFX_HEMI_WAVE
                     const DV p = hemisphere_ball(nm, key, rn);
-#else
-                    DV p = dv(20, 20, 20);
-                    while (vdot(p, p) >= 1.0 || vdot(nm, p) <= 0.) {
-                        const double rx = rng_next(key, rn);
-                        const double ry = rng_next(key, rn);
-                        const double rz = rng_next(key, rn);
-                        p = vsub(vmul(dv(rx, ry, rz), 2.0), dv(1, 1, 1));
-                    }
 #endif
                     const DV wi = vnormalize(p);
                     const double ei = vdot(nm, wi);
-                    const double* a = sh.albedo;
                     // NewAreaLight.Sample_Li — Light.fs:42-47,57-59; Rect/Triangle.SamplePoint
                     const MfxLight& LT = P.light;
                     const double sel = rng_next(key, rn);
@@ -629,8 +708,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const int v = P.max_depth - (dw & 0xff);          // this vertex's index
                     // the operands of col = INVPI * a * ei * TwoPi (Material.fs:36), c_v (k_resolve)
                     P.vei[v * P.vstride + j] = ei;
-                    P.vmat[v * P.vstride + j] = sh.material;
-                    (void)a;
+                    P.vmat[v * P.vstride + j] = mat;
                     // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56)
                     // is the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0.
                     // Its operands cs and solid travel with the shadow ray.
