@@ -20,9 +20,9 @@ ctx = NativeContext(a, seed=DEFAULT_SEED)
 res = []
 for k in range(STEPS + 1):
     ctx.accum_clear(); t = time.perf_counter(); ctx.trace_accumulate(SPP, k * SPP); ctx.sync(); dt = time.perf_counter() - t
-    c = ctx.ray_counts(); ms = ctx.last_trace_ms()
-    if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms))
-print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res]}))
+    c = ctx.ray_counts(); ms = ctx.last_trace_ms(); tt = ctx.trace_timing()
+    if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms, tt["total_ms"] - tt["extend_ms"] - tt["shadow_ms"]))
+print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest": [r[2] for r in res]}))
 '''
 
 
@@ -49,7 +49,8 @@ def main():
                 continue
             d = json.loads(p.stdout.strip().splitlines()[-1])
             out[os.path.basename(l)] += d["mrays"]
-            print(os.path.basename(l), "round", r, ["%.1f" % x for x in d["mrays"]], "ms", ["%.2f" % x for x in d["ms"]], flush=True)
+            print(os.path.basename(l), "round", r, ["%.1f" % x for x in d["mrays"]], "ms", ["%.2f" % x for x in d["ms"]],
+                  "rest ms (resolve + memsets)", ["%.3f" % x for x in d.get("rest", [])], flush=True)
     print("SUMMARY", json.dumps({k: (max(v) if v else None) for k, v in out.items()}))
 
 
