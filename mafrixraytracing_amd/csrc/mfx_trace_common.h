@@ -600,6 +600,12 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 #endif
     return r;
 }
+// the same ray from another origin (an instance frame's o - off, or back to the world's o): the
+// direction terms are the ray's own, so only the origin products are recomputed, with make_rayf's
+// expressions (the result is make_rayf(o, d) bit for bit)
+__device__ __forceinline__ void rayf_origin(RayF& r, DV o) {
+    r.oix = (float)o.x * r.ix; r.oiy = (float)o.y * r.iy; r.oiz = (float)o.z * r.iz;
+}
 
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
 
@@ -682,13 +688,13 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
                                           RayF& rf) {
     if (inst >= 0 && sp < inst_sp) {
         inst = -1;
-        rf = make_rayf(o, d);
+        rayf_origin(rf, o);
     }
     if (is_inst_code(node)) {
         inst = ~node & ~MFX_INST_FLAG;
         inst_sp = sp;
         const InstR r = load_inst(S, inst);
-        rf = make_rayf(vsub(o, r.off), d);
+        rayf_origin(rf, vsub(o, r.off));
         node = r.root;
     }
     return node;

@@ -222,7 +222,7 @@ template <bool SHADOW, bool STATS, bool INST, typename ST>
 __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
                                           DiagAcc& dg, bool diag) {
     // the frame of the entry popped at the end of the last round (an instance left or entered)
-    RayF rf;
+    RayF rf{};  // (the frame switch's own ray update is superseded below)
     if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
     // the FP32 ray and the node-test limit are recomputed each round (the same values) rather than
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
