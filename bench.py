@@ -54,9 +54,13 @@ CONFIGS = {
     "C3": ("cube_cornell.xml", 1024, "C3 Cube (12 tris) in the synthetic Cornell box"),
     "C4": ("renault.xml", 32, "C4 Renault12TL (36996 tris) + stage, per-GPU share of 256 spp over 8 GPUs"),
     "C5": ("spot16_instanced.xml", 64,
-           "C5 spot x16 instanced (16 x 5856 tris, two-level BVH) + stage, per-GPU share of 512 spp over 8 GPUs"),
+           "C5 spot x16 instanced (16 x 5856 tris; the library flattens it: its flat image fits the budget) + stage, "
+           "per-GPU share of 512 spp over 8 GPUs"),
+    "C5T": ("spot16_instanced.xml", 64,
+            "C5 spot x16 instanced, two-level BVH forced (MFX_F_TWO_LEVEL) + stage, per-GPU share of 512 spp over 8 GPUs"),
     "C5F": ("spot16.xml", 64, "C5 scene flattened (93696 tris, one BVH) + stage, per-GPU share of 512 spp over 8 GPUs"),
 }
+CONFIG_FLAGS = {"C5T": 32}  # mafrixraytracing_amd.abi.MFX_F_TWO_LEVEL
 
 
 def parse():
@@ -159,7 +163,7 @@ def cpu_baseline(arrays, spp, seed, budget_s):
                       f"per-thread rate x nproc (linear, not measured)"}
 
 
-def render_api(arrays, seed, calls, devices=None, render_ahead=0):
+def render_api(arrays, seed, calls, devices=None, render_ahead=0, flags=0):
     """Scene.Render's call pattern (Scene.fs:331-333): `calls` x mfx_render_rgba8(ctx, 1, buf), each
     one 1-spp frame into the film, ACES/sqrt/RGBA8 post and the RGBA8 readback to host memory.
     Rays from the kernels' counters of every call; wall time per call by the host clock.
@@ -168,9 +172,9 @@ def render_api(arrays, seed, calls, devices=None, render_ahead=0):
     timed calls trace exactly the samples they consume."""
     import numpy as np
     from mafrixraytracing_amd.native import NativeContext
-    ctx = NativeContext(arrays, seed=seed, devices=devices, render_ahead=render_ahead)
-    if render_ahead > 1:
-        calls = max(1, calls // render_ahead) * render_ahead
+    ctx = NativeContext(arrays, seed=seed, devices=devices, render_ahead=render_ahead, flags=flags)
+    if render_ahead > 1:  # whole batches; at least two, so the background batch is in steady state
+        calls = max(2, calls // render_ahead) * render_ahead
     buf = np.empty(arrays.width * arrays.height * 4, dtype=np.uint8)
     import ctypes as C
     bp = buf.ctypes.data_as(C.POINTER(C.c_uint8))
@@ -194,8 +198,73 @@ def render_api(arrays, seed, calls, devices=None, render_ahead=0):
             "ms_per_call_max": round(max(wall) * 1e3, 4),
             "includes": "per call: mfx_render_rgba8(ctx, 1, buf) = trace of 1 spp (all bounces), film add, "
                         "ACES/sqrt/RGBA8 post, 8 MB RGBA8 copy to pageable host memory, synchronize" +
-                        (f"; render-ahead: one call in {render_ahead} traces the next {render_ahead} samples "
-                         "in one wavefront batch, the others add their held sample plane" if render_ahead > 1 else "")}
+                        (f"; render-ahead K = {render_ahead}: the calls take their frames from batches of "
+                         f"{render_ahead} samples traced in one wavefront pass, their film add + post run ahead on "
+                         "the GPU, and the next batch is traced in the background while one is served "
+                         "(the call reporting a batch reports its rays and device time)" if render_ahead > 1 else "")}
+
+
+def sample_api(arrays, seed, spp, calls=2, flags=0):
+    """SURVEY §8(d)'s metric to the letter: Mrays/s over the wall time of mfx_sample(spp) — the trace,
+    the mean kernel and the FP64 x-major RGBA readback (66 MB at 1080p) — per call."""
+    from mafrixraytracing_amd.native import NativeContext
+    with NativeContext(arrays, seed=seed, flags=flags) as ctx:
+        ctx.sample(spp)  # warmup (pool allocation)
+        wall, rays = 0.0, 0.0
+        for _ in range(calls):
+            t0 = time.perf_counter()
+            ctx.sample(spp)
+            wall += time.perf_counter() - t0
+            c = ctx.ray_counts()
+            rays += c[0] + c[1] + c[2]
+    return {"value": round(rays / wall / 1e6, 2), "unit": "Mrays/s", "calls": calls, "spp": spp,
+            "ms_per_call": round(wall / calls * 1e3, 3),
+            "includes": "per call: mfx_sample(ctx, spp, frame) = trace, mean kernel, FP64 RGBA x-major readback "
+                        "to pageable host memory, synchronize"}
+
+
+def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=3, flags=0):
+    """One GPU's share of a strong-scaled job, measured on this GPU: the config's spp split over N
+    GPUs is spp / N samples per GPU per step (C2: 32 / 16 / 8). Timed per N: the share's trace
+    (clear + trace + sync, the step's fixed per-generation costs included), and the library's RCCL
+    reduce of the FP64 accumulator on a devices=[0] context (a 1-rank communicator: its launch and
+    local cost; the xGMI transfer of an N-rank reduce is not in it). predicted_efficiency =
+    (t_1GPU / N) / (t_share + t_reduce): what the N-GPU strong run can reach at most."""
+    from mafrixraytracing_amd.native import NativeContext
+    out = {}
+    with NativeContext(arrays, seed=seed, devices=[0], flags=flags) as rc:
+        for _ in range(3):
+            rc.accum_reduce()
+        rc.sync()
+        t0 = time.perf_counter()
+        n_red = 20
+        for _ in range(n_red):
+            rc.accum_reduce()
+        rc.sync()
+        t_red = (time.perf_counter() - t0) / n_red * 1e3
+    with NativeContext(arrays, seed=seed, flags=flags) as ctx:
+        for n in (2, 4, 8):
+            share = spp // n
+            if share < 1:
+                continue
+            ctx.accum_clear()
+            ctx.trace_accumulate(share, 0)
+            ctx.sync()
+            rays, t0 = 0.0, time.perf_counter()
+            for k in range(steps):
+                ctx.accum_clear()
+                ctx.trace_accumulate(share, (k + 1) * spp)
+                ctx.sync()
+                c = ctx.ray_counts()
+                rays += c[0] + c[1] + c[2]
+            t = (time.perf_counter() - t0) / steps * 1e3
+            out[str(n)] = {"spp_per_gpu": share, "ms_per_step": round(t, 3),
+                           "mrays_per_s_per_gpu": round(rays / steps / (t / 1e3) / 1e6, 2),
+                           "vs_full_step_rate": round(rays / steps / (t / 1e3) / 1e6 / value_1gpu, 4),
+                           "predicted_efficiency": round((ms_1gpu / n) / (t + t_red), 4)}
+    return {"reduce_ms_1rank": round(t_red, 4), "shares": out,
+            "note": "per-GPU share of --scaling strong at N GPUs, measured on one GPU; reduce_ms_1rank is the "
+                    "devices=[0] RCCL reduce (no xGMI transfer)"}
 
 
 def main():
@@ -218,15 +287,21 @@ def main():
     ngpu = args.gpus if args.single_process else world  # GPUs of the job
     if args.api == "render" and world > 1:
         sys.exit("--api render is one process (use --single-process for N > 1)")
+    if args.single_process and world > 1:
+        sys.exit("--single-process drives every GPU from one process: do not launch it under torchrun")
+    # MFX_BENCH_FORCE_DIST=1: run the multi-process path (process group, attached torch accumulator,
+    # RCCL reduce) even at world 1 — how tests/test_gpu_distributed.py runs the driver's N-GPU
+    # sequence on a one-GPU box
+    use_dist = world > 1 or os.environ.get("MFX_BENCH_FORCE_DIST") == "1"
 
     import numpy as np
     from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE
     from mafrixraytracing_amd.distributed import native_partitioned_render, step_spp
-    from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
+    from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
     dist = torch = None
-    if world > 1:
+    if use_dist:
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
@@ -236,18 +311,18 @@ def main():
     W, H = arrays.width, arrays.height
     npix = W * H
     spp_step = step_spp(args.spp, ngpu, args.scaling)  # the whole job's spp per step
-    mode = MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE
+    mode = (MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE) | CONFIG_FLAGS.get(args.config, 0)
     devices = list(range(args.gpus)) if args.single_process else None
     ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world,
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
     pr = None
-    if world > 1:
+    if use_dist:
         acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
         pr = native_partitioned_render(ctx, acc, rank, world)
     rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
         ctx.sync()
@@ -294,7 +369,7 @@ def main():
     elapsed = time.perf_counter() - t0
     if args.api == "render":
         elapsed = call_s
-    if world > 1:
+    if use_dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
@@ -353,6 +428,33 @@ def main():
                 if tdata.get("spp", args.spp) != args.spp:
                     tdata = None  # profiled on another workload
 
+            tdroof = None  # profiles/td_<scene>.json (scripts/pmc_td_roof.sh): the TD / L1 line-request roof
+            tdfile = os.path.join(ROOT, "profiles", f"td_{sname}.json")
+            if os.path.exists(tdfile) and ngpu == 1 and args.api == "batch" and not CONFIG_FLAGS.get(args.config):
+                with open(tdfile) as f:
+                    tdroof = json.load(f)
+
+            def td_roofline(kname, kms, launches):
+                """The bound these kernels sit under: vector-memory line requests. achieved = the PMC
+                pass's TCP line lookups per launch over this run's HIP-event launch time; peak = the
+                td_gather peak case's lookups per GPU clock x the clock the PMC pass ran at."""
+                if not tdroof:
+                    return None
+                base = kname.split("<")[0]
+                for kk, kv in tdroof["kernels"].items():
+                    if kk.split("<")[0] == base:
+                        lines = kv["tcp_accesses_per_launch"]
+                        ach = lines / (kms / launches / 1e3) / 1e9
+                        peak = tdroof["peak"]["lines_per_clock"] * kv["clock_mhz"] * 1e6 / 1e9
+                        return {"bound": "td", "achieved": round(ach, 2), "peak": round(peak, 2),
+                                "unit": "G line-lookups/s", "frac": round(ach / peak, 4),
+                                "frac_pmc_pass": round(kv["frac_of_peak"], 4),
+                                "td_busy_frac": round(kv["td_busy_frac"], 4), "ta_busy_frac": round(kv["ta_busy_frac"], 4),
+                                "lines_per_launch": lines, "clock_mhz_pmc_pass": round(kv["clock_mhz"], 1),
+                                "peak_case": tdroof["peak"]["case"],
+                                "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
+                return None
+
             def kernel_roofline(kname, kms, krays, launches, bray):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
                 achieved = krays * bray / (kms / 1e3) / 1e9
@@ -364,6 +466,7 @@ def main():
                             traffic = kv.get("hbm_bytes_per_launch")
                 return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                        "td": td_roofline(kname, kms, launches),
                         "kernel": kname, "launches_per_step": launches,
                         "avg_launch_ms": round(kms / launches, 4),
                         "bytes_per_ray": round(bray, 1), "bytes_per_ray_source":
@@ -397,18 +500,27 @@ def main():
             roofline["counters"] = {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
                                         else round(d, 4)) for g, d in stats.items()}
         value = rays_all / elapsed / 1e6
-        rapi = None
+        rapi = sapi = share = None
         if ngpu == 1 and args.api == "batch" and not args.no_render_api and not args.megakernel:
-            rapi = render_api(arrays, DEFAULT_SEED, args.spp)
+            # the shipped binding's default (fsharp/Native.fs DefaultRenderAhead, native.Scene): Scene.Render
+            # served from batches of DEFAULT_RENDER_AHEAD samples
+            cf = CONFIG_FLAGS.get(args.config, 0)
+            rapi = render_api(arrays, DEFAULT_SEED, 2 * DEFAULT_RENDER_AHEAD, render_ahead=DEFAULT_RENDER_AHEAD, flags=cf)
             rapi["vs_batch"] = round(rapi["value"] / value, 4)
-            # the same calls with render-ahead over the config's spp (one batch per `spp` calls)
-            ra = render_api(arrays, DEFAULT_SEED, args.spp, render_ahead=args.spp)
-            ra["vs_batch"] = round(ra["value"] / value, 4)
-            rapi["with_render_ahead"] = ra
+            rapi["binding_default"] = True
+            # the same calls one sample at a time (render_ahead = 0)
+            plain = render_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
+            plain["vs_batch"] = round(plain["value"] / value, 4)
+            rapi["without_render_ahead"] = plain
+            sapi = sample_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
+            sapi["vs_batch"] = round(sapi["value"] / value, 4)
+            share = strong_share(arrays, DEFAULT_SEED, args.spp, value, elapsed / args.steps * 1e3, flags=cf)
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
-        if ngpu == 1:
+        if ngpu == 1 and use_dist:
+            par = "one GPU through the one-process-per-GPU path (process group, attached accumulator, reduce)"
+        elif ngpu == 1:
             par = "one GPU"
         elif args.single_process:
             par = f"sample-partition x{ngpu}, one process, library RCCL reduce (mfx_options.devices)"
@@ -420,6 +532,7 @@ def main():
         result = {
             "metric": METRIC, "value": round(value, 2), "unit": "Mrays/s", "n_gpus": ngpu,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "rays_per_step": rays_all / args.steps,
             "higher_is_better": True, "scaling": args.scaling, "vs_baseline": None, "dtype": "f64",
             "data": "synthetic",
             "config": {"workload": f"{cfg_label}, {W}x{H}, {spp_step} spp per step over {ngpu} GPU(s)",
@@ -428,11 +541,11 @@ def main():
                        "spp_per_gpu": per_gpu, "global_spp_per_step": spp_step, "max_depth": 3,
                        "pipeline": "megakernel" if args.megakernel else "wavefront", "api": api,
                        "parallelism": par},
-            "roofline": roofline, "render_api": rapi, "cpu_baseline": cpu,
+            "roofline": roofline, "render_api": rapi, "sample_api": sapi, "strong_share": share, "cpu_baseline": cpu,
         }
         print(json.dumps(result), file=json_out, flush=True)
     ctx.close()
-    if world > 1:
+    if use_dist:
         dist.barrier()
         dist.destroy_process_group()
     return result

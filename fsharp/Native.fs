@@ -139,6 +139,11 @@ module Api =
 let MFX_F_NONE = 0
 let MFX_F_HOST_BVH = 4      // build the traversal BVH on the CPU instead of the GPU (the same tree)
 let DefaultSeed = 0x4D414652UL
+/// Scene.Render's one-sample calls are served from batches of this many samples (mfx_options.render_ahead):
+/// the batch is traced at once, the film add and post of all its calls run on the GPU ahead of them, and
+/// the next batch is traced in the background while this one is served; every frame is the bytes of the
+/// one-sample-per-call path. The library cuts it to what fits in a quarter of the free HBM.
+let DefaultRenderAhead = 64
 
 /// The library returns 0 or a negative MFX_E_* code; the reference signals failures by raising.
 let check (rc : int) (what : string) =
@@ -264,7 +269,7 @@ type NativePixelIntegrator(shapes : IHitable[], light : INewLight, camera : ICam
             o.partIndex <- 0
             o.partCount <- 1
             o.ndevices <- devices.Length
-            o.renderAhead <- 0  // K > 1: Scene.Render's one-sample calls served from batches of K samples
+            o.renderAhead <- DefaultRenderAhead  // Scene.Render's one-sample calls served from batches of K samples
             o.devices <- (if devices.Length > 0 then hd.AddrOfPinnedObject() else 0n)
             let mutable c = 0n
             check (Api.mfx_create(&d, &o, &c)) "mfx_create"   // deep copy: the arrays are unpinned after

@@ -123,6 +123,9 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
                                and gives the same bits (one path per pixel: no summation order) */
 #define MFX_F_FLATTEN 16    /* mfx_create_instanced: flatten every instance into one BVH (no two-level
                                traversal); the same world scene, hits and images */
+#define MFX_F_TWO_LEVEL 32  /* mfx_create_instanced: keep the two-level traversal. Default (neither flag):
+                               flattened when the flat image fits MFX_FLATTEN_MAX_BYTES (env; default
+                               2 GiB at 512 B per traversal slot of the expansion), two-level otherwise */
 
 /* One entry of an instanced scene (mfx_create_instanced; an extension: the reference has no
  * instancing, its scenes are flat lists). The world primitive list — the index space Bvh.Build

@@ -22,6 +22,7 @@ MFX_F_MEGAKERNEL = 2
 MFX_F_HOST_BVH = 4
 MFX_F_WAVEFRONT = 8
 MFX_F_FLATTEN = 16
+MFX_F_TWO_LEVEL = 32
 MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
 MFX_ABI_VERSION = 4

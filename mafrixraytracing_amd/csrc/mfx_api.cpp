@@ -80,6 +80,24 @@ hipError_t upload(T** dptr, const std::vector<T>& v) {
 }  // namespace
 
 
+// One render-ahead buffer: the 1-spp images (FP64 planes) of global samples [base, base + n), the
+// RGBA8 frame each of those one-sample render calls returns, and the film the frames start from.
+struct AheadBuf {
+    double* planes = nullptr;           // [cap][3][npix]
+    uint8_t* frames = nullptr;          // [cap][npix][4] (y-major RGBA8)
+    double* film_in = nullptr;          // [3][npix] the film before plane k0 (as the frames assume)
+    double* film_out = nullptr;         // [3][npix] the film after plane n - 1
+    unsigned long long* counters = nullptr;  // the batch's ray counters [WF_SHARDS][WF_NCTR]
+    hipEvent_t t0 = nullptr, t1 = nullptr;   // around the batch's trace
+    hipEvent_t ready = nullptr;         // frames computed
+    int64_t base = 0, n = 0;            // samples held (n == 0: empty)
+    int64_t k0 = 0;                     // frames computed from index k0 on
+    int64_t expect = 0;                 // the index whose frame a call may take next
+    uint64_t epoch = 0;                 // film epoch the frames were computed in
+    double count0 = 0.0;                // Film frameCount before plane k0
+    bool reported = false;              // a call has reported the batch's rays and time
+};
+
 struct mfx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -132,12 +150,22 @@ struct mfx_ctx {
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     double* d_vscratch = nullptr;    // megakernel: per-lane vertex records [max_depth + 1][6][grid * 256]
     double* d_albedo = nullptr;      // [nmat][3]
-    // render-ahead (mfx_options.render_ahead): one-sample render calls take their sample's image
-    // from planes a batched wavefront trace filled for the next render_ahead samples
+    // render-ahead (mfx_options.render_ahead; see the section above mfx_render_rgba8): one-sample
+    // render calls take their frame from batches of the next render_ahead samples, traced and
+    // post-processed ahead of the calls, the next batch in the background while the current one is
+    // served (two buffers)
     int render_ahead = 0;
-    double* d_ahead = nullptr;       // [ahead_cap][3][npix]
-    int ahead_cap = 0;               // planes allocated
-    int64_t ahead_base = 0, ahead_n = 0;  // global samples [ahead_base, ahead_base + ahead_n) held
+    AheadBuf ab[2];
+    int ab_nbuf = 0;                 // buffers allocated (0: none yet; 1: no background batch)
+    int ab_cap = 0;                  // samples per buffer
+    int ab_cur = -1;                 // the buffer the last render call was served from (-1: none)
+    int64_t ab_last_k = -1;          // and its index in that buffer
+    uint64_t film_epoch = 1;         // bumped when the film leaves the held frames' sequence
+    bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its planes)
+    hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
+    bool rep_valid = false;          // the last call was served from held frames: its stats are rep_*
+    double rep_counts[16] = {0};
+    double rep_ms = 0.0;
     bool diag_iter = false;
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
@@ -145,6 +173,7 @@ struct mfx_ctx {
     std::vector<ncclComm_t> comms;       // [G] one RCCL communicator per device, rank g = device g
     double* d_reduce_stage = nullptr;    // repeated-device list: a peer's accumulator copied here
     std::vector<hipEvent_t> peer_done;   // repeated-device list: per peer, its trace has finished
+    hipEvent_t reduce_done = nullptr;    // repeated-device list: the primary has read every peer's buffer
 };
 
 // the devices of a context, primary first
@@ -152,6 +181,19 @@ static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
     std::vector<mfx_ctx*> v{c};
     v.insert(v.end(), c->peers.begin(), c->peers.end());
     return v;
+}
+
+static void ahead_free(mfx_ctx* c) {
+    for (AheadBuf& B : c->ab) {
+        for (void* b : {(void*)B.planes, (void*)B.frames, (void*)B.film_in, (void*)B.film_out, (void*)B.counters})
+            if (b) (void)hipFree(b);
+        for (hipEvent_t e : {B.t0, B.t1, B.ready})
+            if (e) (void)hipEventDestroy(e);
+        B = AheadBuf{};
+    }
+    c->ab_nbuf = 0;
+    c->ab_cap = 0;
+    c->ab_cur = -1;
 }
 
 static void free_ctx(mfx_ctx* c) {
@@ -164,11 +206,14 @@ static void free_ctx(mfx_ctx* c) {
     (void)hipSetDevice(c->device);
     for (hipEvent_t e : c->peer_done)
         if (e) (void)hipEventDestroy(e);
+    if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_ahead};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
+    ahead_free(c);
+    if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -205,6 +250,7 @@ static int ctx_setup(mfx_ctx* c) {
     } while (0)
     CK(hipSetDevice(c->device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
@@ -337,6 +383,26 @@ static int ctx_setup(mfx_ctx* c) {
     return MFX_OK;
 }
 
+// Two-level or flat for an instanced scene. The flat image (one BVH over the expansion) is the faster
+// search (C5: 5,088 vs 4,729 Mrays/s, r02bt) and exactly the same results, so it is taken whenever it
+// fits the budget: traversal slots of the expansion x 512 B (slot, shade record, nodes and reference
+// leaves) <= MFX_FLATTEN_MAX_BYTES (default 2 GiB; C5 is 93,698 slots, 48 MB). MFX_F_TWO_LEVEL keeps
+// the instances two-level regardless; MFX_F_FLATTEN flattens regardless.
+static bool flatten_instances(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
+                              int32_t flags) {
+    if (flags & MFX_F_FLATTEN) return true;
+    if (!instances || (flags & MFX_F_TWO_LEVEL)) return false;
+    double budget = 2.0 * 1024 * 1024 * 1024;
+    if (const char* e = getenv("MFX_FLATTEN_MAX_BYTES")) budget = atof(e);
+    double slots = 0.0;
+    for (int32_t i = 0; i < ninstances; ++i) {
+        const int64_t f = instances[i].first, n = instances[i].count;
+        if (f < 0 || n < 0 || f + n > scene->nprims) return false;  // mfx_build_scene reports the bad entry
+        for (int64_t k = f; k < f + n; ++k) slots += scene->prims[k].kind == MFX_PRIM_RECT ? 2.0 : 1.0;
+    }
+    return slots * 512.0 <= budget;
+}
+
 static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
                        const mfx_options* opt, mfx_ctx** out) {
     if (!scene || !opt || !out) return fail(MFX_E_INVALID, "mfx_create: null argument");
@@ -361,7 +427,7 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
     // the traversal BVH is built on the first device unless the caller asks for the host build
     // (the same tree either way: tests/test_gpu_build.py); the other devices get copies
     if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0, instances, ninstances,
-                         (opt->flags & MFX_F_FLATTEN) != 0)) {
+                         flatten_instances(scene, instances, ninstances, opt->flags))) {
         delete c;
         const bool dev = err.rfind("GPU BVH build", 0) == 0;
         return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
@@ -426,12 +492,14 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         } else {
             hipError_t e = hipSetDevice(c->device);
             if (e == hipSuccess) e = hipMalloc((void**)&c->d_reduce_stage, 3 * sizeof(double) * (size_t)c->npix);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&c->reduce_done, hipEventDisableTiming);
             for (size_t k = 0; k < c->peers.size() && e == hipSuccess; ++k) {
                 hipEvent_t ev = nullptr;
                 e = hipSetDevice(c->peers[k]->device);
                 if (e == hipSuccess) e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
                 if (e == hipSuccess) c->peer_done.push_back(ev);
             }
+            if (e == hipSuccess) e = hipSetDevice(c->device);
             if (e != hipSuccess) {
                 free_ctx(c);
                 return fail(MFX_E_DEVICE, std::string("mfx_create: device reduce setup: ") + hipGetErrorString(e));
@@ -489,7 +557,8 @@ int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* in
     if (!out) return fail(MFX_E_INVALID, "null argument");
     MfxHostScene h;
     std::string err;
-    if (!mfx_build_scene(scene, h, err, false, instances, ninstances, (flags & MFX_F_FLATTEN) != 0))
+    if (!scene) return fail(MFX_E_INVALID, "null argument");
+    if (!mfx_build_scene(scene, h, err, false, instances, ninstances, flatten_instances(scene, instances, ninstances, flags)))
         return fail(MFX_E_INVALID, "mfx_build_instanced_info: " + err);
     instancing_info(h, out);
     if (stack_entries) *stack_entries = h.stack_entries;
@@ -546,7 +615,11 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
 // max_depth extension rays of PathIntegrator.TraceRay (Integrators.fs:107-137), one bounce of
 // every live path per iteration — then k_resolve adds its finished paths to their pixels. Every
 // launch count is known up front, so the whole call is enqueued without a host round trip.
-static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes = nullptr) {
+// planes != null (render-ahead): each sample's 1-spp image to its own plane, the ray counters to
+// `counters` and the trace bracketed by the events e0 / e1 instead of the context's (no per-iteration
+// events), so a batch traced in the background leaves the last call's timing records alone.
+static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes = nullptr,
+                    unsigned long long* counters = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
@@ -557,7 +630,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     WfParams P = c->wf;
     fill_scene_params(c, P);
     P.ctl = c->d_wfctl;
-    P.counters = c->d_counters;
+    P.counters = counters ? counters : c->d_counters;
+    const bool own_events = e0 == nullptr;
     P.seed = c->seed;
     P.sample_base = sample_base;
     P.part_index = c->part_index;
@@ -579,12 +653,12 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
-    while ((int)c->it_ev.size() < 3 * iters) {
+    while (own_events && (int)c->it_ev.size() < 3 * iters) {
         hipEvent_t e;
         HIPCHECK(hipEventCreate(&e));
         c->it_ev.push_back(e);
     }
-    HIPCHECK(hipEventRecord(c->ev0, c->stream));
+    HIPCHECK(hipEventRecord(own_events ? c->ev0 : e0, c->stream));
     int it = 0;
     for (int64_t g = 0; g < ngen; ++g) {
         P.path_base = g * gen_max;
@@ -595,6 +669,10 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
         for (int d = 0; d <= P.max_depth; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;
+            if (!own_events) {
+                HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
+                continue;
+            }
             hipEvent_t* ev = c->it_ev.data() + 3 * it;
             HIPCHECK(hipEventRecord(ev[0], c->stream));
             HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, ev + 1));
@@ -617,6 +695,10 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             }
         }
         HIPCHECK(mfx_wf_resolve(P, c->stream));
+    }
+    if (!own_events) {
+        HIPCHECK(hipEventRecord(e1, c->stream));
+        return MFX_OK;
     }
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
@@ -691,14 +773,19 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
 int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
+    c->rep_valid = false;  // the stats now describe this trace
     for (mfx_ctx* d : devs_of(c)) {
         const int rc = dev_trace_accumulate(d, spp, sample_base);
         if (rc) return rc;
     }
+    HIPCHECK(hipSetDevice(c->device));  // the primary stays current for what the caller enqueues next
     return MFX_OK;
 }
 
-// Sum every device's accumulator into the primary's, stream-ordered after each device's trace.
+// Sum every device's accumulator into the primary's, stream-ordered after each device's trace, and
+// every peer's later work (a clear or trace of its accumulator) after the reduce: the RCCL reduce
+// runs on each device's own stream; the repeated-device copies run on the primary's stream, so
+// each peer's stream waits for them (reduce_done) before anything the caller enqueues next.
 int mfx_accum_reduce(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (!c->comms.empty()) {  // RCCL: rank g sends device g's buffer, the root reduces in place
@@ -713,6 +800,7 @@ int mfx_accum_reduce(mfx_ctx* c) {
         const ncclResult_t r2 = R->groupEnd();
         if (r == ncclSuccess) r = r2;
         if (r != ncclSuccess) return fail(MFX_E_DEVICE, std::string("mfx_accum_reduce: ") + R->errorString(r));
+        HIPCHECK(hipSetDevice(c->device));
         return MFX_OK;
     }
     // a repeated-device list: add the peers' accumulators in device order (a0 + a1) + a2 ...
@@ -726,11 +814,25 @@ int mfx_accum_reduce(mfx_ctx* c) {
         HIPCHECK(hipMemcpyAsync(c->d_reduce_stage, p->d_accum, bytes, hipMemcpyDefault, c->stream));
         HIPCHECK(mfx_launch_accum_add(c->d_accum, c->d_reduce_stage, 3 * c->npix, c->stream));
     }
+    if (!c->peers.empty()) {
+        HIPCHECK(hipSetDevice(c->device));
+        HIPCHECK(hipEventRecord(c->reduce_done, c->stream));
+        for (mfx_ctx* p : c->peers) {
+            HIPCHECK(hipSetDevice(p->device));
+            HIPCHECK(hipStreamWaitEvent(p->stream, c->reduce_done, 0));
+        }
+        HIPCHECK(hipSetDevice(c->device));
+    }
     return MFX_OK;
 }
 
 int mfx_trace_timing(mfx_ctx* c, double out[8]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    if (c->rep_valid) {  // a call served from held frames: its batch's device time, no stage split
+        for (int k = 0; k < 8; ++k) out[k] = 0.0;
+        out[0] = c->rep_ms;
+        return MFX_OK;
+    }
     double total = 0;
     int rc = mfx_last_trace_ms(c, &total);
     if (rc) return rc;
@@ -760,6 +862,10 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
 
 int mfx_last_trace_ms(mfx_ctx* c, double* ms) {
     if (!c || !ms) return fail(MFX_E_INVALID, "null argument");
+    if (c->rep_valid) {
+        *ms = c->rep_ms;
+        return MFX_OK;
+    }
     double worst = 0.0;  // the devices run concurrently: the slowest one's time
     for (mfx_ctx* d : devs_of(c)) {
         if (!d->ev_valid) return fail(MFX_E_STATE, "no trace launch recorded yet");
@@ -826,21 +932,191 @@ int mfx_stream(mfx_ctx* c, void** stream) {
     return MFX_OK;
 }
 
+static void sum_counters(const unsigned long long* h, double out[16]) {
+    for (int k = 0; k < 16; ++k) {
+        double v = 0;
+        for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[WF_NCTR * g + k];
+        out[k] += v;
+    }
+}
+
 int mfx_ray_counts(mfx_ctx* c, double out[16]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    if (c->rep_valid) {  // a call served from held frames (render-ahead)
+        for (int k = 0; k < 16; ++k) out[k] = c->rep_counts[k];
+        return MFX_OK;
+    }
     for (int k = 0; k < 16; ++k) out[k] = 0.0;
     for (mfx_ctx* d : devs_of(c)) {  // summed over the context's devices
         HIPCHECK(hipSetDevice(d->device));
         unsigned long long h[WF_NCTR * WF_SHARDS];  // per-shard counter sets (the megakernel uses set 0)
         HIPCHECK(hipMemcpyAsync(h, d->d_counters, sizeof(h), hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipStreamSynchronize(d->stream));
-        for (int k = 0; k < 16; ++k) {
-            double v = 0;
-            for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[WF_NCTR * g + k];
-            out[k] += v;
-        }
+        sum_counters(h, out);
     }
     out[3] = out[0];  // paths == primary rays
+    return MFX_OK;
+}
+
+// ---- render-ahead --------------------------------------------------------------------------------
+// mfx_options.render_ahead = K > 1 on a one-device context with the whole sample set. Scene.Render
+// (Scene.fs:331-333) asks for one sample per call: alone, a 1080p sample is ~21 rays per lane of a
+// persistent grid plus the film/post launch and the readback per call. A sample's 1-spp image
+// depends only on (seed, global sample index), so a call whose sample is not held traces the next K
+// samples in one batched wavefront pass (k_resolve writes each sample's image to its own FP64
+// plane) and film_frames_kernel then runs, in call order, the film add and post of all K calls
+// (the FP64 operations film_post_kernel runs per call, in the same order): each call of the batch
+// only copies its RGBA8 frame to the host. While a batch is served, the next one is traced and
+// post-processed in the background into the second buffer (the frame copies run on their own
+// stream, so they overlap that trace). Every frame and the film are the bytes the one-sample path
+// gives (tests/test_gpu_render_ahead.py).
+// The frames assume the calls follow each other with nothing else touching the film. A reset, a
+// render call of spp != 1 or an mfx_sample call (which moves the sample sequence) bumps film_epoch
+// after bringing d_film up to date; a buffer whose frames belong to an older epoch recomputes them
+// from the index it is at, from d_film.
+static int ahead_alloc(mfx_ctx* c) {
+    const size_t plane = 3 * sizeof(double) * (size_t)c->npix, frame = 4 * (size_t)c->npix;
+    const size_t per_sample = plane + frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    const size_t budget = fr / 4;  // both buffers within a quarter of the free HBM
+    int nbuf = 2;
+    int64_t k = c->render_ahead;
+    if ((size_t)k * per_sample + fixed > budget / 2) {
+        nbuf = 1;  // no background batch: one buffer of as many samples as fit
+        k = budget > fixed ? (int64_t)((budget - fixed) / per_sample) : 0;
+        k = std::min<int64_t>(k, c->render_ahead);
+    }
+    if (k < 2) return MFX_E_NOMEM;
+    for (int b = 0; b < nbuf; ++b) {
+        AheadBuf& B = c->ab[b];
+        hipError_t e = hipMalloc((void**)&B.planes, (size_t)k * plane);
+        if (e == hipSuccess) e = hipMalloc((void**)&B.frames, (size_t)k * frame);
+        if (e == hipSuccess) e = hipMalloc((void**)&B.film_in, plane);
+        if (e == hipSuccess) e = hipMalloc((void**)&B.film_out, plane);
+        if (e == hipSuccess) e = hipMalloc((void**)&B.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipEventCreate(&B.t0);
+        if (e == hipSuccess) e = hipEventCreate(&B.t1);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&B.ready, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            (void)hipGetLastError();
+            ahead_free(c);
+            return e == hipErrorOutOfMemory ? MFX_E_NOMEM : fail(MFX_E_DEVICE, std::string("render-ahead: ") + hipGetErrorString(e));
+        }
+    }
+    c->ab_nbuf = nbuf;
+    c->ab_cap = (int)k;
+    return MFX_OK;
+}
+
+// d_film = the film as of the last render call (film_in of the buffer it was served from plus that
+// buffer's planes up to it, added in call order)
+static int ahead_materialize(mfx_ctx* c) {
+    if (c->film_in_dfilm) return MFX_OK;
+    const AheadBuf& B = c->ab[c->ab_cur];
+    HIPCHECK(mfx_launch_film_frames(B.planes, B.k0, c->ab_last_k + 1, B.film_in, c->d_film, c->host.width,
+                                    c->host.height, 0.0, nullptr, c->stream));
+    c->film_in_dfilm = true;
+    return MFX_OK;
+}
+
+// the film leaves the held frames' sequence (a reset, an spp != 1 render call, mfx_sample)
+static int ahead_break(mfx_ctx* c) {
+    if (c->ab_nbuf == 0) return MFX_OK;
+    const int rc = ahead_materialize(c);
+    if (rc) return rc;
+    c->film_epoch += 1;
+    c->ab_cur = -1;
+    return MFX_OK;
+}
+
+// frames of B from index k on, starting from film `film_src` and frame count `count0`
+static int ahead_frames(mfx_ctx* c, AheadBuf& B, int64_t k, const double* film_src, double count0) {
+    const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
+    if (film_src != B.film_in)
+        HIPCHECK(hipMemcpyAsync(B.film_in, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHECK(mfx_launch_film_frames(B.planes, k, B.n, B.film_in, B.film_out, c->host.width, c->host.height, count0,
+                                    B.frames, c->stream));
+    HIPCHECK(hipEventRecord(B.ready, c->stream));
+    B.k0 = k;
+    B.expect = k;
+    B.epoch = c->film_epoch;
+    B.count0 = count0;
+    return MFX_OK;
+}
+
+// trace samples [base, base + ab_cap) into B, then their frames from film_src / count0 (enqueued only)
+static int ahead_launch(mfx_ctx* c, AheadBuf& B, int64_t base, const double* film_src, double count0) {
+    B.base = base;
+    B.n = c->ab_cap;
+    B.reported = false;
+    HIPCHECK(hipMemsetAsync(B.counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
+    const int rc = wf_trace(c, B.n, base, B.planes, B.counters, B.t0, B.t1);
+    if (rc) {
+        B.n = 0;
+        return rc;
+    }
+    return ahead_frames(c, B, 0, film_src, count0);
+}
+
+// One render call (spp = 1) served from held frames. Returns MFX_E_NOMEM when no buffer fits (the
+// caller then renders one sample per call, without render-ahead).
+static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
+    if (c->ab_nbuf == 0) {
+        const int rc = ahead_alloc(c);
+        if (rc) return rc;
+    }
+    const int64_t s = c->next_sample;
+    int xi = -1;
+    for (int b = 0; b < c->ab_nbuf; ++b)
+        if (c->ab[b].n > 0 && s >= c->ab[b].base && s < c->ab[b].base + c->ab[b].n) xi = b;
+    int rc = MFX_OK;
+    if (xi < 0) {  // not held: trace a batch from this sample, its frames from the film as it is
+        rc = ahead_materialize(c);
+        if (rc) return rc;
+        xi = (c->ab_cur >= 0 && c->ab_nbuf == 2) ? 1 - c->ab_cur : 0;
+        rc = ahead_launch(c, c->ab[xi], s, c->d_film, c->frame_count);
+    } else if (c->ab[xi].epoch != c->film_epoch || c->ab[xi].expect != s - c->ab[xi].base) {
+        rc = ahead_materialize(c);  // held, but the frames assumed another film: recompute from here
+        if (!rc) rc = ahead_frames(c, c->ab[xi], s - c->ab[xi].base, c->d_film, c->frame_count);
+    }
+    if (rc) return rc;
+    AheadBuf& X = c->ab[xi];
+    const int64_t k = s - X.base;
+    if (c->ab_nbuf == 2) {  // the next batch, in the background, unless the other buffer holds it
+        AheadBuf& Y = c->ab[1 - xi];
+        const double count_end = X.count0 + (double)(X.n - X.k0);  // frameCount after X's last call
+        if (!(Y.n > 0 && Y.base == X.base + X.n))
+            rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
+        else if (Y.epoch != c->film_epoch || Y.k0 != 0)  // held, but its frames assumed another film
+            rc = ahead_frames(c, Y, 0, X.film_out, count_end);
+        if (rc) return rc;
+    }
+    // this call's frame: the copy waits for the frames only, not for the background batch
+    HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
+    if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * 4 * c->npix, 4 * (size_t)c->npix, hipMemcpyDeviceToHost,
+                                      c->copy_stream));
+    for (int q = 0; q < 16; ++q) c->rep_counts[q] = 0.0;
+    c->rep_ms = 0.0;
+    if (!X.reported) {  // the first call served from a batch reports its rays and device time
+        unsigned long long h[WF_NCTR * WF_SHARDS];
+        HIPCHECK(hipMemcpyAsync(h, X.counters, sizeof(h), hipMemcpyDeviceToHost, c->copy_stream));
+        HIPCHECK(hipStreamSynchronize(c->copy_stream));
+        sum_counters(h, c->rep_counts);
+        c->rep_counts[3] = c->rep_counts[0];
+        float f = 0.f;
+        HIPCHECK(hipEventElapsedTime(&f, X.t0, X.t1));
+        c->rep_ms = f;
+        X.reported = true;
+    }
+    HIPCHECK(hipStreamSynchronize(c->copy_stream));
+    c->rep_valid = true;
+    c->ab_cur = xi;
+    c->ab_last_k = k;
+    X.expect = k + 1;
+    c->film_in_dfilm = false;
+    c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
+    c->next_sample += 1;
     return MFX_OK;
 }
 
@@ -849,7 +1125,9 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     if (c->api_part_count != 1)
         return fail(MFX_E_STATE, "mfx_sample needs the whole sample set (part_count == 1); "
                                  "partitioned contexts compose with mfx_trace_accumulate + a reduce");
-    int rc = mfx_accum_clear(c);
+    int rc = ahead_break(c);  // it moves the sample sequence past held frames
+    if (rc) return rc;
+    rc = mfx_accum_clear(c);
     if (rc) return rc;
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
@@ -863,83 +1141,30 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     return mfx_sync(c);
 }
 
-// Render-ahead (mfx_options.render_ahead = K > 1, one device, whole sample set): a one-sample
-// render call whose global sample is not held traces the next K samples in one batched wavefront
-// pass, k_resolve writing each sample's 1-spp image to its own plane; that call and the next K - 1
-// take their plane. A sample's image depends only on (seed, global sample index), so the film and
-// every RGBA8 frame are the bits the one-sample-per-call path gives (tests/test_gpu_render_ahead.py);
-// mfx_reset clears the film, not the sample sequence, so held planes stay valid across it. The
-// batch's rays and device time are reported by the call that traced it; the others trace nothing
-// and report 0 rays in 0 device time.
-// Makes the context hold the plane of sample next_sample (tracing the next batch if needed).
-static int ahead_ensure(mfx_ctx* c) {
-    const int64_t s = c->next_sample;
-    if (!(c->ahead_n > 0 && s >= c->ahead_base && s < c->ahead_base + c->ahead_n)) {
-        const size_t pb = 3 * sizeof(double) * (size_t)c->npix;
-        int k = c->render_ahead;
-        if (k > c->ahead_cap) {
-            if (c->d_ahead) (void)hipFree(c->d_ahead);
-            c->d_ahead = nullptr;
-            c->ahead_cap = 0;
-            c->ahead_n = 0;
-            size_t fr = 0, tot = 0;
-            HIPCHECK(hipMemGetInfo(&fr, &tot));
-            const int fit = (int)std::min<size_t>((size_t)k, fr / 4 / pb);  // at most a quarter of the free HBM
-            if (fit < 2 || hipMalloc((void**)&c->d_ahead, (size_t)fit * pb) != hipSuccess) {
-                c->d_ahead = nullptr;
-                (void)hipGetLastError();
-                return MFX_E_NOMEM;  // the caller renders this call (and the later ones) one sample at a time
-            }
-            c->ahead_cap = fit;
-        }
-        k = std::min(k, c->ahead_cap);
-        HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
-        HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
-        c->mega_last = false;
-        const int rc = wf_trace(c, k, s, c->d_ahead);
-        if (rc) return rc;
-        c->ahead_base = s;
-        c->ahead_n = k;
-    } else {  // held: nothing traced by this call
-        HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
-        HIPCHECK(hipEventRecord(c->ev0, c->stream));
-        HIPCHECK(hipEventRecord(c->ev1, c->stream));
-        c->ev_valid = true;
-        c->it_recorded = 0;
-        c->generations = 0;
-        c->mega_last = false;
-    }
-    return MFX_OK;
-}
-
 int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     if (!c) return fail(MFX_E_INVALID, "null context");
     if (c->api_part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
-    const double* frame = c->d_accum;
-    const bool ahead = spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty();
-    if (ahead) {
+    if (spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty()) {
         HIPCHECK(hipSetDevice(c->device));
-        const int rc = ahead_ensure(c);
-        if (rc == MFX_E_NOMEM) c->render_ahead = 0;  // no room for the planes: render-ahead off for this context
-        else if (rc) return rc;
+        const int rc = ahead_render(c, rgba);
+        if (rc != MFX_E_NOMEM) return rc;
+        c->render_ahead = 0;  // no room for the planes: this context renders one sample per call
     }
-    if (ahead && c->render_ahead > 1) {
-        frame = c->d_ahead + (c->next_sample - c->ahead_base) * 3 * c->npix;
-        c->next_sample += 1;
-    } else {
-        int rc = mfx_accum_clear(c);
+    int rc = ahead_break(c);
+    if (rc) return rc;
+    rc = mfx_accum_clear(c);
+    if (rc) return rc;
+    rc = mfx_trace_accumulate(c, spp, c->next_sample);
+    if (rc) return rc;
+    c->next_sample += spp;
+    if (!c->peers.empty() || !c->comms.empty()) {
+        rc = mfx_accum_reduce(c);
         if (rc) return rc;
-        rc = mfx_trace_accumulate(c, spp, c->next_sample);
-        if (rc) return rc;
-        c->next_sample += spp;
-        if (!c->peers.empty() || !c->comms.empty()) {
-            rc = mfx_accum_reduce(c);
-            if (rc) return rc;
-        }
     }
     c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
-    HIPCHECK(mfx_launch_film_post(frame, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
+    HIPCHECK(hipSetDevice(c->device));
+    HIPCHECK(mfx_launch_film_post(c->d_accum, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
                                   rgba ? c->d_rgba : nullptr, c->stream));
     if (rgba)
         HIPCHECK(hipMemcpyAsync(rgba, c->d_rgba, 4 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
@@ -969,15 +1194,24 @@ int mfx_stats(mfx_ctx* c, double* rays, double* seconds) {
 int mfx_reset(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
     HIPCHECK(hipSetDevice(c->device));
+    // stream-ordered after anything that reads the film (no wait for a background batch)
     HIPCHECK(hipMemsetAsync(c->d_film, 0, 3 * sizeof(double) * (size_t)c->npix, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
     c->frame_count = 0.0;
+    c->film_in_dfilm = true;
+    if (c->ab_nbuf) {
+        c->film_epoch += 1;
+        c->ab_cur = -1;
+    } else {
+        HIPCHECK(hipStreamSynchronize(c->stream));
+    }
     return MFX_OK;
 }
 
 int mfx_film_mean(mfx_ctx* c, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     HIPCHECK(hipSetDevice(c->device));
+    const int rc = ahead_materialize(c);
+    if (rc) return rc;
     HIPCHECK(mfx_launch_film_mean(c->d_film, c->npix, c->frame_count, c->d_frame, c->stream));
     HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));

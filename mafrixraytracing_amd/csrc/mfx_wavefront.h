@@ -122,7 +122,7 @@ struct WfParams {
 // resident blocks per CU of k_extend / k_shadow with `stack_lds` stack entries per lane (spill: the
 // SpillStack instance), ntop top BVH nodes and min(ninst, WF_INST_LDS) instance records in LDS
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu);
-// one iteration (extend, shadow); ev[0] is recorded between the two kernels
+// one iteration (extend, shadow); ev[0] is recorded between the two kernels (ev may be null)
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);
 // after a generation's last iteration: add its finished paths' radiance to their pixels

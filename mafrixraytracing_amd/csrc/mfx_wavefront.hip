@@ -1057,8 +1057,10 @@ static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid
     // compiled for 3 waves per SIMD (up to 168 VGPRs) when its LDS allows no more blocks anyway
     if (P.stack_lds_ext < P.stack_size) launch_extend<true, INST>(P, ext_grid, stats, st, lds_e);
     else launch_extend<false, INST>(P, ext_grid, stats, st, lds_e);
-    hipError_t e = hipEventRecord(ev[0], st);
-    if (e != hipSuccess) return e;
+    if (ev) {  // between the two kernels (per-stage timing); null: not recorded
+        const hipError_t e = hipEventRecord(ev[0], st);
+        if (e != hipSuccess) return e;
+    }
     const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
     if (spill && w3) launch_shadow<true, 3, INST>(P, shd_grid, stats, st, lds_s);
     else if (spill) launch_shadow<true, 4, INST>(P, shd_grid, stats, st, lds_s);

@@ -41,9 +41,11 @@ def step_spp(config_spp: int, world: int, scaling: str) -> int:
 
 
 def reduce_accumulator(acc, dst: int = 0, all_ranks: bool = False):
-    """Sum-reduce a rank's accumulator tensor (torch) across the process group, in place."""
+    """Sum-reduce a rank's accumulator tensor (torch) across the process group, in place. A group of
+    one rank still runs the collective (so a 1-GPU job exercises the N-GPU sequence); without a
+    process group there is nothing to reduce."""
     import torch.distributed as dist
-    if not dist.is_available() or not dist.is_initialized() or dist.get_world_size() == 1:
+    if not dist.is_available() or not dist.is_initialized():
         return acc
     if all_ranks:
         dist.all_reduce(acc, op=dist.ReduceOp.SUM)
@@ -83,15 +85,25 @@ class PartitionedRender:
 def native_partitioned_render(ctx, acc, rank: int, world: int) -> PartitionedRender:
     """PartitionedRender over a HIP context: `acc` (a device tensor on the context's GPU, at least
     3*w*h doubles) becomes the context's accumulator (mfx_accum_attach), so the trace writes
-    straight into the buffer RCCL reduces. The context must render partition `rank` of `world`."""
+    straight into the buffer RCCL reduces. The context must render partition `rank` of `world`.
+    A context over a device list (mfx_options.devices) first sums its devices into the primary's
+    accumulator with its own reduce (mfx_accum_reduce), so no device's samples are dropped.
+
+    Stream order: clear and trace run on the context's HIP stream; sync_fn (mfx_sync) waits for
+    them before the collective, which torch enqueues on its own stream; after_reduce waits for
+    that stream, so the next frame's clear cannot overwrite the buffer while RCCL still reads it."""
     ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
+    multi = len(getattr(ctx, "devices", [0])) > 1
+
+    def render(a, spp, base, r, w):
+        ctx.trace_accumulate(spp, base)
+        if multi:
+            ctx.accum_reduce()
 
     def sync_torch():  # the reduce ran on torch's stream
         import torch
         if acc.is_cuda:
-            torch.cuda.synchronize()
+            torch.cuda.synchronize(acc.device)
 
-    return PartitionedRender(
-        render_fn=lambda a, spp, base, r, w: ctx.trace_accumulate(spp, base),
-        acc=acc, rank=rank, world=world,
-        clear_fn=ctx.accum_clear, sync_fn=ctx.sync, after_reduce=sync_torch if world > 1 else None)
+    return PartitionedRender(render_fn=render, acc=acc, rank=rank, world=world,
+                             clear_fn=ctx.accum_clear, sync_fn=ctx.sync, after_reduce=sync_torch)

@@ -13,6 +13,7 @@ import numpy as np
 from .abi import (INSTANCING_KEYS, MFX_F_NONE, MfxInstance, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
 
 DEFAULT_SEED = 0x4D414652
+DEFAULT_RENDER_AHEAD = 64  # fsharp/Native.fs DefaultRenderAhead: Scene.Render served from batches of 64 samples
 
 
 class NativeContext:
@@ -235,11 +236,14 @@ class NativePixelIntegrator:
 
 
 class Scene:
-    """Scene (Scene.fs:291-333) with the path-tracing hot path on the GPU."""
+    """Scene (Scene.fs:291-333) with the path-tracing hot path on the GPU. Render's one-sample calls
+    are served from batches of `render_ahead` samples (the F# binding's DefaultRenderAhead;
+    mfx_options.render_ahead): the same bytes per frame as one sample per call."""
 
-    def __init__(self, state, seed: int = DEFAULT_SEED, device: int = 0, max_depth: int = 3):
+    def __init__(self, state, seed: int = DEFAULT_SEED, device: int = 0, max_depth: int = 3,
+                 render_ahead: int = DEFAULT_RENDER_AHEAD):
         arrays = state.arrays(max_depth=max_depth) if hasattr(state, "arrays") else state
-        self._ctx = NativeContext(arrays, seed=seed, device=device)
+        self._ctx = NativeContext(arrays, seed=seed, device=device, render_ahead=render_ahead)
         self.width, self.height = arrays.width, arrays.height
         self.film = Film(self._ctx)
         self.pixelIntegrator = NativePixelIntegrator(self._ctx)

@@ -445,7 +445,10 @@ static double fb_area(const double lo[3], const double hi[3]) {
     double dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
     return (dx < 0 || dy < 0 || dz < 0) ? 0.0 : 2.0 * (dx * dy + dy * dz + dz * dx);
 }
-static int fb_build(FastBvh* f, const Prim* prims, int* idx, int first, int n) {
+/* A split level adds at most one stack entry in fast_hit (two pushes, one pop), so capping the
+ * depth at FB_MAX_DEPTH bounds its fixed stack: a deeper range becomes one (long) leaf.        */
+enum { FB_MAX_DEPTH = 100, FB_STACK = FB_MAX_DEPTH + 4 };
+static int fb_build(FastBvh* f, const Prim* prims, int* idx, int first, int n, int depth) {
     const int me = f->nnodes++;
     FNode* nd = &f->nodes[me];
     fb_box(prims, idx + first, n, nd->lo, nd->hi, 0);
@@ -493,6 +496,7 @@ static int fb_build(FastBvh* f, const Prim* prims, int* idx, int first, int n) {
         }
     }
     if (best_split < 0 && n > 8) best_split = NB / 2; /* no SAH win but too many to test: median-ish */
+    if (depth >= FB_MAX_DEPTH) best_split = -1;
     if (best_split < 0) {
         nd->first = first;
         nd->count = n;
@@ -509,8 +513,8 @@ static int fb_build(FastBvh* f, const Prim* prims, int* idx, int first, int n) {
     }
     if (mid == first || mid == first + n) mid = first + n / 2;
     nd->count = 0;
-    fb_build(f, prims, idx, first, mid - first);
-    f->nodes[me].first = fb_build(f, prims, idx, mid, first + n - mid);
+    fb_build(f, prims, idx, first, mid - first, depth + 1);
+    f->nodes[me].first = fb_build(f, prims, idx, mid, first + n - mid, depth + 1);
     return me;
 }
 static void fast_bvh_build(FastBvh* f, const Prim* prims, int n) {
@@ -518,7 +522,7 @@ static void fast_bvh_build(FastBvh* f, const Prim* prims, int n) {
     for (int k = 0; k < n; k++) f->idx[k] = k;
     f->nodes = (FNode*)calloc((size_t)(2 * n), sizeof(FNode));
     f->nnodes = 0;
-    fb_build(f, prims, f->idx, 0, n);
+    fb_build(f, prims, f->idx, 0, n, 0);
 }
 /* slab test with precomputed reciprocals; returns the entry distance or INFINITY */
 static double fb_slab(const FNode* nd, const double o[3], const double inv[3], double tMin, double tMax) {
@@ -538,7 +542,7 @@ static HitRecord fast_hit(const FastBvh* f, const Prim* prims, V3 o, V3 d, doubl
     const double inv[3] = {1.0 / d.x, 1.0 / d.y, 1.0 / d.z};
     HitRecord best = HIT_EMPTY;
     double tbest = tMax;
-    int stack[128], sp = 0;
+    int stack[FB_STACK], sp = 0; /* depth <= FB_MAX_DEPTH: at most depth + 2 entries */
     stack[sp++] = 0;
     while (sp) {
         const FNode* nd = &f->nodes[stack[--sp]];

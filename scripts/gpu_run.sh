@@ -1,0 +1,59 @@
+#!/bin/bash
+# One runner for every GPU-box recipe (replaces the per-experiment gpu_*.sh of rounds 1-2).
+# Usage: scripts/gpu_run.sh TAG STEP [STEP ...]; output under gpurun_out/TAG. Steps run in order,
+# each under its own time limit; the first failing step ends the run (set -e).
+#   tests[:PATTERN]      pytest -m gpu (optionally -k PATTERN), verbose log
+#   smoke                __graft_entry__.smoke()
+#   bench:CFG[:ARGS]     bench.py --config CFG (ARGS: extra bench args, comma-separated) -> bench_CFG.json
+#   default              bench.py with no arguments (the driver's N = 1 line) -> bench_default.json
+#   prof:CFG             rocprofv3 kernel trace/stats + FETCH_SIZE / WRITE_SIZE passes (profile_traffic.sh)
+#   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
+#   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
+#   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   diag:CFG             one MFX_DIAG_ITER=1 frame (per-iteration ray counts and stage times)
+set -e
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+TAG=$1
+shift
+O=gpurun_out/$TAG
+mkdir -p $O
+for step in "$@"; do
+  IFS=: read -r kind a1 a2 a3 <<< "$step"
+  echo "== $step $(date +%T)" | tee -a $O/steps.log
+  case $kind in
+    tests)
+      K=(); [ -n "$a1" ] && K=(-k "$a1")
+      timeout -k 10 900 python3 -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread "${K[@]}" \
+        > $O/pytest_gpu.log 2>&1
+      tail -1 $O/pytest_gpu.log ;;
+    smoke)
+      timeout -k 10 180 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+      cat $O/smoke.log ;;
+    bench)
+      X=(); [ -n "$a2" ] && IFS=, read -ra X <<< "$a2"
+      timeout -k 10 420 python3 bench.py --config $a1 "${X[@]}" > $O/bench_$a1.json 2> $O/bench_$a1.err
+      python3 -c "import json; d=json.load(open('$O/bench_$a1.json')); print('$a1', d['value'], d['ms_per_step'])" ;;
+    default)
+      timeout -k 10 420 python3 bench.py > $O/bench_default.json 2> $O/bench_default.err
+      python3 -c "import json; d=json.load(open('$O/bench_default.json')); print('default', d['value'], d['ms_per_step'])" ;;
+    prof)
+      bash scripts/profile_traffic.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/prof_$a1.log 2>&1 ;;
+    td)
+      make -s -C scripts/ubench td_gather > /dev/null 2>&1 || true
+      bash scripts/pmc_td_roof.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/td_$a1.log 2>&1 ;;
+    pmc)
+      bash scripts/pmc_td.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/pmc_$a1.log 2>&1 ;;
+    ab)
+      IFS=, read -ra SC <<< "$a3"
+      for sc in "${SC[@]}"; do
+        echo "== $sc" >> $O/ab.txt
+        timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
+      done
+      grep -E "==|SUMMARY" $O/ab.txt ;;
+    diag)
+      MFX_DIAG_ITER=1 timeout -k 10 300 python3 bench.py --config $a1 --steps 1 --warmup 1 --no-cpu-baseline \
+        --no-render-api --no-stats > $O/diag_$a1.json 2> $O/diag_$a1.txt ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done

@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 template <int W>
@@ -59,11 +60,17 @@ int main(int argc, char** argv) {
     const int blocks = cus * 8;  // 8 blocks of 4 waves per CU = 8 waves / SIMD
     const int iters = 256;
     printf("cus %d clock %.0f MHz\n", cus, clk_khz / 1e3);
+    // `td_gather peak`: only the TD roof case — every lane of every wave a distinct 64-B line of an
+    // L1-resident 16 KB table, 16-B loads, 4 independent loads per round — for a PMC pass whose
+    // TCP_TOTAL_ACCESSES / GRBM_GUI_ACTIVE per dispatch is the peak the trace kernels are held to
+    // (scripts/pmc_td_roof.sh)
+    const bool peak_only = argc > 1 && std::string(argv[1]) == "peak";
     printf("%8s %5s %3s %3s %5s %3s %12s %14s %14s\n", "table", "far%", "W", "act", "group", "ilp", "ms", "winst/CUclk", "lanes/CUclk");
     const size_t tb = 16 << 10;
     for (double farp : {0.0, 0.01, 0.02, 0.05, 0.1, 0.2, 1.0})
         for (int w : {16})
             for (int act : {64, 22})
+                if (!peak_only || (farp == 0.0 && act == 64))
                 for (int group : {1}) {
                     const uint32_t far_mask = (1u << 14) - 1;  // 1 MB far table (L2-resident)
                     const uint32_t far_thresh = (uint32_t)(farp * 65536.0);

@@ -1,0 +1,136 @@
+"""The driver's multi-process composition on a real GPU (VERDICT r02 Next #1).
+
+bench.py --gpus N runs one process per GPU under torch.distributed.run: each rank attaches a torch
+device tensor as its context's accumulator (mfx_accum_attach), clears it, traces its sample
+partition, waits for the context's stream and reduces over the process group
+(distributed.native_partitioned_render). That replaces the reference's in-process fan-out
+(Integrators.fs:164). A one-GPU box cannot run N > 1 ranks on N GPUs, so the sequence is pinned
+here in the shapes it can take:
+- a world-1 nccl (= RCCL) group: the whole attach / clear / trace / sync / reduce sequence with a
+  real collective, bit-identical to a plain context's accumulator, for several frames;
+- two ranks sharing device 0 over gloo with CUDA tensors (all_reduce): the reduced accumulator is
+  bit for bit the two partitioned contexts' sum and matches the oracle;
+- bench.py itself under torch.distributed.run with the multi-process path forced at world 1.
+"""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, SEED
+
+pytestmark = pytest.mark.gpu
+
+W, H = 64, 36
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _plain_accumulators(name, frames, part_index=0, part_count=1):
+    """Per frame (spp, base): a plain context's accumulator after clear + trace, as 3 x npix."""
+    from conftest import scene
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, W, H)
+    out = []
+    with NativeContext(a, seed=SEED, part_index=part_index, part_count=part_count) as ctx:
+        for spp, base in frames:
+            ctx.accum_clear()
+            ctx.trace_accumulate(spp, base)
+            m = ctx.accum_read_mean(1.0)
+            out.append(np.concatenate([m[:, c] for c in range(3)]))
+    return out
+
+
+def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks):
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import torch
+    import torch.distributed as dist
+
+    from conftest import scene
+    from mafrixraytracing_amd.distributed import native_partitioned_render
+    from mafrixraytracing_amd.native import NativeContext
+
+    torch.cuda.set_device(0)
+    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    a = scene(name, W, H)
+    acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
+    with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world) as ctx:
+        pr = native_partitioned_render(ctx, acc, rank, world)
+        got = []
+        for spp, base in frames:
+            pr.frame(spp, base, all_ranks=all_ranks)
+            got.append(acc.cpu().numpy().copy())
+        ctx.accum_attach(None)
+    if rank == 0:
+        np.save(os.path.join(outdir, "frames.npy"), np.stack(got))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _spawn(world, backend, name, frames, outdir, all_ranks):
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks),
+                       nprocs=world, join=True, start_method="spawn")
+    return np.load(os.path.join(outdir, "frames.npy"))
+
+
+FRAMES = [(3, 0), (5, 3), (1, 8), (4, 9)]  # (spp, sample base) per frame: one-sample frames included
+
+
+def test_world1_nccl_sequence_bit_identical(gpu, tmp_path):
+    """World-1 RCCL group through native_partitioned_render: attach, clear, trace, sync, a real
+    reduce, torch sync — the accumulator of every frame equals a plain context's bit for bit."""
+    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False)
+    want = _plain_accumulators("spot", FRAMES)
+    for k in range(len(FRAMES)):
+        assert np.array_equal(got[k], want[k]), k
+
+
+def test_two_ranks_on_one_device_gloo_allreduce(gpu, oracle, tmp_path):
+    """Two ranks sharing device 0, gloo all_reduce on CUDA tensors: the reduced accumulator is the
+    sum of the two partitioned contexts' (a0 + a1, exact for two terms in either order), and the
+    image is within 1e-12 of the oracle's whole sample set."""
+    frames = [(4, 0), (3, 4)]
+    got = _spawn(2, "gloo", "cube_cornell", frames, tmp_path, True)
+    p0 = _plain_accumulators("cube_cornell", frames, 0, 2)
+    p1 = _plain_accumulators("cube_cornell", frames, 1, 2)
+    from conftest import scene
+    o = oracle.OracleScene(scene("cube_cornell", W, H))
+    npix = W * H
+    for k, (spp, base) in enumerate(frames):
+        assert np.array_equal(got[k], p0[k] + p1[k]), k
+        ref = o.sample(spp, SEED, sample_base=base)
+        img = np.stack([got[k][c * npix:(c + 1) * npix] for c in range(3)], 1) / spp
+        assert np.abs(img - ref[:, :3]).max() <= 1e-12, k
+
+
+def test_bench_multiprocess_path_under_torchrun(gpu, tmp_path):
+    """bench.py under torch.distributed.run (the driver's launch) with the multi-process path
+    forced at world 1: process group, attached accumulator and RCCL reduce in the timed step; one
+    JSON line with the metric, and the same ray count as the plain single-process run."""
+    env = dict(os.environ, MFX_BENCH_FORCE_DIST="1")
+    common = ["--steps", "2", "--warmup", "1", "--spp", "2", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=1", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py")] + common
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + common, capture_output=True, text=True,
+                        timeout=300, cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    plain = json.loads(r1.stdout.strip().splitlines()[-1])
+    assert line["metric"] == plain["metric"] and line["n_gpus"] == 1
+    assert "process group" in line["config"]["parallelism"]
+    # rays per step are a property of the sample set: equal whichever path traced it
+    assert line["rays_per_step"] == plain["rays_per_step"] > 0

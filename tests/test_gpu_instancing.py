@@ -73,7 +73,8 @@ def test_instanced_closest_and_shadow_exact(gpu, oracle, seed):
     ot, op, on = o.closest_hit(rays)
     tmax = rng.uniform(0.05, 3.0, size=len(rays))
     occ_o = o.any_hit(rays, tmax)
-    with NativeContext(a) as ctx:
+    from mafrixraytracing_amd.abi import MFX_F_TWO_LEVEL
+    with NativeContext(a, flags=MFX_F_TWO_LEVEL) as ctx:
         info = ctx.instancing_info()
         gt, gp, gn = ctx.closest_hit(rays)
         occ_g = ctx.any_hit(rays, tmax)
@@ -95,7 +96,9 @@ def test_instanced_images_exact(gpu, oracle):
     o = oracle.OracleScene(a)
     ref4, st4 = o.sample(4, SEED, with_stats=True)
     ref1, st1 = o.sample(1, SEED, sample_base=4, with_stats=True)
-    with NativeContext(a, seed=SEED) as ctx:
+    from mafrixraytracing_amd.abi import MFX_F_TWO_LEVEL
+    with NativeContext(a, seed=SEED, flags=MFX_F_TWO_LEVEL) as ctx:
+        assert ctx.instancing_info()["instances"] > 0
         img4 = ctx.sample(4)
         c4 = ctx.ray_counts()[:3].copy()
         img1 = ctx.sample(1)  # continues at global sample 4: the megakernel call
@@ -106,12 +109,13 @@ def test_instanced_images_exact(gpu, oracle):
 
 
 def test_instanced_equals_flattened_and_flat(gpu):
-    from mafrixraytracing_amd.abi import MFX_F_FLATTEN, MFX_F_HOST_BVH, MFX_F_NONE
+    from mafrixraytracing_amd.abi import MFX_F_FLATTEN, MFX_F_HOST_BVH, MFX_F_NONE, MFX_F_TWO_LEVEL
     from mafrixraytracing_amd.native import NativeContext
     a = instanced_scene(np.random.default_rng(31), n_soup=2000, w=96, h=54)
     out = {}
-    for name, kw in {"two-level": dict(flags=MFX_F_NONE), "two-level host": dict(flags=MFX_F_HOST_BVH),
-                     "flattened": dict(flags=MFX_F_FLATTEN), "flat": dict(instancing=False)}.items():
+    for name, kw in {"two-level": dict(flags=MFX_F_TWO_LEVEL), "two-level host": dict(flags=MFX_F_HOST_BVH | MFX_F_TWO_LEVEL),
+                     "flattened": dict(flags=MFX_F_FLATTEN), "auto": dict(flags=MFX_F_NONE),
+                     "flat": dict(instancing=False)}.items():
         with NativeContext(a, seed=SEED, **kw) as ctx:
             img = ctx.sample(8)
             out[name] = (img, ctx.ray_counts()[:3].copy(), ctx.build_info()["digest"])
@@ -121,16 +125,18 @@ def test_instanced_equals_flattened_and_flat(gpu):
         assert np.array_equal(img, ref[0]), name
     assert out["two-level"][2] == out["two-level host"][2]  # the template BVH: GPU build == host build
     assert out["flattened"][2] == out["flat"][2]             # MFX_F_FLATTEN builds the flat scene's images
+    assert out["auto"][2] == out["flat"][2]                  # it fits the budget: flattened by default
 
 
 def test_c5_instanced_full_size_matches_flat(gpu):
     """C5 at its 4K film: the two-level context against the flat one, 2 spp through the wavefront
     and one megakernel call, bit for bit, with identical ray counts."""
     from mafrixraytracing_amd.native import NativeContext
+    from mafrixraytracing_amd.abi import MFX_F_TWO_LEVEL
     a = scene("spot16_instanced")
     res = []
     for inst in (True, False):
-        with NativeContext(a, seed=SEED, instancing=inst) as ctx:
+        with NativeContext(a, seed=SEED, instancing=inst, flags=MFX_F_TWO_LEVEL if inst else 0) as ctx:
             ctx.accum_clear()
             ctx.trace_accumulate(2, 3)
             img = ctx.accum_read_mean(2.0)

@@ -62,6 +62,26 @@ def test_repeated_device_list_sums_partitions_in_device_order(gpu, oracle, G):
     assert np.sqrt((diff ** 2).mean(axis=0)).max() <= 1e-4 and diff.max() <= 1e-12
 
 
+def test_repeated_device_reduce_orders_later_work(gpu):
+    """mfx_accum_reduce then, with no mfx_sync, another trace onto the same accumulators: the peers'
+    streams wait for the primary's copies of their buffers, so the reduced frame holds
+    only the first trace's samples — equal to the same calls with a sync after the reduce."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("cube_cornell", 48, 27)
+    out = []
+    for synced in (False, True):
+        with NativeContext(a, seed=SEED, devices=[0, 0, 0]) as m:
+            m.accum_clear()
+            m.trace_accumulate(6, 0)
+            m.accum_reduce()
+            if synced:
+                m.sync()
+            m.trace_accumulate(5, 6)  # no clear: every device adds onto its buffer
+            m.accum_reduce()
+            out.append(m.accum_read_mean(1.0))
+    assert np.array_equal(out[0], out[1])
+
+
 def test_repeated_device_render_and_stats(gpu, oracle):
     """Scene.Render on a 2-device context: the film on devices[0] holds the reduced frames;
     mfx_stats sums rays over the devices."""

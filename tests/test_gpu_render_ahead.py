@@ -33,6 +33,30 @@ def test_render_ahead_frames_are_the_one_sample_frames(gpu, name, w, h, K):
     assert rays_plain > 0 and rays_ahead > 0
 
 
+def test_render_ahead_pipeline_survives_interleaved_calls(gpu):
+    """30 calls over ~8 batches (the next batch traced and post-processed in the background while
+    one is served): frames without pixels (rgba = NULL), an mfx_sample call that moves the sample
+    sequence mid-batch, a film read mid-batch and a reset; every frame, the Sample image and the
+    film equal the one-sample-per-call context's."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 51, 29)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, render_ahead=4) as c2:
+        for k in range(30):
+            if k == 6:
+                assert np.array_equal(c1.sample(3), c2.sample(3))
+            if k == 11:
+                assert np.array_equal(c1.film_mean(), c2.film_mean())
+            if k == 17:
+                c1.reset()
+                c2.reset()
+            want = k % 3 != 1
+            r1 = c1.render_rgba8(1, want_pixels=want)
+            r2 = c2.render_rgba8(1, want_pixels=want)
+            if want:
+                assert np.array_equal(r1, r2), k
+        assert np.array_equal(c1.film_mean(), c2.film_mean())
+
+
 def test_render_ahead_stats_account_for_whole_batches(gpu):
     """The batch call reports K samples' rays and device time; held calls report 0 rays in 0 s;
     over K calls the rays equal K one-sample calls'."""

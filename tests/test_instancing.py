@@ -16,7 +16,7 @@ import pytest
 from conftest import SCENES
 
 from mafrixraytracing_amd import abi, scene_io
-from mafrixraytracing_amd.abi import INSTANCE_DTYPE, MFX_F_FLATTEN, MFX_INSTANCE_VERBATIM, PRIM_DTYPE
+from mafrixraytracing_amd.abi import INSTANCE_DTYPE, MFX_F_FLATTEN, MFX_F_TWO_LEVEL, MFX_INSTANCE_VERBATIM, PRIM_DTYPE
 
 
 @pytest.fixture(scope="module")
@@ -107,8 +107,10 @@ def test_expansion_rejects_bad_instances(rows, msg):
 
 def test_c5_two_level_images(c5):
     flat, inst = c5
-    two = abi.build_instanced_info(inst)
+    two = abi.build_instanced_info(inst, MFX_F_TWO_LEVEL)
     one = abi.build_instanced_info(inst, MFX_F_FLATTEN)
+    auto = abi.build_instanced_info(inst)  # fits the flatten budget: the flat image by default
+    assert auto == one
     _, _, _, finfo = abi.build_leaves(flat)
     assert two["instances"] == 16 and two["templates"] == 1
     assert two["template_slots"] == 5856 and two["top_slots"] == 2  # spot's triangles once; the floor rect
@@ -129,7 +131,7 @@ def test_single_use_ranges_are_flattened():
     I = np.array(rows, dtype=INSTANCE_DTYPE)
     W = abi.expand_instances(T, I)
     a = abi.SceneArrays(W, base.albedo, base.light, base.camera, 32, 18, instancing=(T, I))
-    info = abi.build_instanced_info(a)
+    info = abi.build_instanced_info(a, MFX_F_TWO_LEVEL)
     assert info["instances"] == 2 and info["templates"] == 1
     slots = lambda p: int((p["kind"] == 1).sum()) * 2 + int((p["kind"] != 1).sum())
     assert info["template_slots"] == slots(T[:20]) and info["top_slots"] == slots(T[20:40])
@@ -139,3 +141,13 @@ def test_loader_rejects_bad_offsets(tmp_path):
     text = open(os.path.join(SCENES, "spot16_instanced.xml")).read().replace("-1.8,0.0,-2.7;", "-1.8,0.0;")
     with pytest.raises(scene_io.SceneError, match="offset"):
         scene_io.InitSceneState(text, base_dir=SCENES, manager=scene_io.MaterialManager())
+
+
+def test_flatten_budget_selects_two_level(c5, monkeypatch):
+    """Without a flag the library flattens an instanced scene whose flat image fits
+    MFX_FLATTEN_MAX_BYTES (512 B per traversal slot of the expansion); below it, two-level."""
+    _, inst = c5
+    monkeypatch.setenv("MFX_FLATTEN_MAX_BYTES", str(93698 * 512))
+    assert abi.build_instanced_info(inst)["instances"] == 0
+    monkeypatch.setenv("MFX_FLATTEN_MAX_BYTES", str(93698 * 512 - 1))
+    assert abi.build_instanced_info(inst)["instances"] == 16
