@@ -443,14 +443,16 @@ def main():
                 base = kname.split("<")[0]
                 for kk, kv in tdroof["kernels"].items():
                     if kk.split("<")[0] == base:
-                        lines = kv["tcp_accesses_per_launch"]
+                        lines = kv["line_lookups_per_launch"]
                         ach = lines / (kms / launches / 1e3) / 1e9
                         peak = tdroof["peak"]["lines_per_clock"] * kv["clock_mhz"] * 1e6 / 1e9
                         return {"bound": "td", "achieved": round(ach, 2), "peak": round(peak, 2),
                                 "unit": "G line-lookups/s", "frac": round(ach / peak, 4),
                                 "frac_pmc_pass": round(kv["frac_of_peak"], 4),
-                                "td_busy_frac": round(kv["td_busy_frac"], 4), "ta_busy_frac": round(kv["ta_busy_frac"], 4),
-                                "lines_per_launch": lines, "clock_mhz_pmc_pass": round(kv["clock_mhz"], 1),
+                                "td_busy_frac": round(kv["td_busy_frac"], 4),
+                                "td_busy_frac_peak_case": round(tdroof["peak"]["td_busy_frac"], 4),
+                                "lines_per_launch": lines, "l2_reads_per_launch": kv["l2_reads_per_launch"],
+                                "clock_mhz_pmc_pass": round(kv["clock_mhz"], 1),
                                 "peak_case": tdroof["peak"]["case"],
                                 "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
                 return None

@@ -85,7 +85,7 @@ typedef struct mfx_scene_desc {
     int64_t nprims;
     const double* albedo; /* [nmat][3] Lambert albedo per MaterialManager slot (Material.fs:29-37);
                              Metal -> its albedo (Material.fs:68), SpecularTransmission -> 0 (:121) */
-    int32_t nmat;
+    int32_t nmat;      /* at most 65,536 (the path pool keeps a vertex's material in 16 bits) */
     int32_t width;     /* Film width  (Scene.fs:201-211) */
     int32_t height;    /* Film height */
     int32_t max_depth; /* PathIntegrator maxDepth; the reference hard-codes 3 (Scene.fs:304) */
@@ -301,6 +301,13 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
  * left to the FP64 test) and the vertex-box proof's (1 proved to pass, 0 not proved). Wherever a
  * shortcut decides it must agree with the FP64 answer.                                         */
 int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out);
+
+/* Device self-test of the FP32 triangle screen the leaf test can put in front of the FP64
+ * Triangle.Hit (Trangle.fs:120-155; MFX_LEAF_SCREEN32 builds): rec = n records of 18 doubles
+ * (origin[3], direction[3], v0[3], e1[3], e2[3], tMin, beyond, tMax); out = 3 doubles per record:
+ * the FP64 test's hit (0/1) and t, and the screen's skip (1: it claims the FP64 test misses, or hits
+ * at beyond < t < tMax). A skip where the FP64 test hits at t <= beyond or t >= tMax is an error.  */
+int mfx_tri_screen_selftest(int32_t device, int64_t n, const double* rec, double* out);
 
 /* ---- misc -------------------------------------------------------------------------------- */
 const char* mfx_last_error(void);

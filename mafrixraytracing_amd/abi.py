@@ -81,11 +81,14 @@ class SceneArrays:
 
     prims is the world primitive list (the reference's flat scene). `instancing`, when given, is
     (templates, instances): the same world scene as template primitives and mfx_instance entries
-    whose expansion is `prims` (mfx_create_instanced traces it two-level)."""
+    whose expansion is `prims` (mfx_create_instanced: flattened when the flat image fits the library's
+    budget, two-level otherwise). two_level: ask for the two-level traversal regardless
+    (MFX_F_TWO_LEVEL)."""
 
     def __init__(self, prims: np.ndarray, albedo: np.ndarray, light: dict, camera: dict,
-                 width: int, height: int, max_depth: int = 3, instancing=None):
+                 width: int, height: int, max_depth: int = 3, instancing=None, two_level: bool = False):
         self.prims = np.ascontiguousarray(prims, dtype=PRIM_DTYPE)
+        self.two_level = bool(two_level)
         self.instancing = None
         if instancing is not None:
             self.instancing = (np.ascontiguousarray(instancing[0], dtype=PRIM_DTYPE),
@@ -120,7 +123,7 @@ class SceneArrays:
 
     def with_film(self, width: int, height: int) -> "SceneArrays":
         return SceneArrays(self.prims, self.albedo, self.light, self.camera, width, height, self.max_depth,
-                           self.instancing)
+                           self.instancing, self.two_level)
 
     def flat(self) -> "SceneArrays":
         """The same scene without its instancing (the reference's flat primitive list)."""
@@ -165,6 +168,7 @@ def _bind(lib):
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
         "mfx_fp64_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _dp, _dp]),
         "mfx_aabb_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _ip]),
+        "mfx_tri_screen_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp]),
         "mfx_build_leaves": (C.c_int, [_P(MfxSceneDesc), _ip, _ip, _ip, _ip, _ip]),
         "mfx_build_info": (C.c_int, [C.c_void_p, _dp, _P(C.c_uint64)]),
         "mfx_last_error": (C.c_char_p, []),
@@ -183,7 +187,7 @@ EXPORTED_SYMBOLS = [
     "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
-    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_tri_screen_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 
 _lib = None

@@ -90,6 +90,8 @@ struct AheadBuf {
     unsigned long long* counters = nullptr;  // the batch's ray counters [WF_SHARDS][WF_NCTR]
     hipEvent_t t0 = nullptr, t1 = nullptr;   // around the batch's trace
     hipEvent_t ready = nullptr;         // frames computed
+    uint8_t* host = nullptr;            // [cap][npix][4] page-locked host copy of the frames (or null)
+    hipEvent_t host_ready = nullptr;    // the host copy is complete
     int64_t base = 0, n = 0;            // samples held (n == 0: empty)
     int64_t k0 = 0;                     // frames computed from index k0 on
     int64_t expect = 0;                 // the index whose frame a call may take next
@@ -103,6 +105,7 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
+    MfxTri32* d_tri32 = nullptr;  // FP32 triangle copies of the slots (the leaf screen)
     MfxSlot* d_slots = nullptr;
     int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
@@ -163,6 +166,9 @@ struct mfx_ctx {
     uint64_t film_epoch = 1;         // bumped when the film leaves the held frames' sequence
     bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its planes)
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
+    hipStream_t xfer_stream = nullptr;  // whole batches of frames to page-locked host memory
+    unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
+    bool ab_pinned = true;              // frames reach the caller from a page-locked copy (MFX_AHEAD_PINNED=0: off)
     bool rep_valid = false;          // the last call was served from held frames: its stats are rep_*
     double rep_counts[16] = {0};
     double rep_ms = 0.0;
@@ -187,7 +193,8 @@ static void ahead_free(mfx_ctx* c) {
     for (AheadBuf& B : c->ab) {
         for (void* b : {(void*)B.planes, (void*)B.frames, (void*)B.film_in, (void*)B.film_out, (void*)B.counters})
             if (b) (void)hipFree(b);
-        for (hipEvent_t e : {B.t0, B.t1, B.ready})
+        if (B.host) (void)hipHostFree(B.host);
+        for (hipEvent_t e : {B.t0, B.t1, B.ready, B.host_ready})
             if (e) (void)hipEventDestroy(e);
         B = AheadBuf{};
     }
@@ -208,12 +215,14 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     ahead_free(c);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->xfer_stream) (void)hipStreamDestroy(c->xfer_stream);
+    if (c->h_counters) (void)hipHostFree(c->h_counters);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -251,10 +260,30 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipSetDevice(c->device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    CK(hipStreamCreateWithFlags(&c->xfer_stream, hipStreamNonBlocking));
+    if (const char* e = getenv("MFX_AHEAD_PINNED")) c->ab_pinned = atoi(e) != 0;
+    CK(hipHostMalloc((void**)&c->h_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
     CK(upload(&c->d_slots, c->host.slots));
+    {  // v0, e1, e2 of every triangle slot rounded to FP32 (tri_skip32); spheres are never screened
+        std::vector<MfxTri32> t32(c->host.slots.size());
+        for (size_t i = 0; i < t32.size(); ++i) {
+            const MfxSlot& sl = c->host.slots[i];
+            MfxTri32& t = t32[i];
+            for (int k = 0; k < 3; ++k) {
+                t.v0[k] = (float)sl.a[k];
+                t.e1[k] = (float)sl.b[k];
+                t.e2[k] = (float)sl.c[k];
+            }
+            const int kind = (sl.info >> MFX_INFO_KIND_SHIFT) & 3;
+            t.flags = kind == MFX_KIND_SPHERE ? MFX_T32_NOSCREEN
+                                              : (kind == MFX_KIND_RECT && !(sl.info & MFX_INFO_RECT2) ? MFX_T32_RECT : 0);
+            t.pad[0] = t.pad[1] = 0.f;
+        }
+        CK(upload(&c->d_tri32, t32));
+    }
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
@@ -413,6 +442,7 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         return fail(MFX_E_INVALID, "mfx_create: bad device list");
     if (opt->render_ahead < 0 || opt->render_ahead > MFX_MAX_RENDER_AHEAD)
         return fail(MFX_E_INVALID, "mfx_create: render_ahead out of range");
+    if (scene->nmat > WF_MAT_MAX) return fail(MFX_E_INVALID, "mfx_create: more than 65,536 materials");
     int ndev = 0;
     HIPCHECK(hipGetDeviceCount(&ndev));
     std::vector<int> devlist;
@@ -585,7 +615,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     for (double** d : dbl) *d = (double*)take(P * 8);
     c->wf.vei = (double*)take(P * 8 * nv);
     c->wf.vls = (double*)take(P * 8 * 2 * nv);
-    c->wf.vmat = (int32_t*)take(P * 4 * nv);
+    c->wf.vmat = (WfMat*)take(P * sizeof(WfMat) * nv);
     c->wf.vstride = (int64_t)P;
     c->wf.key = (uint64_t*)take(P * 8);
     c->wf.rn = (uint32_t*)take(P * 4);
@@ -597,6 +627,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
+    P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
@@ -730,6 +761,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
+    P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
@@ -998,6 +1030,12 @@ static int ahead_alloc(mfx_ctx* c) {
         if (e == hipSuccess) e = hipEventCreate(&B.t0);
         if (e == hipSuccess) e = hipEventCreate(&B.t1);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&B.ready, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipEventCreateWithFlags(&B.host_ready, hipEventDisableTiming);
+        if (e == hipSuccess && c->ab_pinned && hipHostMalloc((void**)&B.host, (size_t)k * frame, hipHostMallocDefault) != hipSuccess) {
+            (void)hipGetLastError();  // no page-locked memory: frames copied per call instead
+            B.host = nullptr;
+            c->ab_pinned = false;
+        }
         if (e != hipSuccess) {
             (void)hipGetLastError();
             ahead_free(c);
@@ -1038,6 +1076,13 @@ static int ahead_frames(mfx_ctx* c, AheadBuf& B, int64_t k, const double* film_s
     HIPCHECK(mfx_launch_film_frames(B.planes, k, B.n, B.film_in, B.film_out, c->host.width, c->host.height, count0,
                                     B.frames, c->stream));
     HIPCHECK(hipEventRecord(B.ready, c->stream));
+    if (c->ab_pinned) {  // the whole batch's frames to page-locked host memory, behind the frames kernel
+        const size_t frame = 4 * (size_t)c->npix;
+        HIPCHECK(hipStreamWaitEvent(c->xfer_stream, B.ready, 0));
+        HIPCHECK(hipMemcpyAsync(B.host + k * frame, B.frames + k * frame, (size_t)(B.n - k) * frame,
+                                hipMemcpyDeviceToHost, c->xfer_stream));
+        HIPCHECK(hipEventRecord(B.host_ready, c->xfer_stream));
+    }
     B.k0 = k;
     B.expect = k;
     B.epoch = c->film_epoch;
@@ -1083,26 +1128,26 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     if (rc) return rc;
     AheadBuf& X = c->ab[xi];
     const int64_t k = s - X.base;
-    if (c->ab_nbuf == 2) {  // the next batch, in the background, unless the other buffer holds it
-        AheadBuf& Y = c->ab[1 - xi];
-        const double count_end = X.count0 + (double)(X.n - X.k0);  // frameCount after X's last call
-        if (!(Y.n > 0 && Y.base == X.base + X.n))
-            rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
-        else if (Y.epoch != c->film_epoch || Y.k0 != 0)  // held, but its frames assumed another film
-            rc = ahead_frames(c, Y, 0, X.film_out, count_end);
-        if (rc) return rc;
+    // This call's frame. A copy from device memory into the caller's pageable buffer waits for the
+    // whole device, a background batch included, so the batch's frames were copied to page-locked
+    // memory behind the frames kernel (ahead_frames) and the call copies its frame from there on
+    // the host; without page-locked memory, from the device before the next batch is enqueued.
+    const size_t frame = 4 * (size_t)c->npix;
+    if (c->ab_pinned) {
+        HIPCHECK(hipEventSynchronize(X.host_ready));
+        if (rgba) std::memcpy(rgba, X.host + k * frame, frame);
+    } else {
+        HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
+        if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * frame, frame, hipMemcpyDeviceToHost, c->copy_stream));
     }
-    // this call's frame: the copy waits for the frames only, not for the background batch
-    HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
-    if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * 4 * c->npix, 4 * (size_t)c->npix, hipMemcpyDeviceToHost,
-                                      c->copy_stream));
     for (int q = 0; q < 16; ++q) c->rep_counts[q] = 0.0;
     c->rep_ms = 0.0;
     if (!X.reported) {  // the first call served from a batch reports its rays and device time
-        unsigned long long h[WF_NCTR * WF_SHARDS];
-        HIPCHECK(hipMemcpyAsync(h, X.counters, sizeof(h), hipMemcpyDeviceToHost, c->copy_stream));
+        HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
+        HIPCHECK(hipMemcpyAsync(c->h_counters, X.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, c->copy_stream));
         HIPCHECK(hipStreamSynchronize(c->copy_stream));
-        sum_counters(h, c->rep_counts);
+        sum_counters(c->h_counters, c->rep_counts);
         c->rep_counts[3] = c->rep_counts[0];
         float f = 0.f;
         HIPCHECK(hipEventElapsedTime(&f, X.t0, X.t1));
@@ -1117,6 +1162,15 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     c->film_in_dfilm = false;
     c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
     c->next_sample += 1;
+    if (c->ab_nbuf == 2) {  // the next batch, in the background, unless the other buffer holds it
+        AheadBuf& Y = c->ab[1 - xi];
+        const double count_end = X.count0 + (double)(X.n - X.k0);  // frameCount after X's last call
+        if (!(Y.n > 0 && Y.base == X.base + X.n))
+            rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
+        else if (Y.epoch != c->film_epoch || Y.k0 != 0)  // held, but its frames assumed another film
+            rc = ahead_frames(c, Y, 0, X.film_out, count_end);
+        if (rc) return rc;
+    }
     return MFX_OK;
 }
 
@@ -1237,6 +1291,7 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         QueryParams Q;
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
+        Q.tri32 = c->d_tri32;
         Q.slots = c->d_slots;
     Q.slot_ref = c->d_slot_ref;
         Q.ref_blob = c->d_ref_blob;
@@ -1354,6 +1409,22 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
     for (void* p : {(void*)da, (void*)db, (void*)dd, (void*)ds})
         if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("fp64 selftest: ") + hipGetErrorString(e));
+    return MFX_OK;
+}
+
+int mfx_tri_screen_selftest(int32_t device, int64_t n, const double* rec, double* out) {
+    if (n <= 0 || !rec || !out) return fail(MFX_E_INVALID, "bad selftest arguments");
+    HIPCHECK(hipSetDevice(device));
+    double *dr = nullptr, *dout = nullptr;
+    hipError_t e = hipMalloc((void**)&dr, sizeof(double) * 18 * n);
+    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 3 * n);
+    if (e == hipSuccess) e = hipMemcpy(dr, rec, sizeof(double) * 18 * n, hipMemcpyHostToDevice);
+    if (e == hipSuccess) e = mfx_launch_tri_screen_selftest(dr, n, dout, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * 3 * n, hipMemcpyDeviceToHost);
+    if (dr) (void)hipFree(dr);
+    if (dout) (void)hipFree(dout);
+    if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("tri screen selftest: ") + hipGetErrorString(e));
     return MFX_OK;
 }
 

@@ -71,6 +71,20 @@ struct alignas(16) MfxSlot {
 #define MFX_LEAF_SLOTS_MAX 8
 #define MFX_SLOTS_MAX (1 << 27)  // leaf codes stay below MFX_INST_FLAG
 
+// FP32 copy of a traversal slot's triangle (v0, e1, e2 rounded to nearest) for the conservative
+// screen in front of the exact FP64 test (mfx_trace_common.h: tri_skip32): 48 B, three 16-B loads
+// instead of the FP64 slot's five. flags: MFX_T32_NOSCREEN (a sphere: never screened), MFX_T32_RECT
+// (first half of a rect: the next slot is its second half).
+struct alignas(16) MfxTri32 {
+    float v0[3];
+    float e1[3];
+    float e2[3];
+    int32_t flags;
+    float pad[2];
+};
+#define MFX_T32_NOSCREEN 1
+#define MFX_T32_RECT 2
+
 struct alignas(16) MfxShade {
     double n[3];        // face normal of this triangle slot; a sphere's centre
     double albedo[3];   // MaterialManager[material] flattened to its Lambert albedo (Material.fs:52-68)

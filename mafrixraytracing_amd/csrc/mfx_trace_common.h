@@ -235,6 +235,7 @@ __device__ __forceinline__ bool sphere_hit64(const MfxSlot& s, DV o, DV d, doubl
 
 struct SceneView {
     const MfxNode* __restrict__ nodes;
+    const MfxTri32* __restrict__ tri32;    // FP32 copies of the slots' triangles (the leaf screen)
     const MfxSlot* __restrict__ slots;     // traversal leaves: runs of MfxSlot records
     const int32_t* __restrict__ slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
@@ -455,6 +456,71 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
     return ok;
 }
 
+#ifndef MFX_LEAF_SCREEN32
+#define MFX_LEAF_SCREEN32 0  // 1: the FP32 triangle screen (tri_skip32) in front of every slot's FP64 test
+#endif
+
+// FP32 copy of the ray for tri_skip32 (o and d rounded to nearest)
+struct Ray32 {
+    float o[3], d[3];
+};
+__device__ __forceinline__ Ray32 ray32(DV o, DV d) {
+    return Ray32{{(float)o.x, (float)o.y, (float)o.z}, {(float)d.x, (float)d.y, (float)d.z}};
+}
+
+// The exact FP64 Triangle.Hit (tri_hit64, Trangle.fs:120-155) of this slot certainly cannot change
+// the leaf's result: it returns false (|div| < 1e-6, b1 < 0, b1 > 1, b2 < 0, b1 + b2 >= 1 or
+// t <= tMin), or a t certainly above `beyond` (the best hit of a closest query; +inf otherwise) and
+// below tMax (so no whole-reference-leaf evaluation either). false: undecided, the FP64 test runs.
+// Every quantity the FP64 test compares — div, and b1, b2, t times |div| with div's sign — is a
+// polynomial of degree <= 3 in o, v0, d, e1, e2. Computed in FP32 from the inputs rounded to
+// nearest, it differs from the FP64 test's value by less than 2^-16 Q + 1e-30, Q the polynomial
+// over the inputs' magnitudes (|o| + |v0| for o - v0): at most 3 input roundings of 2^-24 per
+// factor (o - v0 counts two) and 7 operation roundings along any term bound the FP32 error by
+// 12 * 2^-24 Q, the FP64 test's own error is below 2^-48 Q, and FP32 underflow adds at most 2^-126
+// per operation, so 2^-16 keeps a factor of 16. A decision is taken only when it holds for every
+// value in those intervals, with another 2^-20 for the FP64 quotients' roundings and for tMin /
+// beyond / tMax rounded to FP32. Magnitudes bound the values, so an overflow makes a margin
+// infinite; NaN and infinite values fail every comparison below and leave the slot undecided.
+__device__ __forceinline__ bool tri_skip32(const MfxTri32* __restrict__ p, const Ray32& r, float tmin, float beyond,
+                                           float tmax) {
+    const float4* __restrict__ q = (const float4*)p;
+    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+    if (__float_as_int(q2.y) & MFX_T32_NOSCREEN) return false;
+    const float E = 0x1p-16f, A = 1e-30f, U = 1.f + 0x1p-20f, L = 1.f - 0x1p-20f;
+    const float vx = q0.x, vy = q0.y, vz = q0.z, ax = q0.w, ay = q1.x, az = q1.y, bx = q1.z, by = q1.w, bz = q2.x;
+    const float dx = r.d[0], dy = r.d[1], dz = r.d[2];
+    const float adx = fabsf(dx), ady = fabsf(dy), adz = fabsf(dz);
+    // s1 = d x e2, div = s1 . e1
+    const float s1x = dy * bz - dz * by, s1y = dz * bx - dx * bz, s1z = dx * by - dy * bx;
+    const float S1x = ady * fabsf(bz) + adz * fabsf(by), S1y = adz * fabsf(bx) + adx * fabsf(bz),
+                S1z = adx * fabsf(by) + ady * fabsf(bx);
+    const float div = s1x * ax + s1y * ay + s1z * az;
+    const float Ed = E * (S1x * fabsf(ax) + S1y * fabsf(ay) + S1z * fabsf(az)) + A;
+    const float adv = fabsf(div);
+    if (adv + Ed < 1e-6f * L) return true;  // culled
+    const float lo = adv - Ed, hi = (adv + Ed) * U;
+    if (!(lo > 1e-6f * U)) return false;    // near the cull, or div's sign unknown
+    const float sg = div < 0.f ? -1.f : 1.f;
+    // dd = o - v0; b1 |div| = sg (dd . s1)
+    const float ddx = r.o[0] - vx, ddy = r.o[1] - vy, ddz = r.o[2] - vz;
+    const float Dx = fabsf(r.o[0]) + fabsf(vx), Dy = fabsf(r.o[1]) + fabsf(vy), Dz = fabsf(r.o[2]) + fabsf(vz);
+    const float n1 = sg * (ddx * s1x + ddy * s1y + ddz * s1z), E1 = E * (Dx * S1x + Dy * S1y + Dz * S1z) + A;
+    if (n1 + E1 < -A) return true;  // b1 < 0
+    if (n1 - E1 > hi) return true;  // b1 > 1
+    // s2 = dd x e1; b2 |div| = sg (d . s2), t |div| = sg (e2 . s2)
+    const float s2x = ddy * az - ddz * ay, s2y = ddz * ax - ddx * az, s2z = ddx * ay - ddy * ax;
+    const float S2x = Dy * fabsf(az) + Dz * fabsf(ay), S2y = Dz * fabsf(ax) + Dx * fabsf(az),
+                S2z = Dx * fabsf(ay) + Dy * fabsf(ax);
+    const float n2 = sg * (dx * s2x + dy * s2y + dz * s2z), E2 = E * (adx * S2x + ady * S2y + adz * S2z) + A;
+    if (n2 + E2 < -A) return true;                 // b2 < 0
+    if ((n1 - E1) + (n2 - E2) > hi) return true;   // b1 + b2 >= 1 (reached only with 0 <= b1 <= 1, b2 >= 0)
+    const float nt = sg * (bx * s2x + by * s2y + bz * s2z),
+                Et = E * (fabsf(bx) * S2x + fabsf(by) * S2y + fabsf(bz) * S2z) + A;
+    if (nt + Et < 0.f || nt + Et < tmin * L * lo) return true;                      // t <= tMin
+    return nt - Et > beyond * U * hi && nt + Et < tmax * L * lo;                     // beyond the best hit
+}
+
 // One traversal leaf (1..4 primitives of possibly different reference leaves; child code = first
 // slot << 3 | slots - 1). Each primitive hit is a candidate for its reference leaf's result: with
 // t < tMax the reference leaf's minBy result is a hit of t no larger (the leaf's other primitives
@@ -474,7 +540,28 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     if (STATS) st.clusters++;
     bool improved = false;
     constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
+#if MFX_LEAF_SCREEN32
+    const Ray32 r32 = ray32(o, d);
+    const float tmin32 = (float)tMin, tmax32 = (float)tMax;
+#endif
     for (int k = 0; k < n; ++k) {
+#if MFX_LEAF_SCREEN32
+        {  // slots the FP64 test certainly rejects (a rect: both halves) are skipped unread
+            const float beyond = (!SHADOW && B.found) ? (float)B.t : __builtin_inff();
+            const MfxTri32* t32 = S.tri32 + s0 + k;
+            if (tri_skip32(t32, r32, tmin32, beyond, tmax32)) {
+                if (!(__float_as_int(((const float4*)t32)[2].y) & MFX_T32_RECT)) {
+                    if (STATS) st.prims++;
+                    continue;
+                }
+                if (tri_skip32(t32 + 1, r32, tmin32, beyond, tmax32)) {
+                    if (STATS) st.prims++;
+                    ++k;
+                    continue;
+                }
+            }
+        }
+#endif
 #if MFX_LEAF_PRELOAD
         SlotR r = load_slot(sl + k);
         // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)

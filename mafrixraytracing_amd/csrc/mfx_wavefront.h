@@ -57,9 +57,23 @@
 #define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
 #define WF_NCTL (2 * WF_SHARDS)
 
+// A vertex record's material: 16 bits (k_resolve reads every vertex level's array nearly whole, so
+// its bytes are the kernel's cost); scenes are limited to 65,536 materials (mfx_create checks).
+#ifndef MFX_VMAT16
+#define MFX_VMAT16 1
+#endif
+#if MFX_VMAT16
+typedef uint16_t WfMat;
+#define WF_MAT_MAX 65536
+#else
+typedef int32_t WfMat;
+#define WF_MAT_MAX 0x7fffffff
+#endif
+
 struct WfParams {
     // scene
     const MfxNode* nodes;
+    const MfxTri32* tri32;  // FP32 triangle copies per slot (MFX_LEAF_SCREEN32)
     const MfxSlot* slots;
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
@@ -74,7 +88,7 @@ struct WfParams {
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
     double *dx, *dy, *dz;  // ray direction
     double* vei;           // [vertex][stride] the vertex's cosine ei = n . wi (Material.fs:35)
-    int32_t* vmat;         // [vertex][stride] its material (MaterialManager slot)
+    WfMat* vmat;           // [vertex][stride] its material (MaterialManager slot)
     double* vls;           // [vertex][2][stride] a lit vertex's cs = unit . n and solid = |cos_o| A / dist^2
     int64_t vstride;       // slots per vertex-record row (the allocated pool)
     const double* albedo;  // [nmat][3] Lambert albedo per material (Material.fs:29-37)

@@ -435,7 +435,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
     int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -602,7 +602,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -727,7 +727,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const int v = P.max_depth - (dw & 0xff);          // this vertex's index
                     // the operands of col = INVPI * a * ei * TwoPi (Material.fs:36), c_v (k_resolve)
                     P.vei[v * P.vstride + j] = ei;
-                    P.vmat[v * P.vstride + j] = mat;
+                    P.vmat[v * P.vstride + j] = (WfMat)mat;
                     // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56)
                     // is the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0.
                     // Its operands cs and solid travel with the shadow ray.

@@ -10,7 +10,7 @@ import ctypes as C
 
 import numpy as np
 
-from .abi import (INSTANCING_KEYS, MFX_F_NONE, MfxInstance, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
+from .abi import (INSTANCING_KEYS, MFX_F_NONE, MFX_F_TWO_LEVEL, MfxInstance, MfxOptions, SceneArrays, check, dptr, iptr, load_library)
 
 DEFAULT_SEED = 0x4D414652
 DEFAULT_RENDER_AHEAD = 64  # fsharp/Native.fs DefaultRenderAhead: Scene.Render served from batches of 64 samples
@@ -32,6 +32,8 @@ class NativeContext:
         self.arrays = arrays
         self.w, self.h = arrays.width, arrays.height
         inst = instancing and arrays.instancing is not None
+        if inst and getattr(arrays, "two_level", False):
+            flags |= MFX_F_TWO_LEVEL
         self._desc = arrays.desc(templates=inst)
         self.devices = list(devices) if devices else [device]
         self._devs = (C.c_int32 * len(self.devices))(*self.devices)
@@ -207,6 +209,16 @@ def aabb_selftest(rec: np.ndarray, device: int = 0):
     out = np.zeros((len(rec), 3), dtype=np.int32)
     check(lib.mfx_aabb_selftest(device, len(rec), dptr(rec), iptr(out)), "mfx_aabb_selftest")
     return out[:, 0], out[:, 1], out[:, 2]
+
+
+def tri_screen_selftest(rec: np.ndarray, device: int = 0):
+    """(FP64 Triangle.Hit hit, its t, the FP32 screen's skip) for n x 18 records
+    (mfx_tri_screen_selftest)."""
+    lib = load_library()
+    rec = np.ascontiguousarray(rec, dtype=np.float64).reshape(-1, 18)
+    out = np.zeros((len(rec), 3))
+    check(lib.mfx_tri_screen_selftest(device, len(rec), dptr(rec), dptr(out)), "mfx_tri_screen_selftest")
+    return out[:, 0].astype(bool), out[:, 1], out[:, 2].astype(bool)
 
 
 # ---- the reference's object model -----------------------------------------------------------

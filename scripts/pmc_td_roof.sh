@@ -1,8 +1,8 @@
 #!/bin/bash
 # The TD (texture-data / vector-memory) roof of the trace kernels, in one rocprofv3 --pmc pass each
-# (kernel trace on, no other trace domain): TCP_TOTAL_ACCESSES (cache-line lookups: one per line a
-# wave memory instruction touches), TD_TD_BUSY, TA_TA_BUSY and GRBM_GUI_ACTIVE (GPU clocks per
-# dispatch), on (1) the bench step and (2) the peak case of scripts/ubench/td_gather (every lane a
+# (kernel trace on, no other trace domain): TCP_TOTAL_CACHE_ACCESSES (L1 tag lookups: one per line a
+# wave memory instruction touches), TCP_TCC_READ_REQ (L1 misses), TD_TD_BUSY and GRBM_GUI_ACTIVE
+# (GPU clocks per dispatch), on (1) the bench step and (2) the peak case of scripts/ubench/td_gather (every lane a
 # distinct line of an L1-resident table). scripts/summarize_td.py writes profiles/td_<scene>.json,
 # which bench.py reads for roofline.td.
 # Usage: scripts/pmc_td_roof.sh TAG [extra bench args...]
@@ -13,7 +13,7 @@ shift || true
 OUT=$R/gpurun_out/tdroof_$TAG
 mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
-CTR="TCP_TOTAL_ACCESSES_sum TD_TD_BUSY_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE"
+CTR="TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE"
 timeout -s KILL 240 rocprofv3 --kernel-trace --pmc $CTR --output-format csv -d $OUT/bench -o run -- \
     python3 $R/bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-stats --no-render-api "$@" > $OUT/bench.log 2>&1
 timeout -s KILL 120 rocprofv3 --kernel-trace --pmc $CTR --output-format csv -d $OUT/ubench -o run -- \

@@ -1,10 +1,13 @@
 """Summarise scripts/pmc_td_roof.sh's passes into profiles/td_<scene>.json (bench.py roofline.td).
 
-Per trace kernel, per launch: TCP_TOTAL_ACCESSES (line lookups), TD / TA busy cycles (summed over
-the 256 TDs / TAs) and GRBM_GUI_ACTIVE (GPU clocks of the dispatch); the dispatch's duration gives
-the clock the pass ran at. The roof is the same counters over the td_gather peak case: line
-lookups per GPU clock when every lane of every wave loads a distinct L1-resident line. The
-fraction a kernel reaches of it is (its lookups per clock) / (the peak's), clock-independent.
+Per trace kernel, per launch: TCP_TOTAL_CACHE_ACCESSES (L1 tag lookups: cache lines touched per
+wave memory instruction), TCP_TCC_READ_REQ (L1 misses read from L2), TD busy cycles (summed over
+the 256 TDs) and GRBM_GUI_ACTIVE (GPU clocks of the dispatch, summed over the 8 XCDs); the
+dispatch's duration gives the clock the pass ran at. (TCP_TOTAL_ACCESSES counts lanes, 64 per wave
+instruction whatever the lines: round 2's per-instruction figure.) The roof is the same counters
+over the td_gather peak case, every lane of every wave a distinct L1-resident line: its lookups per
+GPU clock and its TD busy fraction. A kernel's fraction is (its lookups per clock) / (the peak's),
+clock-independent; td_busy_frac is the share of TD cycles the kernel keeps busy.
 Usage: python3 scripts/summarize_td.py OUTDIR [bench args...]"""
 import collections
 import csv
@@ -14,7 +17,8 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-N_TD = 256  # one TD and one TA per CU
+N_TD = 256  # one TD per CU
+N_XCD = 8  # GRBM_GUI_ACTIVE is summed over the XCDs
 
 
 def per_dispatch(path):
@@ -41,8 +45,10 @@ def main():
         scene = os.path.splitext(os.path.basename(args[args.index("--scene") + 1]))[0]
     ub = [v for (i, k), v in per_dispatch(os.path.join(out, "ubench")).items() if k.startswith("void gather") or "gather" in k]
     ub = [v for v in ub if v.get("GRBM_GUI_ACTIVE", 0) > 0]
-    peak_lpc = max(v["TCP_TOTAL_ACCESSES_sum"] / v["GRBM_GUI_ACTIVE"] for v in ub)
-    peak_v = max(ub, key=lambda v: v["TCP_TOTAL_ACCESSES_sum"] / v["GRBM_GUI_ACTIVE"])
+    for v in ub:
+        v["cyc"] = v["GRBM_GUI_ACTIVE"] / N_XCD
+    peak_v = max(ub, key=lambda v: v["TCP_TOTAL_CACHE_ACCESSES_sum"] / v["cyc"])
+    peak_lpc = peak_v["TCP_TOTAL_CACHE_ACCESSES_sum"] / peak_v["cyc"]
     kern = collections.defaultdict(lambda: collections.defaultdict(float))
     for (i, k), v in per_dispatch(os.path.join(out, "bench")).items():
         name = k.replace("void ", "")
@@ -52,28 +58,28 @@ def main():
         for c, x in v.items():
             kern[name][c] += x
         kern[name]["launches"] += 1
-    res = {"scene": scene, "config": cfg, "counters": "TCP_TOTAL_ACCESSES_sum TD_TD_BUSY_sum TA_TA_BUSY_sum GRBM_GUI_ACTIVE",
+    res = {"scene": scene, "config": cfg,
+           "counters": "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TD_TD_BUSY_sum GRBM_GUI_ACTIVE",
            "peak": {"case": "scripts/ubench/td_gather peak: 64 active lanes, each a distinct 64-B line of a 16 KB "
                             "(L1-resident) table, 16-B loads, 4 independent per round",
                     "lines_per_clock": peak_lpc,
-                    "td_busy_frac": peak_v["TD_TD_BUSY_sum"] / (peak_v["GRBM_GUI_ACTIVE"] * N_TD),
-                    "clock_mhz": peak_v["GRBM_GUI_ACTIVE"] / peak_v["ns"] * 1e3},
+                    "td_busy_frac": peak_v["TD_TD_BUSY_sum"] / (peak_v["cyc"] * N_TD),
+                    "clock_mhz": peak_v["cyc"] / peak_v["ns"] * 1e3},
            "kernels": {}}
     for name, v in kern.items():
         n = v["launches"]
-        cyc = v["GRBM_GUI_ACTIVE"]
+        cyc = v["GRBM_GUI_ACTIVE"] / N_XCD
         res["kernels"][name] = {
             "launches": n,
-            "tcp_accesses_per_launch": v["TCP_TOTAL_ACCESSES_sum"] / n,
+            "line_lookups_per_launch": v["TCP_TOTAL_CACHE_ACCESSES_sum"] / n,
+            "l2_reads_per_launch": v["TCP_TCC_READ_REQ_sum"] / n,
             "td_busy_per_launch": v["TD_TD_BUSY_sum"] / n,
-            "ta_busy_per_launch": v["TA_TA_BUSY_sum"] / n,
             "gpu_clocks_per_launch": cyc / n,
             "ms_per_launch": v["ns"] / n / 1e6,
             "clock_mhz": cyc / v["ns"] * 1e3,
-            "lines_per_clock": v["TCP_TOTAL_ACCESSES_sum"] / cyc,
-            "frac_of_peak": v["TCP_TOTAL_ACCESSES_sum"] / cyc / peak_lpc,
+            "lines_per_clock": v["TCP_TOTAL_CACHE_ACCESSES_sum"] / cyc,
+            "frac_of_peak": v["TCP_TOTAL_CACHE_ACCESSES_sum"] / cyc / peak_lpc,
             "td_busy_frac": v["TD_TD_BUSY_sum"] / (cyc * N_TD),
-            "ta_busy_frac": v["TA_TA_BUSY_sum"] / (cyc * N_TD),
         }
     dst = os.path.join(ROOT, "profiles", f"td_{scene}.json")
     with open(os.path.join(out, "td.json"), "w") as f:

@@ -40,8 +40,12 @@ def gpu():
 
 
 def scene(name, w=None, h=None, max_depth=3):
+    """scenes/<name>.xml; "<name>@2l": an instanced scene traced two-level (MFX_F_TWO_LEVEL) instead
+    of the library's default (flattened when it fits)."""
     from mafrixraytracing_amd.scene_io import load_scene_file
-    a = load_scene_file(os.path.join(SCENES, name + ".xml"), max_depth=max_depth)
+    two = name.endswith("@2l")
+    a = load_scene_file(os.path.join(SCENES, name.replace("@2l", "") + ".xml"), max_depth=max_depth)
+    a.two_level = two
     if w is not None:
         a = a.with_film(w, h)
     return a

@@ -10,7 +10,7 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced"]
+SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced", "spot16_instanced@2l"]
 
 
 def both(a):
@@ -28,7 +28,8 @@ def test_gpu_bvh_equals_host_bvh(gpu, name):
     a = scene(name, 16, 16)
     bg, bh = both(a)
     assert bg["gpu_bvh"] and not bh["gpu_bvh"]
-    assert bg["gpu_images"] == (a.instancing is None)  # flat scenes: collapse and layout on the GPU too
+    # flat (and auto-flattened) scenes: collapse and layout on the GPU too
+    assert bg["gpu_images"] == (a.instancing is None or not a.two_level)
     for k in ("nodes2", "nodes4", "slots"):
         assert bg[k] == bh[k], (k, bg[k], bh[k])
     assert bg["digest"] == bh["digest"]

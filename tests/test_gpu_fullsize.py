@@ -14,7 +14,7 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-FULL = ["spot", "cube_cornell", "renault", "spot16", "spot16_instanced"]  # C2-C5 at their film sizes (C5 flat and two-level)
+FULL = ["spot", "cube_cornell", "renault", "spot16", "spot16_instanced@2l"]  # C2-C5 at their film sizes (C5 flat and two-level)
 
 
 @pytest.mark.parametrize("name", FULL)

@@ -14,7 +14,7 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced"]
+SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced@2l"]
 
 
 def random_rays(arrays, n, rng, camera_frac=0.5):
@@ -104,7 +104,7 @@ def test_fp64_device_math_bit_exact(gpu):
     ("cube_cornell", 64, 36, 8),
     ("renault", 64, 36, 4),
     ("spot16", 64, 36, 4),
-    ("spot16_instanced", 64, 36, 4),
+    ("spot16_instanced@2l", 64, 36, 4),
 ])
 @pytest.mark.parametrize("mode", ["wavefront", "megakernel"])
 def test_image_parity(gpu, oracle, name, w, h, spp, mode):

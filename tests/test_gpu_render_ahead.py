@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("name,w,h,K", [("spot", 67, 37, 4), ("cube_cornell", 48, 27, 5),
-                                         ("spot16_instanced", 40, 24, 3), ("two_spheres_plane", 32, 32, 2)])
+                                         ("spot16_instanced@2l", 40, 24, 3), ("two_spheres_plane", 32, 32, 2)])
 def test_render_ahead_frames_are_the_one_sample_frames(gpu, name, w, h, K):
     """12 Scene.Render calls with a reset after the 7th and an spp = 2 call in between (traced by
     the plain path; the next one-sample call still takes its plane from the held batch): identical
