@@ -90,8 +90,6 @@ struct AheadBuf {
     unsigned long long* counters = nullptr;  // the batch's ray counters [WF_SHARDS][WF_NCTR]
     hipEvent_t t0 = nullptr, t1 = nullptr;   // around the batch's trace
     hipEvent_t ready = nullptr;         // frames computed
-    uint8_t* host = nullptr;            // [cap][npix][4] page-locked host copy of the frames (or null)
-    hipEvent_t host_ready = nullptr;    // the host copy is complete
     int64_t base = 0, n = 0;            // samples held (n == 0: empty)
     int64_t k0 = 0;                     // frames computed from index k0 on
     int64_t expect = 0;                 // the index whose frame a call may take next
@@ -166,9 +164,9 @@ struct mfx_ctx {
     uint64_t film_epoch = 1;         // bumped when the film leaves the held frames' sequence
     bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its planes)
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
-    hipStream_t xfer_stream = nullptr;  // whole batches of frames to page-locked host memory
     unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
-    bool ab_pinned = true;              // frames reach the caller from a page-locked copy (MFX_AHEAD_PINNED=0: off)
+    uint8_t* h_stage = nullptr;         // page-locked staging of large readbacks (host_readback)
+    size_t h_stage_bytes = 0;
     bool rep_valid = false;          // the last call was served from held frames: its stats are rep_*
     double rep_counts[16] = {0};
     double rep_ms = 0.0;
@@ -193,8 +191,7 @@ static void ahead_free(mfx_ctx* c) {
     for (AheadBuf& B : c->ab) {
         for (void* b : {(void*)B.planes, (void*)B.frames, (void*)B.film_in, (void*)B.film_out, (void*)B.counters})
             if (b) (void)hipFree(b);
-        if (B.host) (void)hipHostFree(B.host);
-        for (hipEvent_t e : {B.t0, B.t1, B.ready, B.host_ready})
+        for (hipEvent_t e : {B.t0, B.t1, B.ready})
             if (e) (void)hipEventDestroy(e);
         B = AheadBuf{};
     }
@@ -221,8 +218,8 @@ static void free_ctx(mfx_ctx* c) {
         if (b) (void)hipFree(b);
     ahead_free(c);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    if (c->xfer_stream) (void)hipStreamDestroy(c->xfer_stream);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -260,13 +257,12 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipSetDevice(c->device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     CK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    CK(hipStreamCreateWithFlags(&c->xfer_stream, hipStreamNonBlocking));
-    if (const char* e = getenv("MFX_AHEAD_PINNED")) c->ab_pinned = atoi(e) != 0;
     CK(hipHostMalloc((void**)&c->h_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
     CK(upload(&c->d_slots, c->host.slots));
+#if MFX_LEAF_SCREEN32
     {  // v0, e1, e2 of every triangle slot rounded to FP32 (tri_skip32); spheres are never screened
         std::vector<MfxTri32> t32(c->host.slots.size());
         for (size_t i = 0; i < t32.size(); ++i) {
@@ -284,6 +280,7 @@ static int ctx_setup(mfx_ctx* c) {
         }
         CK(upload(&c->d_tri32, t32));
     }
+#endif
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
@@ -938,15 +935,46 @@ int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
     return MFX_OK;
 }
 
+// Device -> caller's (pageable) host memory, stream-ordered, complete on return. A pageable
+// destination is slow for large copies (mfx_sample's 66 MB FP64 frame at 1080p: ~10 ms, r03b), so a
+// large readback goes to a page-locked staging buffer by DMA and from there to the caller's buffer
+// by host threads; a small one (or with no staging memory) is a plain copy.
+static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    const size_t kLarge = 16u << 20;
+    if (bytes >= kLarge && bytes > c->h_stage_bytes) {
+        if (c->h_stage) (void)hipHostFree(c->h_stage);
+        c->h_stage = nullptr;
+        c->h_stage_bytes = 0;
+        if (hipHostMalloc((void**)&c->h_stage, bytes, hipHostMallocDefault) == hipSuccess) c->h_stage_bytes = bytes;
+        else (void)hipGetLastError();
+    }
+    if (bytes < kLarge || !c->h_stage) {
+        HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        return MFX_OK;
+    }
+    HIPCHECK(hipMemcpyAsync(c->h_stage, src, bytes, hipMemcpyDeviceToHost, st));
+    HIPCHECK(hipStreamSynchronize(st));
+    const int nt = 4;
+    const size_t part = (bytes / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) {
+        const size_t off = part * t;
+        if (off >= bytes) break;
+        th.emplace_back([=] { std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, bytes - off)); });
+    }
+    std::memcpy(dst, c->h_stage, std::min(part, bytes));
+    for (auto& t : th) t.join();
+    return MFX_OK;
+}
+
 int mfx_accum_read_mean(mfx_ctx* c, double count, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     if (!(count > 0.0)) return fail(MFX_E_INVALID, "mfx_accum_read_mean: count must be > 0");
     HIPCHECK(hipSetDevice(c->device));
     // texture[i,j] <- color / float n (Integrators.fs:171): divided by the count itself
     HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, count, c->d_frame, c->stream));
-    HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    return MFX_OK;
+    return host_readback(c, frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, c->stream);
 }
 
 int mfx_sync(mfx_ctx* c) {
@@ -1030,12 +1058,6 @@ static int ahead_alloc(mfx_ctx* c) {
         if (e == hipSuccess) e = hipEventCreate(&B.t0);
         if (e == hipSuccess) e = hipEventCreate(&B.t1);
         if (e == hipSuccess) e = hipEventCreateWithFlags(&B.ready, hipEventDisableTiming);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&B.host_ready, hipEventDisableTiming);
-        if (e == hipSuccess && c->ab_pinned && hipHostMalloc((void**)&B.host, (size_t)k * frame, hipHostMallocDefault) != hipSuccess) {
-            (void)hipGetLastError();  // no page-locked memory: frames copied per call instead
-            B.host = nullptr;
-            c->ab_pinned = false;
-        }
         if (e != hipSuccess) {
             (void)hipGetLastError();
             ahead_free(c);
@@ -1076,13 +1098,6 @@ static int ahead_frames(mfx_ctx* c, AheadBuf& B, int64_t k, const double* film_s
     HIPCHECK(mfx_launch_film_frames(B.planes, k, B.n, B.film_in, B.film_out, c->host.width, c->host.height, count0,
                                     B.frames, c->stream));
     HIPCHECK(hipEventRecord(B.ready, c->stream));
-    if (c->ab_pinned) {  // the whole batch's frames to page-locked host memory, behind the frames kernel
-        const size_t frame = 4 * (size_t)c->npix;
-        HIPCHECK(hipStreamWaitEvent(c->xfer_stream, B.ready, 0));
-        HIPCHECK(hipMemcpyAsync(B.host + k * frame, B.frames + k * frame, (size_t)(B.n - k) * frame,
-                                hipMemcpyDeviceToHost, c->xfer_stream));
-        HIPCHECK(hipEventRecord(B.host_ready, c->xfer_stream));
-    }
     B.k0 = k;
     B.expect = k;
     B.epoch = c->film_epoch;
@@ -1128,22 +1143,16 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     if (rc) return rc;
     AheadBuf& X = c->ab[xi];
     const int64_t k = s - X.base;
-    // This call's frame. A copy from device memory into the caller's pageable buffer waits for the
-    // whole device, a background batch included, so the batch's frames were copied to page-locked
-    // memory behind the frames kernel (ahead_frames) and the call copies its frame from there on
-    // the host; without page-locked memory, from the device before the next batch is enqueued.
+    // This call's frame, on the copy stream behind this batch's frames only: it overlaps the
+    // background batch. Everything the call reads back goes there before the next batch is
+    // enqueued, and the counters go to page-locked memory: a pageable copy enqueued behind the
+    // background batch waited for it (r03b: 6,794 Mrays/s, 73 % of batch; r03c: 8,579, 93 %).
     const size_t frame = 4 * (size_t)c->npix;
-    if (c->ab_pinned) {
-        HIPCHECK(hipEventSynchronize(X.host_ready));
-        if (rgba) std::memcpy(rgba, X.host + k * frame, frame);
-    } else {
-        HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
-        if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * frame, frame, hipMemcpyDeviceToHost, c->copy_stream));
-    }
+    HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
+    if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * frame, frame, hipMemcpyDeviceToHost, c->copy_stream));
     for (int q = 0; q < 16; ++q) c->rep_counts[q] = 0.0;
     c->rep_ms = 0.0;
     if (!X.reported) {  // the first call served from a batch reports its rays and device time
-        HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
         HIPCHECK(hipMemcpyAsync(c->h_counters, X.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long),
                                 hipMemcpyDeviceToHost, c->copy_stream));
         HIPCHECK(hipStreamSynchronize(c->copy_stream));
@@ -1267,9 +1276,7 @@ int mfx_film_mean(mfx_ctx* c, double* frame) {
     const int rc = ahead_materialize(c);
     if (rc) return rc;
     HIPCHECK(mfx_launch_film_mean(c->d_film, c->npix, c->frame_count, c->d_frame, c->stream));
-    HIPCHECK(hipMemcpyAsync(frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    return MFX_OK;
+    return host_readback(c, frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, c->stream);
 }
 
 static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, double tmax, const double* tmax_arr,

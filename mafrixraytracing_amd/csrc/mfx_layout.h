@@ -82,6 +82,9 @@ struct alignas(16) MfxTri32 {
     int32_t flags;
     float pad[2];
 };
+#ifndef MFX_LEAF_SCREEN32
+#define MFX_LEAF_SCREEN32 0  // 1: the FP32 screen in front of every slot's FP64 test (r03c: -27 to -33 %, spills)
+#endif
 #define MFX_T32_NOSCREEN 1
 #define MFX_T32_RECT 2
 

@@ -456,10 +456,6 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
     return ok;
 }
 
-#ifndef MFX_LEAF_SCREEN32
-#define MFX_LEAF_SCREEN32 0  // 1: the FP32 triangle screen (tri_skip32) in front of every slot's FP64 test
-#endif
-
 // FP32 copy of the ray for tri_skip32 (o and d rounded to nearest)
 struct Ray32 {
     float o[3], d[3];
