@@ -117,6 +117,8 @@ struct WfParams {
     int32_t ntop_ext, ntop_shd;           // top BVH nodes each trace kernel keeps in LDS (<= nodes)
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
+    const int32_t* order;                 // k_extend: non-null (MFX_RAY_SORT): take the slots of this sorted
+                                          // list ([pool], -1 = none) instead of scanning state words
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
@@ -141,5 +143,11 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
                             hipEvent_t* ev);
 // after a generation's last iteration: add its finished paths' radiance to their pixels
 hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st);
+// MFX_RAY_SORT (mfx_raysort.hip): the pool's NEED_EXT slots sorted by origin cell and direction bin
+// into vals_out (-1 past the last one); tmp: hipcub temporary storage of mfx_raysort_tmp_bytes(pool)
+hipError_t mfx_raysort(const WfParams& P, const float lo[3], const float hi[3], int obits, int dbits, uint16_t* keys_in,
+                       uint16_t* keys_out, int32_t* vals_in, int32_t* vals_out, void* tmp, size_t tmp_bytes,
+                       hipStream_t st);
+size_t mfx_raysort_tmp_bytes(int64_t n);
 
 #endif

@@ -437,6 +437,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
     const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
+    // the words the scan reads: state words, or a sorted slot list (MFX_RAY_SORT, iterations >= 1)
+    const bool sorted = P.order != nullptr;
+    const int32_t* __restrict__ words = sorted ? P.order : P.state;
 
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
@@ -460,24 +463,30 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 // list at least 64 slots to trace (or all that are left) from as many windows as it
                 // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, words)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
-                    bool take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
-                    if (P.start && sj == WF_FREE && j < P.total) {
-                        int x, y;
-                        int64_t smp;
-                        // edge-tile padding starts no path (none when 8 divides the film size)
-                        take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
+                    bool take;
+                    int ent;
+                    if (sorted) {  // a listed slot (extension ray), or -1
+                        take = sj >= 0;
+                        ent = sj;
+                    } else {
+                        take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
+                        if (P.start && sj == WF_FREE && j < P.total) {
+                            int x, y;
+                            int64_t smp;
+                            // edge-tile padding starts no path (none when 8 divides the film size)
+                            take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
+                        }
+                        // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
+                        ent = sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
                     }
                     const uint64_t tm = __ballot(take);
-                    // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
-                    if (take)
-                        pend[n + __popcll(tm & lanes_below())] =
-                            sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
+                    if (take) pend[n + __popcll(tm & lanes_below())] = ent;
                     n += __popcll(tm);
-                    sc.advance(P.state);
+                    sc.advance(words);
                 }
                 wave_lds_sync();
 #if MFX_OCTANT_SORT
