@@ -143,6 +143,8 @@ struct mfx_ctx {
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
+    double wf_tail_frac = 0.0;  // share of each shard taken in tail chunks at a launch's end
+    int wf_tail_chunk = 128;
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
@@ -341,6 +343,8 @@ static int ctx_setup(mfx_ctx* c) {
     }
     if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
+    if (const char* e = getenv("MFX_TAIL_FRAC")) c->wf_tail_frac = std::max(0.0, std::min(0.5, atof(e)));
+    if (const char* e = getenv("MFX_TAIL_CHUNK")) c->wf_tail_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(e) / 64 * 64));
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
     CK(hipMemset(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
@@ -738,6 +742,11 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         P.base_q = P.path_base % per_sample;
         P.total = std::min<int64_t>(gen_max, total - P.path_base);
         P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
+        {  // each shard's tail region: a multiple of 64 slots
+            const int shard = P.pool / WF_SHARDS;
+            P.tail_size = (int32_t)((int64_t)(shard * c->wf_tail_frac) / 64 * 64);
+            P.tail_chunk = c->wf_tail_chunk;
+        }
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
         for (int d = 0; d <= P.max_depth; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;

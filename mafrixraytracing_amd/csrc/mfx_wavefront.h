@@ -55,7 +55,8 @@
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
 #define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
-#define WF_NCTL (2 * WF_SHARDS)
+#define WF_CTL_TAIL (2 * WF_SHARDS)  // + either: [WF_SHARDS] heads of the shards' tail regions
+#define WF_NCTL (4 * WF_SHARDS)
 
 // A vertex record's material: 16 bits (k_resolve reads every vertex level's array nearly whole, so
 // its bytes are the kernel's cost); scenes are limited to 65,536 materials (mfx_create checks).
@@ -111,6 +112,8 @@ struct WfParams {
     int32_t stack_lds_ext, stack_lds_shd; // of which in LDS, per kernel; the rest in `spill`
     int32_t* spill;                       // [stack_size - stack_lds][grid * 256] deep stack entries
     int32_t chunk;                        // slots per chunk fetch of the kernels
+    int32_t tail_size;                    // the last tail_size slots of each shard are taken in chunks of
+    int32_t tail_chunk;                   // tail_chunk slots once no shard has bulk chunks left (0: no tail)
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q

@@ -126,6 +126,7 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
 struct Scanner {
     int win_next, win_end, shard;
     bool exhausted;
+    bool in_tail;  // every shard's bulk region is taken: chunks now come from the tail regions
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
     // work are skipped with no further memory round trip. Slots of a taken chunk change only
@@ -133,22 +134,49 @@ struct Scanner {
     int b[WF_LOOKAHEAD];
     int nbuf;
     // Make [win_next, win_end) non-empty; false once every chunk has been taken. A wave takes
-    // chunks from its block's home shard while it lasts, then from the next open shard.
-    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
-                                           const int32_t* __restrict__ state) {
+    // chunks from its block's home shard while it lasts, then from the next open shard. Each shard
+    // is a bulk region taken in `chunk`-slot chunks and a tail region (its last tail_size slots)
+    // taken in tail_chunk-slot chunks once no shard has bulk left, so the launch ends on small
+    // chunks: a 1024-slot chunk of camera rays is ~1 ms of one wave's time, and the waves that
+    // took the last big chunks would otherwise run on while the others have left.
+    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size, int tail_size,
+                                           int tail_chunk, const int32_t* __restrict__ state) {
         if (win_next < win_end) return true;
         if (exhausted) return false;
+        const int bulk = shard_size - tail_size;
         while (true) {
+            if (!in_tail) {
+                unsigned long long c = 0;
+                if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
+                c = __shfl(c, 0);
+                if ((int64_t)c < bulk) {
+                    win_next = shard * shard_size + (int)c;
+                    win_end = shard * shard_size + min((int)c + chunk, bulk);
+                    fill(state);
+                    return true;
+                }
+                const uint64_t open = open_shards(heads, bulk);
+                if (open != 0) {
+                    shard = next_open(open, shard);
+                    continue;
+                }
+                in_tail = true;
+                if (tail_size == 0) {
+                    exhausted = true;
+                    return false;
+                }
+            }
+            unsigned long long* th = heads + WF_CTL_TAIL;
             unsigned long long c = 0;
-            if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
+            if (lane_id() == 0) c = atomicAdd(th + shard, (unsigned long long)tail_chunk);
             c = __shfl(c, 0);
-            if ((int64_t)c < shard_size) {
-                win_next = shard * shard_size + (int)c;
-                win_end = shard * shard_size + min((int)c + chunk, shard_size);
+            if ((int64_t)c < tail_size) {
+                win_next = shard * shard_size + bulk + (int)c;
+                win_end = shard * shard_size + bulk + min((int)c + tail_chunk, tail_size);
                 fill(state);
                 return true;
             }
-            const uint64_t open = open_shards(heads, shard_size);
+            const uint64_t open = open_shards(th, tail_size);
             if (open == 0) {
                 exhausted = true;
                 return false;
@@ -463,7 +491,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 // list at least 64 slots to trace (or all that are left) from as many windows as it
                 // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, words)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.tail_size, P.tail_chunk, words)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -642,7 +670,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
+                while (nshade < 64 &&
+                       sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.tail_size, P.tail_chunk, P.state)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
