@@ -186,14 +186,18 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * progressive mean through ACES -> sqrt -> int(255.99 c) as RGBA8, y-major:
  * rgba[(y*w + x)*4 + {0,1,2,3}]. `Scene.Render(delta, buffer)` is this call with spp = 1.
  * rgba may be NULL (accumulate only).
- * Render-ahead (mfx_options.render_ahead = K > 1, one device, part_count 1): a call with spp = 1
- * whose global sample is not held traces the next K samples in one batched pass (each sample's
- * 1-spp image kept in its own FP64 plane, K x 24 B per pixel of HBM) and the following K - 1
- * calls only add their plane to the film and post it. Every frame's bytes equal the one-sample
- * path's (a sample's image depends only on the seed and its global index); the cost is one call
- * in K taking the batch's time. mfx_stats: the batch call reports the K samples' rays and device
- * time, the others 0 rays in 0 s. K is cut to the planes that fit in a quarter of the free HBM;
- * when not even two fit, the context renders one sample per call as without render-ahead.  */
+ * Render-ahead (mfx_options.render_ahead = K > 1, one device, part_count 1): one-sample calls are
+ * served from batches of K samples. A call whose global sample is not held traces the next K
+ * samples in one batched pass (each sample's 1-spp image in its own FP64 plane) and runs the film
+ * add and post of all K calls ahead, in call order; each call of the batch then only copies its
+ * RGBA8 frame, and while a batch is served the next one is traced in the background (two buffers
+ * of K x 28 B per pixel). Every frame's bytes and the film equal the one-sample path's (a sample's
+ * image depends only on the seed and its global index); mfx_reset, an spp != 1 call or mfx_sample
+ * in between make the held frames recompute from the film as it then is. mfx_stats: the first call
+ * served from a batch reports the K samples' rays and device time, the others 0 rays in 0 s. K is
+ * cut to what fits in a quarter of the free HBM (one buffer, no background batch, if two do not
+ * fit); when not even two samples fit, the context renders one sample per call. The accumulator
+ * (mfx_accum_read_mean) does not hold the samples of calls served from batches.                */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
 /* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */

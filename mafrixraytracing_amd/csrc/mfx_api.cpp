@@ -142,6 +142,7 @@ struct mfx_ctx {
     int generations = 0;
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
+    int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     double wf_tail_frac = 0.0;  // share of each shard taken in tail chunks at a launch's end
     int wf_tail_chunk = 128;
@@ -431,6 +432,15 @@ static int ctx_setup(mfx_ctx* c) {
         sbpc = std::min(sbpc, std::max(1, atoi(b)));
     }
     c->wf_ext_grid = prop.multiProcessorCount * std::max(1, std::min(ebpc, 8));
+    {  // camera-ray packets (flat scenes)
+        int cam = getenv("MFX_CAMERA_PACKETS") ? atoi(getenv("MFX_CAMERA_PACKETS")) : 1;
+        if (cam && !inst) {
+            int cb = 0;
+            CK(mfx_cam_occupancy(c->stack_size, &cb));
+            if (const char* e = getenv("MFX_CAM_BLOCKS")) cb = std::min(cb, std::max(1, atoi(e)));
+            c->wf_cam_grid = prop.multiProcessorCount * std::max(1, std::min(cb, 8));
+        }
+    }
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
     {  // deep traversal-stack entries of every lane of the larger grid
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
@@ -684,7 +694,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
-    const int64_t gen_max = std::min<int64_t>(total, c->wf_pool_max);
+    // generations of whole 64-path windows (one 8x8 tile of one sample each: the camera-ray packets)
+    const int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
     const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
     int rc = wf_ensure_pool(c, pool);
     if (rc) return rc;
@@ -713,6 +724,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     P.order = nullptr;
+    P.cam_grid = c->wf_cam_grid;
     if (c->ray_sort && c->rs_cap < pool) {  // sort buffers for the pool
         for (void* b : {(void*)c->rs_keys, (void*)c->rs_vals, c->rs_tmp})
             if (b) (void)hipFree(b);

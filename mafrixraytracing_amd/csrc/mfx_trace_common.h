@@ -380,6 +380,31 @@ __device__ __forceinline__ SlotR load_slot(const MfxSlot* __restrict__ p) {
     s.info = r4.w;
     return s;
 }
+// The same prefix from a wave-uniform slot address through scalar loads (packet traversal: every
+// lane tests the same slot, so the data comes from the scalar cache, not per lane)
+typedef int mfx_i4 __attribute__((ext_vector_type(4)));
+typedef float mfx_f4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(4))) const mfx_i4 mfx_ci4;
+typedef __attribute__((address_space(4))) const mfx_f4 mfx_cf4;
+__device__ __forceinline__ SlotR load_slot_u(const MfxSlot* __restrict__ p) {
+    mfx_ci4* q = (mfx_ci4*)p;
+    const mfx_i4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    SlotR s;
+    s.a = dv(i2d(r0.x, r0.y), i2d(r0.z, r0.w), i2d(r1.x, r1.y));
+    s.b = dv(i2d(r1.z, r1.w), i2d(r2.x, r2.y), i2d(r2.z, r2.w));
+    s.c = dv(i2d(r3.x, r3.y), i2d(r3.z, r3.w), i2d(r4.x, r4.y));
+    s.first = r4.z;
+    s.info = r4.w;
+    return s;
+}
+// a slot's reference-leaf box (bytes 80..127) through scalar loads
+__device__ __forceinline__ void load_box_u(const MfxSlot* __restrict__ p, double lo[3], double hi[3]) {
+    mfx_ci4* q = (mfx_ci4*)p;
+    const mfx_i4 r5 = q[5], r6 = q[6], r7 = q[7];
+    lo[0] = i2d(r5.x, r5.y); lo[1] = i2d(r5.z, r5.w); lo[2] = i2d(r6.x, r6.y);
+    hi[0] = i2d(r6.z, r6.w); hi[1] = i2d(r7.x, r7.y); hi[2] = i2d(r7.z, r7.w);
+}
+
 // Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148)
 __device__ __forceinline__ bool tri_hit64(const SlotR& s, DV o, DV d, double tMin, double& t) {
     DV s1 = vcross(d, s.c);
@@ -528,7 +553,8 @@ __device__ __forceinline__ bool tri_skip32(const MfxTri32* __restrict__ p, const
 // evaluated whole. SHADOW: returns true at the first occluding candidate. Closest: returns true
 // when B improved.
 // base: the slot index the code counts from (an instance's run of world slots; 0 otherwise).
-template <bool SHADOW, bool STATS>
+// UNI: the leaf is wave-uniform (packet traversal): its slots are read through scalar loads.
+template <bool SHADOW, bool STATS, bool UNI = false>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
                                          Best& B, Stats& st, int base = 0) {
     const int s0 = base + (code >> 3), n = (code & 7) + 1;
@@ -559,7 +585,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         }
 #endif
 #if MFX_LEAF_PRELOAD
-        SlotR r = load_slot(sl + k);
+        SlotR r = UNI ? load_slot_u(sl + k) : load_slot(sl + k);
         // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)
         double2 bx0 = make_double2(0, 0), bx1 = bx0, bx2 = bx0;
         if (PRE == 2) {
@@ -582,7 +608,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
                 ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
                 if (!hit) {
                     hs = k;
-                    r = load_slot(sl + k);
+                    r = UNI ? load_slot_u(sl + k) : load_slot(sl + k);
                     hit = tri_hit64(r, o, d, tMin, t);
                     info = r.info;
                     first = r.first;
@@ -636,6 +662,10 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
 #ifndef MFX_DIAG_NO_LEAFBOX  // timing experiment only: the reference leaf's box test assumed to pass
             if (!aabb_hit(blo, bhi, o, d, tMin, tMax)) continue;
 #endif
+        } else if (UNI) {
+            double blo[3], bhi[3];
+            load_box_u(sl + hs, blo, bhi);
+            if (!aabb_hit(blo, bhi, o, d, tMin, tMax)) continue;
         } else {
             if (!aabb_hit(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
         }
@@ -903,6 +933,83 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
     return next;
+}
+
+// ---- Packet traversal for coherent rays (the camera rays of one 8x8 tile: k_camera) ----------------
+// The wave walks the BVH4 together: the node is wave-uniform and read through scalar loads, each
+// lane tests the four children with its own FP32 ray and limit, and a child is visited when any
+// lane's test hits it. Each lane therefore visits a superset of the nodes its own traversal would
+// (a lane's limit only falls, so a child all lanes miss holds no candidate better than any lane's
+// final hit), and tests every leaf the wave visits; the per-candidate leaf semantics (leaf_hit)
+// make extra candidates harmless, so every lane's closest hit is the single-ray traversal's. Visit
+// order: near to far by the entry distances of the first active lane (children it misses last).
+// The stack is wave-uniform, in LDS.
+__device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
+                                                int* stk, int& sp, int rep) {
+    mfx_cf4* q = (mfx_cf4*)(nodes + node);
+    const mfx_f4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+    const mfx_i4 ch = ((mfx_ci4*)q)[6];
+    float d[4];
+    int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    int nh = 0;
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float a0 = fmaf(LX[k], r.ix, -r.oix), a1 = fmaf(HX[k], r.ix, -r.oix);
+        const float b0 = fmaf(LY[k], r.iy, -r.oiy), b1 = fmaf(HY[k], r.iy, -r.oiy);
+        const float c0 = fmaf(LZ[k], r.iz, -r.oiz), c1 = fmaf(HZ[k], r.iz, -r.oiz);
+        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+        const bool h = n <= f;
+        const bool any = __ballot(h) != 0;
+        const float kd = __shfl(h ? n : 3.0e38f, rep);
+        d[k] = any ? kd : __builtin_inff();
+        nh += any ? 1 : 0;
+    }
+    cswap(d[0], c[0], d[1], c[1]);
+    cswap(d[2], c[2], d[3], c[3]);
+    cswap(d[0], c[0], d[2], c[2]);
+    cswap(d[1], c[1], d[3], c[3]);
+    cswap(d[1], c[1], d[2], c[2]);
+    nh = __builtin_amdgcn_readfirstlane(nh);
+    if (nh >= 2) stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
+    if (nh >= 3) stk[sp + 1] = nh == 4 ? c[2] : c[1];
+    if (nh >= 4) stk[sp + 2] = c[1];
+    int next;
+    if (nh > 0) {
+        next = c[0];
+        sp += nh - 1;
+    } else if (sp > 0) {
+        next = stk[--sp];
+    } else {
+        next = MFX_TRAV_EXIT;
+    }
+    return __builtin_amdgcn_readfirstlane(next);
+}
+
+// Closest hits of the wave's active lanes (act) by packet traversal; B per lane as traverse() gives.
+template <bool STATS>
+__device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
+                                               int* stk, Stats& st) {
+    B = Best{tMax, -1, -1, false};
+    const RayF rf = make_rayf(o, d);
+    float tlim = act ? f_round_up(tMax) : -1.0f;  // an inactive lane hits nothing
+    const int rep = __builtin_ctzll(__ballot(act));
+    int sp = 0, node = 0;
+    while (true) {
+        while (node >= 0) {
+            if (STATS && act) st.nodes++;
+            node = packet_node_step(S.nodes, node, rf, tlim, stk, sp, rep);
+        }
+        if (node == MFX_TRAV_EXIT) return;
+        if (act) {
+            leaf_hit<false, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st);
+            tlim = f_round_up(B.t);
+        }
+        node = sp > 0 ? __builtin_amdgcn_readfirstlane(stk[--sp]) : MFX_TRAV_EXIT;
+    }
 }
 
 // Bvh.Hit over the primitive BVH4 (megakernel and query kernels). SHADOW: returns occluded

@@ -622,6 +622,70 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// k_camera: a generation's first iteration, camera rays traced as packets (MFX_CAMERA_PACKETS). A
+// 64-slot window is one 8x8 tile of one sample: its 64 camera rays are coherent, so
+// the wave traces them together (packet_closest: uniform nodes through scalar loads, one lane per
+// ray). Writes what k_extend writes for a camera ray: the hit point and HIT | FRESH | shade index,
+// or MISS | FRESH. Flat scenes only (two-level scenes take k_extend).
+// ------------------------------------------------------------------------------------------------
+template <bool STATS>
+__global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_camera(WfParams P) {
+    extern __shared__ int lds_all[];
+    const int lane = lane_id();
+    const int wave = threadIdx.x >> 6;
+    int* stk = lds_all + wave * P.stack_size;
+    uint32_t* red = (uint32_t*)(lds_all + 4 * P.stack_size);
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
+    const int shard_size = P.pool / WF_SHARDS;
+    Scanner sc{};
+    sc.shard = blockIdx.x & (WF_SHARDS - 1);
+    uint32_t c_primary = 0;
+    Stats st{0, 0, 0};
+    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.tail_size, P.tail_chunk, P.state)) {
+        const int j = sc.win_next + lane;
+        const int sj = sc.word();
+        sc.advance(P.state);
+        int x = 0, y = 0;
+        int64_t smp = 0;
+        // edge-tile padding starts no path
+        const bool act = sj == WF_FREE && j < P.total && path_pixel(P, P.path_base + j, x, y, smp);
+        if (!__any(act)) continue;
+        DV o = dv(0, 0, 0), d = dv(0, 0, 1);
+        if (act) {  // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
+            const int64_t pixel = (int64_t)x * P.height + y;  // Color[w,h] x-major
+            const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
+            const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
+            uint32_t rn = 0;
+            const double u = ((double)x + rng_next(key, rn)) / (double)P.width;
+            const double v = ((double)y + rng_next(key, rn)) / (double)P.height;
+            const MfxCamera& CAM = P.cam;
+            const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
+            o = ld3(CAM.position);
+            d = vnormalize(vsub(target, o));
+            c_primary++;
+        }
+        Best B;
+        packet_closest<STATS>(S, act, o, d, 99999999., B, stk, st);  // Integrators.fs:108
+        if (act) {
+            if (B.found) {
+                const DV hp = vadd(o, vmul(d, B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
+                P.ox[j] = hp.x; P.oy[j] = hp.y; P.oz[j] = hp.z;
+                P.state[j] = ((B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | WF_FRESH;
+            } else {
+                P.state[j] = WF_MISS | WF_FRESH;
+            }
+        }
+    }
+    unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
+    block_add<4>(cnt + 0, c_primary, red);
+    if (STATS) {
+        block_add<4>(cnt + 4, st.nodes, red);
+        block_add<4>(cnt + 5, st.clusters, red);
+        block_add<4>(cnt + 6, st.prims, red);
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
 template <bool STATS, bool SPILL, int WAVES, bool INST>
@@ -1088,13 +1152,27 @@ static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t s
         hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
 }
 
+static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * sizeof(int) + 64; }
+
+hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_camera<false>, 256,
+                                                                      cam_lds_bytes(stack_size));
+    return e;
+}
+
 template <bool INST>
 static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                                    hipEvent_t* ev, size_t lds_e, size_t lds_s) {
     // each kernel keeps its own share of the traversal stack in LDS (the rest spills); k_shadow is
     // compiled for 3 waves per SIMD (up to 168 VGPRs) when its LDS allows no more blocks anyway
-    if (P.stack_lds_ext < P.stack_size) launch_extend<true, INST>(P, ext_grid, stats, st, lds_e);
-    else launch_extend<false, INST>(P, ext_grid, stats, st, lds_e);
+    if (!INST && P.start && P.cam_grid > 0) {  // camera rays as packets
+        if (stats) hipLaunchKernelGGL(k_camera<true>, dim3(P.cam_grid), dim3(256), cam_lds_bytes(P.stack_size), st, P);
+        else hipLaunchKernelGGL(k_camera<false>, dim3(P.cam_grid), dim3(256), cam_lds_bytes(P.stack_size), st, P);
+    } else if (P.stack_lds_ext < P.stack_size) {
+        launch_extend<true, INST>(P, ext_grid, stats, st, lds_e);
+    } else {
+        launch_extend<false, INST>(P, ext_grid, stats, st, lds_e);
+    }
     if (ev) {  // between the two kernels (per-stage timing); null: not recorded
         const hipError_t e = hipEventRecord(ev[0], st);
         if (e != hipSuccess) return e;

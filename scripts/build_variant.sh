@@ -9,4 +9,4 @@ if [ "$1" == "--src" ]; then SRC=$2; shift 2; fi
 mkdir -p $R/build_variants
 cd $SRC
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wall -Wno-unused-result \
-  -I$R/include "$@" -shared -o $R/build_variants/$NAME.so mfx_api.cpp mfx_scene.cpp mfx_kernels.hip mfx_wavefront.hip mfx_build.hip mfx_raysort.hip
+  -I$R/include "$@" -shared -o $R/build_variants/$NAME.so $(ls *.cpp *.hip) -ldl
