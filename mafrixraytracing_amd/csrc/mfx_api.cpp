@@ -144,8 +144,6 @@ struct mfx_ctx {
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
-    double wf_tail_frac = 0.0;  // share of each shard taken in tail chunks at a launch's end
-    int wf_tail_chunk = 128;
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
@@ -174,15 +172,7 @@ struct mfx_ctx {
     double rep_counts[16] = {0};
     double rep_ms = 0.0;
     bool diag_iter = false;
-    // MFX_RAY_SORT (experiment, mfx_raysort.hip): extension rays sorted by origin cell and direction bin
-    int ray_sort = 0, rs_obits = 4, rs_dbits = 3;
-    unsigned rs_iters = 0xe;          // iterations (bit d) whose k_extend takes the sorted list
-    uint16_t* rs_keys = nullptr;      // [2][rs_cap]
-    int32_t* rs_vals = nullptr;       // [2][rs_cap]
-    void* rs_tmp = nullptr;
-    size_t rs_tmp_bytes = 0;
-    int64_t rs_cap = 0;
-    float scene_lo[3] = {0, 0, 0}, scene_hi[3] = {1, 1, 1};
+
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
     std::vector<mfx_ctx*> peers;         // devices[1..G) of the device list, same host scene
@@ -224,7 +214,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->rs_keys, c->rs_vals, c->rs_tmp, c->d_nodes, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -322,30 +312,8 @@ static int ctx_setup(mfx_ctx* c) {
     }
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
-    if (const char* e = getenv("MFX_RAY_SORT")) c->ray_sort = atoi(e);
-    if (const char* e = getenv("MFX_RAY_SORT_OBITS")) c->rs_obits = std::max(0, std::min(4, atoi(e)));
-    if (const char* e = getenv("MFX_RAY_SORT_DBITS")) c->rs_dbits = atoi(e) == 6 ? 6 : 3;
-    if (const char* e = getenv("MFX_RAY_SORT_ITERS")) c->rs_iters = (unsigned)strtoul(e, nullptr, 0);
-    if (c->ray_sort) {  // the scene's bounds, for the origin cells
-        for (int k = 0; k < 3; ++k) {
-            c->scene_lo[k] = 3e38f;
-            c->scene_hi[k] = -3e38f;
-        }
-        for (const MfxSlot& sl : c->host.slots) {
-            const bool sph = ((sl.info >> MFX_INFO_KIND_SHIFT) & 3) == MFX_KIND_SPHERE;
-            for (int k = 0; k < 3; ++k) {
-                const double a = sl.a[k];
-                const double lo = sph ? a - sl.b[0] : std::min(a, std::min(a + sl.b[k], a + sl.c[k]));
-                const double hi = sph ? a + sl.b[0] : std::max(a, std::max(a + sl.b[k], a + sl.c[k]));
-                c->scene_lo[k] = std::min(c->scene_lo[k], (float)lo);
-                c->scene_hi[k] = std::max(c->scene_hi[k], (float)hi);
-            }
-        }
-    }
     if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
     if (const char* ck = getenv("MFX_CHUNK")) c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
-    if (const char* e = getenv("MFX_TAIL_FRAC")) c->wf_tail_frac = std::max(0.0, std::min(0.5, atof(e)));
-    if (const char* e = getenv("MFX_TAIL_CHUNK")) c->wf_tail_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(e) / 64 * 64));
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
     CK(hipMemset(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
@@ -723,22 +691,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
-    P.order = nullptr;
     P.cam_grid = c->wf_cam_grid;
-    if (c->ray_sort && c->rs_cap < pool) {  // sort buffers for the pool
-        for (void* b : {(void*)c->rs_keys, (void*)c->rs_vals, c->rs_tmp})
-            if (b) (void)hipFree(b);
-        c->rs_keys = nullptr;
-        c->rs_vals = nullptr;
-        c->rs_tmp = nullptr;
-        c->rs_cap = 0;
-        c->rs_tmp_bytes = mfx_raysort_tmp_bytes(pool);
-        hipError_t e = hipMalloc((void**)&c->rs_keys, 2 * sizeof(uint16_t) * (size_t)pool);
-        if (e == hipSuccess) e = hipMalloc((void**)&c->rs_vals, 2 * sizeof(int32_t) * (size_t)pool);
-        if (e == hipSuccess) e = hipMalloc(&c->rs_tmp, std::max<size_t>(c->rs_tmp_bytes, 256));
-        if (e != hipSuccess) return fail(MFX_E_NOMEM, std::string("ray sort buffers: ") + hipGetErrorString(e));
-        c->rs_cap = pool;
-    }
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
     while (own_events && (int)c->it_ev.size() < 3 * iters) {
@@ -754,35 +707,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         P.base_q = P.path_base % per_sample;
         P.total = std::min<int64_t>(gen_max, total - P.path_base);
         P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
-        {  // each shard's tail region: a multiple of 64 slots
-            const int shard = P.pool / WF_SHARDS;
-            P.tail_size = (int32_t)((int64_t)(shard * c->wf_tail_frac) / 64 * 64);
-            P.tail_chunk = c->wf_tail_chunk;
-        }
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
         for (int d = 0; d <= P.max_depth; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;
-            P.order = nullptr;
-            if (c->ray_sort && d > 0 && ((c->rs_iters >> d) & 1)) {
-                hipEvent_t s0 = nullptr, s1 = nullptr;
-                if (c->diag_iter) {
-                    HIPCHECK(hipEventCreate(&s0));
-                    HIPCHECK(hipEventCreate(&s1));
-                    HIPCHECK(hipEventRecord(s0, c->stream));
-                }
-                HIPCHECK(mfx_raysort(P, c->scene_lo, c->scene_hi, c->rs_obits, c->rs_dbits, c->rs_keys, c->rs_keys + c->rs_cap,
-                                     c->rs_vals, c->rs_vals + c->rs_cap, c->rs_tmp, c->rs_tmp_bytes, c->stream));
-                P.order = c->rs_vals + c->rs_cap;
-                if (c->diag_iter) {
-                    HIPCHECK(hipEventRecord(s1, c->stream));
-                    HIPCHECK(hipEventSynchronize(s1));
-                    float f = 0.f;
-                    HIPCHECK(hipEventElapsedTime(&f, s0, s1));
-                    fprintf(stderr, "gen %lld iter %d: ray sort %.3f ms\n", (long long)g, d + 1, f);
-                    (void)hipEventDestroy(s0);
-                    (void)hipEventDestroy(s1);
-                }
-            }
             if (!own_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;

@@ -944,13 +944,32 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
 // make extra candidates harmless, so every lane's closest hit is the single-ray traversal's. Visit
 // order: near to far by the entry distances of the first active lane (children it misses last).
 // The stack is wave-uniform, in LDS.
-__device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                                int* stk, int& sp, int rep) {
+// the node-step sort network over (distance, child, lane mask) triples
+__device__ __forceinline__ void cswap3(float& da, int& ca, uint64_t& ma, float& db, int& cb, uint64_t& mb) {
+    const bool s = db < da;
+    const float t = da;
+    const int u = ca;
+    const uint64_t w = ma;
+    da = s ? db : da;
+    ca = s ? cb : ca;
+    ma = s ? mb : ma;
+    db = s ? t : db;
+    cb = s ? u : cb;
+    mb = s ? w : mb;
+}
+// One node of the packet walk. `mask`, kept beside every stack entry, names the lanes whose own
+// test hit the node: only they test its children, so a leaf is tested by the lanes whose ray hits
+// its box (child boxes lie inside their parent's, so a lane that missed a node misses its subtree).
+// The stack is wave-uniform: stk[] nodes and stm[] masks in LDS.
+__device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ nodes, int node, uint64_t& mask,
+                                                const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp, int rep) {
     mfx_cf4* q = (mfx_cf4*)(nodes + node);
     const mfx_f4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     const mfx_i4 ch = ((mfx_ci4*)q)[6];
+    const bool live = (mask >> __lane_id()) & 1;
     float d[4];
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    uint64_t m[4];
     int nh = 0;
     const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
     const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
@@ -962,53 +981,76 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
         const float c0 = fmaf(LZ[k], r.iz, -r.oiz), c1 = fmaf(HZ[k], r.iz, -r.oiz);
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-        const bool h = n <= f;
-        const bool any = __ballot(h) != 0;
+        const bool h = live && n <= f;
+        m[k] = __ballot(h);
         const float kd = __shfl(h ? n : 3.0e38f, rep);
-        d[k] = any ? kd : __builtin_inff();
-        nh += any ? 1 : 0;
+        d[k] = m[k] ? kd : __builtin_inff();
+        nh += m[k] ? 1 : 0;
     }
-    cswap(d[0], c[0], d[1], c[1]);
-    cswap(d[2], c[2], d[3], c[3]);
-    cswap(d[0], c[0], d[2], c[2]);
-    cswap(d[1], c[1], d[3], c[3]);
-    cswap(d[1], c[1], d[2], c[2]);
+    cswap3(d[0], c[0], m[0], d[1], c[1], m[1]);
+    cswap3(d[2], c[2], m[2], d[3], c[3], m[3]);
+    cswap3(d[0], c[0], m[0], d[2], c[2], m[2]);
+    cswap3(d[1], c[1], m[1], d[3], c[3], m[3]);
+    cswap3(d[1], c[1], m[1], d[2], c[2], m[2]);
     nh = __builtin_amdgcn_readfirstlane(nh);
-    if (nh >= 2) stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
-    if (nh >= 3) stk[sp + 1] = nh == 4 ? c[2] : c[1];
-    if (nh >= 4) stk[sp + 2] = c[1];
+    if (nh >= 2) {
+        stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
+        stm[sp] = nh == 4 ? m[3] : (nh == 3 ? m[2] : m[1]);
+    }
+    if (nh >= 3) {
+        stk[sp + 1] = nh == 4 ? c[2] : c[1];
+        stm[sp + 1] = nh == 4 ? m[2] : m[1];
+    }
+    if (nh >= 4) {
+        stk[sp + 2] = c[1];
+        stm[sp + 2] = m[1];
+    }
     int next;
     if (nh > 0) {
         next = c[0];
+        mask = m[0];
         sp += nh - 1;
     } else if (sp > 0) {
-        next = stk[--sp];
+        --sp;
+        next = stk[sp];
+        mask = stm[sp];
     } else {
         next = MFX_TRAV_EXIT;
     }
+    mask = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(mask >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mask);
     return __builtin_amdgcn_readfirstlane(next);
 }
 
 // Closest hits of the wave's active lanes (act) by packet traversal; B per lane as traverse() gives.
 template <bool STATS>
 __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
-                                               int* stk, Stats& st) {
+                                               int* stk, uint64_t* stm, Stats& st) {
     B = Best{tMax, -1, -1, false};
     const RayF rf = make_rayf(o, d);
-    float tlim = act ? f_round_up(tMax) : -1.0f;  // an inactive lane hits nothing
-    const int rep = __builtin_ctzll(__ballot(act));
+    float tlim = f_round_up(tMax);
+    uint64_t mask = __ballot(act);
+    const int rep = __builtin_ctzll(mask);
     int sp = 0, node = 0;
     while (true) {
         while (node >= 0) {
-            if (STATS && act) st.nodes++;
-            node = packet_node_step(S.nodes, node, rf, tlim, stk, sp, rep);
+            if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
+            node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep);
         }
         if (node == MFX_TRAV_EXIT) return;
-        if (act) {
+        if ((mask >> __lane_id()) & 1) {  // the lanes whose ray hits the leaf's box
             leaf_hit<false, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st);
             tlim = f_round_up(B.t);
         }
-        node = sp > 0 ? __builtin_amdgcn_readfirstlane(stk[--sp]) : MFX_TRAV_EXIT;
+        if (sp > 0) {
+            --sp;
+            node = __builtin_amdgcn_readfirstlane(stk[sp]);
+            const uint64_t mm = stm[sp];
+            mask = ((uint64_t)__builtin_amdgcn_readfirstlane((int)(mm >> 32)) << 32) |
+                   (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mm);
+        } else {
+            return;
+        }
     }
 }
 

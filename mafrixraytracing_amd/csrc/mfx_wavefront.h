@@ -55,8 +55,7 @@
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
 #define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
-#define WF_CTL_TAIL (2 * WF_SHARDS)  // + either: [WF_SHARDS] heads of the shards' tail regions
-#define WF_NCTL (4 * WF_SHARDS)
+#define WF_NCTL (2 * WF_SHARDS)
 
 // A vertex record's material: 16 bits (k_resolve reads every vertex level's array nearly whole, so
 // its bytes are the kernel's cost); scenes are limited to 65,536 materials (mfx_create checks).
@@ -112,8 +111,6 @@ struct WfParams {
     int32_t stack_lds_ext, stack_lds_shd; // of which in LDS, per kernel; the rest in `spill`
     int32_t* spill;                       // [stack_size - stack_lds][grid * 256] deep stack entries
     int32_t chunk;                        // slots per chunk fetch of the kernels
-    int32_t tail_size;                    // the last tail_size slots of each shard are taken in chunks of
-    int32_t tail_chunk;                   // tail_chunk slots once no shard has bulk chunks left (0: no tail)
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
@@ -121,8 +118,6 @@ struct WfParams {
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
     int32_t cam_grid;                     // > 0: a generation's camera rays run k_camera (packets) on this grid
-    const int32_t* order;                 // k_extend: non-null (MFX_RAY_SORT): take the slots of this sorted
-                                          // list ([pool], -1 = none) instead of scanning state words
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
@@ -149,11 +144,6 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
                             hipEvent_t* ev);
 // after a generation's last iteration: add its finished paths' radiance to their pixels
 hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st);
-// MFX_RAY_SORT (mfx_raysort.hip): the pool's NEED_EXT slots sorted by origin cell and direction bin
-// into vals_out (-1 past the last one); tmp: hipcub temporary storage of mfx_raysort_tmp_bytes(pool)
-hipError_t mfx_raysort(const WfParams& P, const float lo[3], const float hi[3], int obits, int dbits, uint16_t* keys_in,
-                       uint16_t* keys_out, int32_t* vals_in, int32_t* vals_out, void* tmp, size_t tmp_bytes,
-                       hipStream_t st);
-size_t mfx_raysort_tmp_bytes(int64_t n);
+
 
 #endif

@@ -126,7 +126,6 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
 struct Scanner {
     int win_next, win_end, shard;
     bool exhausted;
-    bool in_tail;  // every shard's bulk region is taken: chunks now come from the tail regions
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
     // work are skipped with no further memory round trip. Slots of a taken chunk change only
@@ -134,49 +133,22 @@ struct Scanner {
     int b[WF_LOOKAHEAD];
     int nbuf;
     // Make [win_next, win_end) non-empty; false once every chunk has been taken. A wave takes
-    // chunks from its block's home shard while it lasts, then from the next open shard. Each shard
-    // is a bulk region taken in `chunk`-slot chunks and a tail region (its last tail_size slots)
-    // taken in tail_chunk-slot chunks once no shard has bulk left, so the launch ends on small
-    // chunks: a 1024-slot chunk of camera rays is ~1 ms of one wave's time, and the waves that
-    // took the last big chunks would otherwise run on while the others have left.
-    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size, int tail_size,
-                                           int tail_chunk, const int32_t* __restrict__ state) {
+    // chunks from its block's home shard while it lasts, then from the next open shard.
+    __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
+                                           const int32_t* __restrict__ state) {
         if (win_next < win_end) return true;
         if (exhausted) return false;
-        const int bulk = shard_size - tail_size;
         while (true) {
-            if (!in_tail) {
-                unsigned long long c = 0;
-                if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
-                c = __shfl(c, 0);
-                if ((int64_t)c < bulk) {
-                    win_next = shard * shard_size + (int)c;
-                    win_end = shard * shard_size + min((int)c + chunk, bulk);
-                    fill(state);
-                    return true;
-                }
-                const uint64_t open = open_shards(heads, bulk);
-                if (open != 0) {
-                    shard = next_open(open, shard);
-                    continue;
-                }
-                in_tail = true;
-                if (tail_size == 0) {
-                    exhausted = true;
-                    return false;
-                }
-            }
-            unsigned long long* th = heads + WF_CTL_TAIL;
             unsigned long long c = 0;
-            if (lane_id() == 0) c = atomicAdd(th + shard, (unsigned long long)tail_chunk);
+            if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
             c = __shfl(c, 0);
-            if ((int64_t)c < tail_size) {
-                win_next = shard * shard_size + bulk + (int)c;
-                win_end = shard * shard_size + bulk + min((int)c + tail_chunk, tail_size);
+            if ((int64_t)c < shard_size) {
+                win_next = shard * shard_size + (int)c;
+                win_end = shard * shard_size + min((int)c + chunk, shard_size);
                 fill(state);
                 return true;
             }
-            const uint64_t open = open_shards(th, tail_size);
+            const uint64_t open = open_shards(heads, shard_size);
             if (open == 0) {
                 exhausted = true;
                 return false;
@@ -465,9 +437,6 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
     const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
-    // the words the scan reads: state words, or a sorted slot list (MFX_RAY_SORT, iterations >= 1)
-    const bool sorted = P.order != nullptr;
-    const int32_t* __restrict__ words = sorted ? P.order : P.state;
 
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
@@ -491,30 +460,24 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 // list at least 64 slots to trace (or all that are left) from as many windows as it
                 // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.tail_size, P.tail_chunk, words)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
-                    bool take;
-                    int ent;
-                    if (sorted) {  // a listed slot (extension ray), or -1
-                        take = sj >= 0;
-                        ent = sj;
-                    } else {
-                        take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
-                        if (P.start && sj == WF_FREE && j < P.total) {
-                            int x, y;
-                            int64_t smp;
-                            // edge-tile padding starts no path (none when 8 divides the film size)
-                            take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
-                        }
-                        // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
-                        ent = sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
+                    bool take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
+                    if (P.start && sj == WF_FREE && j < P.total) {
+                        int x, y;
+                        int64_t smp;
+                        // edge-tile padding starts no path (none when 8 divides the film size)
+                        take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
                     }
                     const uint64_t tm = __ballot(take);
-                    if (take) pend[n + __popcll(tm & lanes_below())] = ent;
+                    // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
+                    if (take)
+                        pend[n + __popcll(tm & lanes_below())] =
+                            sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
                     n += __popcll(tm);
-                    sc.advance(words);
+                    sc.advance(P.state);
                 }
                 wave_lds_sync();
 #if MFX_OCTANT_SORT
@@ -633,15 +596,16 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_camera(WfParams P) {
     extern __shared__ int lds_all[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    int* stk = lds_all + wave * P.stack_size;
-    uint32_t* red = (uint32_t*)(lds_all + 4 * P.stack_size);
+    uint64_t* stm = (uint64_t*)lds_all + wave * P.stack_size;  // per wave: stack masks, then nodes
+    int* stk = (int*)((uint64_t*)lds_all + 4 * P.stack_size) + wave * P.stack_size;
+    uint32_t* red = (uint32_t*)((int*)((uint64_t*)lds_all + 4 * P.stack_size) + 4 * P.stack_size);
     const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
-    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.tail_size, P.tail_chunk, P.state)) {
+    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
         const int j = sc.win_next + lane;
         const int sj = sc.word();
         sc.advance(P.state);
@@ -665,7 +629,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_camera(WfParams P) {
             c_primary++;
         }
         Best B;
-        packet_closest<STATS>(S, act, o, d, 99999999., B, stk, st);  // Integrators.fs:108
+        packet_closest<STATS>(S, act, o, d, 99999999., B, stk, stm, st);  // Integrators.fs:108
         if (act) {
             if (B.found) {
                 const DV hp = vadd(o, vmul(d, B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
@@ -734,8 +698,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 &&
-                       sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.tail_size, P.tail_chunk, P.state)) {
+                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -1152,7 +1115,7 @@ static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t s
         hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
 }
 
-static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * sizeof(int) + 64; }
+static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64; }
 
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_camera<false>, 256,

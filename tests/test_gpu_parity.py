@@ -206,9 +206,13 @@ def test_wavefront_image_is_deterministic(gpu):
     assert np.array_equal(f1, f2)
 
 
-def test_megakernel_and_wavefront_counters_agree(gpu):
+def test_megakernel_and_wavefront_counters_agree(gpu, monkeypatch):
+    """The same per-ray traversal in both pipelines: identical ray counts and visit counters. (The
+    wavefront's camera rays run as packets by default, k_camera, whose counters add the packet's
+    union of visits; MFX_CAMERA_PACKETS=0 gives them the per-ray traversal compared here.)"""
     from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL
     from mafrixraytracing_amd.native import NativeContext
+    monkeypatch.setenv("MFX_CAMERA_PACKETS", "0")
     a = scene("spot", 96, 54)
     with NativeContext(a, seed=SEED, flags=MFX_F_COUNT_STATS) as w:
         w.sample(2)
