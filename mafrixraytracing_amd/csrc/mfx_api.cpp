@@ -143,7 +143,6 @@ struct mfx_ctx {
     bool mega_last = false;
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
-    int wf_cam_shd_grid = 0;  // > 0: their shadow rays as packets too (MFX_CAMERA_PACKETS=1: camera rays only)
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
@@ -402,13 +401,12 @@ static int ctx_setup(mfx_ctx* c) {
     }
     c->wf_ext_grid = prop.multiProcessorCount * std::max(1, std::min(ebpc, 8));
     {  // camera-ray packets (flat scenes)
-        int cam = getenv("MFX_CAMERA_PACKETS") ? atoi(getenv("MFX_CAMERA_PACKETS")) : 2;
+        int cam = getenv("MFX_CAMERA_PACKETS") ? atoi(getenv("MFX_CAMERA_PACKETS")) : 1;
         if (cam && !inst) {
-            int cb = 0, sb = 0;
-            CK(mfx_cam_occupancy(c->stack_size, &cb, &sb));
+            int cb = 0;
+            CK(mfx_cam_occupancy(c->stack_size, &cb));
             if (const char* e = getenv("MFX_CAM_BLOCKS")) cb = std::min(cb, std::max(1, atoi(e)));
             c->wf_cam_grid = prop.multiProcessorCount * std::max(1, std::min(cb, 8));
-            if (cam != 1) c->wf_cam_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sb, 8));
         }
     }
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
@@ -694,7 +692,6 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     P.cam_grid = c->wf_cam_grid;
-    P.cam_shd_grid = c->wf_cam_shd_grid;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
     while (own_events && (int)c->it_ev.size() < 3 * iters) {

@@ -961,12 +961,8 @@ __device__ __forceinline__ void cswap3(float& da, int& ca, uint64_t& ma, float& 
 // test hit the node: only they test its children, so a leaf is tested by the lanes whose ray hits
 // its box (child boxes lie inside their parent's, so a lane that missed a node misses its subtree).
 // The stack is wave-uniform: stk[] nodes and stm[] masks in LDS.
-// FAR (shadow rays): children ordered far to near by exit distance, as node_step<FAR> orders them.
-// rep: the lane whose distances order the children (the first lane of the mask).
-template <bool FAR = false>
 __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ nodes, int node, uint64_t& mask,
-                                                const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp) {
-    const int rep = __builtin_ctzll(mask);
+                                                const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp, int rep) {
     mfx_cf4* q = (mfx_cf4*)(nodes + node);
     const mfx_f4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     const mfx_i4 ch = ((mfx_ci4*)q)[6];
@@ -987,7 +983,7 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = live && n <= f;
         m[k] = __ballot(h);
-        const float kd = __shfl(h ? (FAR ? -f : n) : 3.0e38f, rep);
+        const float kd = __shfl(h ? n : 3.0e38f, rep);
         d[k] = m[k] ? kd : __builtin_inff();
         nh += m[k] ? 1 : 0;
     }
@@ -1034,11 +1030,12 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
     const RayF rf = make_rayf(o, d);
     float tlim = f_round_up(tMax);
     uint64_t mask = __ballot(act);
+    const int rep = __builtin_ctzll(mask);
     int sp = 0, node = 0;
     while (true) {
         while (node >= 0) {
             if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
-            node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp);
+            node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep);
         }
         if (node == MFX_TRAV_EXIT) return;
         if ((mask >> __lane_id()) & 1) {  // the lanes whose ray hits the leaf's box
@@ -1055,43 +1052,6 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
             return;
         }
     }
-}
-
-// Shadow queries of the wave's active lanes by packet traversal (far-first): true where occluded,
-// as traverse<SHADOW> answers. A lane leaves the walk at its first occluding candidate; the walk
-// ends when every lane has, or the stack is empty.
-template <bool STATS>
-__device__ __forceinline__ bool packet_anyhit(const SceneView& S, bool act, DV o, DV d, double tMax, int* stk,
-                                              uint64_t* stm, Stats& st) {
-    Best B = Best{tMax, -1, -1, false};
-    const RayF rf = make_rayf(o, d);
-    const float tlim = f_round_up(tMax);
-    bool occ = false;
-    uint64_t alive = __ballot(act);
-    uint64_t mask = alive;
-    int sp = 0, node = 0;
-    while (alive) {
-        while (node >= 0) {
-            if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
-            node = packet_node_step<true>(S.nodes, node, mask, rf, tlim, stk, stm, sp);
-        }
-        if (node == MFX_TRAV_EXIT) break;
-        if ((mask >> __lane_id()) & 1) {
-            if (leaf_hit<true, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st)) occ = true;
-        }
-        alive = __ballot(act && !occ);
-        if (sp == 0 || alive == 0) break;
-        // the next entry, for the lanes of its mask still looking (an empty mask: skip it)
-        do {
-            --sp;
-            node = __builtin_amdgcn_readfirstlane(stk[sp]);
-            const uint64_t mm = stm[sp];
-            mask = (((uint64_t)__builtin_amdgcn_readfirstlane((int)(mm >> 32)) << 32) |
-                    (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)mm)) & alive;
-        } while (mask == 0 && sp > 0);
-        if (mask == 0) break;
-    }
-    return occ;
 }
 
 // Bvh.Hit over the primitive BVH4 (megakernel and query kernels). SHADOW: returns occluded

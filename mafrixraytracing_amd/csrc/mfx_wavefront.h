@@ -118,7 +118,6 @@ struct WfParams {
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
     int32_t cam_grid;                     // > 0: a generation's camera rays run k_camera (packets) on this grid
-    int32_t cam_shd_grid;                 // > 0: and their shadow rays k_shadow<PACKET> on this grid
 };
 
 // 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
@@ -138,8 +137,8 @@ struct WfParams {
 // resident blocks per CU of k_extend / k_shadow with `stack_lds` stack entries per lane (spill: the
 // SpillStack instance), ntop top BVH nodes and min(ninst, WF_INST_LDS) instance records in LDS
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu);
-// resident blocks per CU of k_camera (camera-ray packets) and k_shadow<PACKET> (their shadow rays)
-hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu, int* shd_blocks_per_cu);
+// resident blocks per CU of k_camera (camera-ray packets)
+hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu);
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels (ev may be null)
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

@@ -652,48 +652,19 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_camera(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
-// The vertex's end once its shadow ray is answered: record its direct term's operands if unoccluded
-// and lightable, then continue the path (NEED_EXT with the next remaining depth) or finish it.
-__device__ __forceinline__ void finish_vertex(const WfParams& P, int s, int vflag, bool occluded, double scs,
-                                              double ssolid) {
-    const int v = (vflag >> 2) & 15;
-    int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
-    if (!occluded && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
-        double* vl = P.vls + (int64_t)(2 * v) * P.vstride + s;
-        vl[0] = scs;
-        vl[P.vstride] = ssolid;
-        mask |= 1 << v;
-    }
-    const bool cont = (vflag & 1) != 0;
-    // continue with the next vertex's remaining depth; or finished: k_resolve folds the
-    // recorded vertices (none lit: nothing to add, FREE)
-    if (cont || mask) P.depth[s] = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-    P.state[s] = cont ? (WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT)) : (mask ? WF_DONE : WF_FREE);
-}
-
-// PACKET (a generation's first iteration, flat scenes): the shadow rays of each shading batch come
-// from the hits of one or two 8x8 tiles of one sample and all head for the light, so the wave
-// traces them together (packet_anyhit) instead of handing them to the per-lane traversal; the
-// per-lane traversal, its stacks and the top nodes in LDS are compiled out.
-template <bool STATS, bool SPILL, int WAVES, bool INST, bool PACKET = false>
+template <bool STATS, bool SPILL, int WAVES, bool INST>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
-    const int ntop = PACKET ? 0 : P.ntop_shd;
-    const TopNodes tn{(const float4*)lds_all, ntop};
-    if (!PACKET) load_top_nodes((float4*)lds_all, P.nodes, ntop);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + ntop * 32);
+    const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
-    // per-lane stacks (stack_lds entries x 64 lanes per wave), or PACKET: a wave-uniform stack of
-    // stack_size nodes and 64-bit lane masks per wave in the same region
-    const int slds = PACKET ? (P.stack_size * 12 + 255) / 256 : P.stack_lds_shd;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
-    const Stack stack = make_stack<SPILL>(lds + wave * slds * 64 + lane, P, slds);
-    uint64_t* pstm = (uint64_t*)(lds + wave * slds * 64);
-    int* pstk = (int*)(pstm + P.stack_size);
-    uint8_t* pend_base = (uint8_t*)(lds + 4 * slds * 64);
+    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_shd * 64 + lane, P, P.stack_lds_shd);
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
     const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
@@ -853,27 +824,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 if (lane < rest) { shl[lane] = mv_j; shl[WF_SHD_LIST + lane] = mv_s; }
                 wave_lds_sync();
                 nshade = rest;
-                if constexpr (PACKET) {  // the batch's shadow rays, traced together, and the vertices' ends
-                    const bool act = lane < cnt;
-                    int ps = 0, pf = 0;
-                    double pcs = 0.0, pso = 0.0, ptm = 0.0;
-                    DV po = dv(0, 0, 0), pdir = dv(0, 0, 1);
-                    if (act) {
-                        ps = pd.slot[lane];
-                        pf = pd.flag[lane];
-                        pcs = pd.v[4 * 64 + lane];
-                        pso = pd.v[5 * 64 + lane];
-                        ptm = pd.v[3 * 64 + lane];
-                        po = dv(P.ox[ps], P.oy[ps], P.oz[ps]);
-                        pdir = dv(pd.v[0 * 64 + lane], pd.v[1 * 64 + lane], pd.v[2 * 64 + lane]);
-                    }
-                    const bool occ = packet_anyhit<STATS>(S, act, po, pdir, ptm, pstk, pstm, st);
-                    if (act) finish_vertex(P, ps, pf, occ, pcs, pso);
-                    pend_lo = pend_hi = 0;
-                } else {
-                    pend_lo = 0;
-                    pend_hi = cnt;
-                }
+                pend_lo = 0;
+                pend_hi = cnt;
                 DIAG_MARK(dg, shade, DG);
                 continue;
             }
@@ -898,7 +850,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             pend_lo += pm < avail ? pm : avail;
             m = __ballot(idle);
         }
-        if (PACKET || !__any(active)) break;
+        if (!__any(active)) break;
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
@@ -919,7 +871,19 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 dg_occ_leaves += st.clusters - T.l0;
             }
 #endif
-            finish_vertex(P, s, vflag, T.B.found, scs, ssolid);
+            const int v = (vflag >> 2) & 15;
+            int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
+            if (!T.B.found && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
+                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + s;
+                vl[0] = scs;
+                vl[P.vstride] = ssolid;
+                mask |= 1 << v;
+            }
+            const bool cont = (vflag & 1) != 0;
+            // continue with the next vertex's remaining depth; or finished: k_resolve folds the
+            // recorded vertices (none lit: nothing to add, FREE)
+            if (cont || mask) P.depth[s] = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
+            P.state[s] = cont ? (WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT)) : (mask ? WF_DONE : WF_FREE);
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
@@ -1152,20 +1116,10 @@ static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t s
 }
 
 static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64; }
-// k_shadow<PACKET>: the uniform stacks (in the per-lane stack region's shape), pending lists, shade lists
-static size_t shd_packet_lds_bytes(int stack_size) {
-    const int slds = (stack_size * 12 + 255) / 256;
-    return (size_t)4 * slds * 64 * sizeof(int) + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int);
-}
 
-hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu, int* shd_blocks_per_cu) {
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_camera<false>, 256,
-                                                                cam_lds_bytes(stack_size));
-    if (e != hipSuccess) return e;
-    const size_t l = shd_packet_lds_bytes(stack_size);
-    e = hipOccupancyMaxActiveBlocksPerMultiprocessor(shd_blocks_per_cu, (const void*)k_shadow<false, false, 4, false, true>,
-                                                     256, l);
-    *shd_blocks_per_cu = std::min(*shd_blocks_per_cu, wf_lds_blocks(l));
+hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_camera<false>, 256,
+                                                                      cam_lds_bytes(stack_size));
     return e;
 }
 
@@ -1185,12 +1139,6 @@ static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid
     if (ev) {  // between the two kernels (per-stage timing); null: not recorded
         const hipError_t e = hipEventRecord(ev[0], st);
         if (e != hipSuccess) return e;
-    }
-    if (!INST && P.start && P.cam_shd_grid > 0) {  // the first vertex's shadow rays as packets
-        const size_t l = shd_packet_lds_bytes(P.stack_size);
-        if (stats) hipLaunchKernelGGL((k_shadow<true, false, 4, false, true>), dim3(P.cam_shd_grid), dim3(256), l, st, P);
-        else hipLaunchKernelGGL((k_shadow<false, false, 4, false, true>), dim3(P.cam_shd_grid), dim3(256), l, st, P);
-        return hipSuccess;
     }
     const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
     if (spill && w3) launch_shadow<true, 3, INST>(P, shd_grid, stats, st, lds_s);
