@@ -389,9 +389,17 @@ def main():
         # traversal counters (separate, untimed pass at 1 spp of the same frame)
         stats = None
         if not args.no_stats:
+            # per-ray counters: the camera rays' packet walk (k_camera) would count its union of
+            # visits for every lane, so this pass traces them one ray per lane
+            old = os.environ.get("MFX_CAMERA_PACKETS")
+            os.environ["MFX_CAMERA_PACKETS"] = "0"
             with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS | mode) as sc:
                 sc.trace_accumulate(1, 10 ** 6)
                 s = sc.ray_counts()
+            if old is None:
+                del os.environ["MFX_CAMERA_PACKETS"]
+            else:
+                os.environ["MFX_CAMERA_PACKETS"] = old
             rc, rs = s[0] + s[1], s[2]
             # closest-hit traversal counters in s[4..6], shadow in s[7..9]
             stats = {"closest": {"node_visits_per_ray": s[4] / rc, "cluster_visits_per_ray": s[5] / rc,
