@@ -347,6 +347,7 @@ def main():
     t0 = time.perf_counter()
     rays = 0.0
     closest_rays = 0.0
+    primary_rays = 0.0
     timings = []
     call_s = 0.0  # --api render: host time inside the render calls (counters are read between calls)
     for k in range(args.steps):
@@ -358,12 +359,14 @@ def main():
                 c = ctx.ray_counts()
                 rays += c[0] + c[1] + c[2]
                 closest_rays += c[0] + c[1]
+                primary_rays += c[0]
                 timings.append(ctx.trace_timing())
             continue
         step(args.warmup + k)
         c = ctx.ray_counts()
         rays += c[0] + c[1] + c[2]
         closest_rays += c[0] + c[1]
+        primary_rays += c[0]
         timings.append(ctx.trace_timing())
     barrier()
     elapsed = time.perf_counter() - t0
@@ -379,7 +382,7 @@ def main():
     else:
         rays_all = rays
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
-                for k in ("total_ms", "logic_ms", "extend_ms", "shade_ms", "shadow_ms", "iterations", "launches",
+                for k in ("total_ms", "camera_ms", "extend_ms", "camera_launches", "shadow_ms", "iterations", "launches",
                           "generations")}
 
     result = None
@@ -493,15 +496,25 @@ def main():
             else:
                 # the two wavefront kernels; the roofline object is the one with the larger share of
                 # the step (the dominant kernel), the other is reported beside it
+                # the wavefront's kernels: k_camera (each generation's camera rays as packets, flat
+                # scenes), k_extend (the other closest-hit launches), k_shadow; each priced with its
+                # own rays, launches and HIP-event time
                 launches = stage_ms["launches"]
+                cl = stage_ms["camera_launches"]
                 bc = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
                 bs = fixture["shadow"]["B_ray"] if fixture else bytes_per_ray(stats["shadow"])
-                ext = kernel_roofline("k_extend<false>", stage_ms["extend_ms"], closest_rays / nt, launches, bc)
-                shd = kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"], (rays - closest_rays) / nt,
-                                      launches, bs)
-                dom, other = (shd, ext) if stage_ms["shadow_ms"] > stage_ms["extend_ms"] else (ext, shd)
-                roofline = dict(dom)
-                roofline["other_kernel"] = other
+                ks = []
+                if cl > 0:
+                    ks.append((stage_ms["camera_ms"],
+                               kernel_roofline("k_camera<false>", stage_ms["camera_ms"], primary_rays / nt, cl, bc)))
+                ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt
+                ext_ms = stage_ms["extend_ms"] - stage_ms["camera_ms"]
+                ks.append((ext_ms, kernel_roofline("k_extend<false>", ext_ms, ext_rays, launches - cl, bc)))
+                ks.append((stage_ms["shadow_ms"], kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"],
+                                                                  (rays - closest_rays) / nt, launches, bs)))
+                ks.sort(key=lambda x: -x[0])
+                roofline = dict(ks[0][1])
+                roofline["other_kernels"] = [k for _, k in ks[1:]]
                 step_bytes = (closest_rays * bc + (rays - closest_rays) * bs) / nt
                 roofline["step"] = {"achieved": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9, 2),
                                     "frac": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),

@@ -240,12 +240,13 @@ int mfx_stream(mfx_ctx* ctx, void** stream);
 int mfx_last_trace_ms(mfx_ctx* ctx, double* ms);
 
 /* Per-stage device time of the last mfx_trace_accumulate (wavefront pipeline), summed over its
- * iterations from HIP events around each kernel: out[0] = whole call, out[2] = k_extend (path
- * start + closest hit), out[4] = k_shadow (shading + shadow ray + path finish); out[1] and
- * out[3] are 0 (no separate logic / shade stages: they are fused into the two kernels), the
- * per-generation k_resolve launches make up the rest of out[0]; out[5] = iterations (max_depth + 1
- * per generation), out[6] = launches of each stage kernel (= out[5]), out[7] = generations.
- * Megakernel: out[0] = out[2] = its single launch.                                            */
+ * iterations from HIP events around each kernel: out[0] = whole call, out[2] = the closest-hit
+ * kernels (path start + closest hit: k_camera and k_extend), out[4] = k_shadow (shading + shadow
+ * ray + path finish); out[1] = the part of out[2] spent in k_camera (each generation's camera
+ * rays traced as packets, flat scenes) and out[3] = its launches (0 when k_extend traced them);
+ * the per-generation k_resolve launches make up the rest of out[0]; out[5] = iterations
+ * (max_depth + 1 per generation), out[6] = launches of each stage (= out[5]), out[7] =
+ * generations. Megakernel: out[0] = out[2] = its single launch.                               */
 int mfx_trace_timing(mfx_ctx* ctx, double out[8]);
 
 /* Ray counters of the last mfx_trace_accumulate / mfx_sample call:

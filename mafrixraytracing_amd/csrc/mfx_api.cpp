@@ -141,6 +141,7 @@ struct mfx_ctx {
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
     int generations = 0;
     bool mega_last = false;
+    bool cam_last = false;  // the last wavefront trace ran its camera rays as packets (k_camera)
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
     int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
@@ -697,7 +698,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
-    P.cam_grid = c->wf_cam_grid;
+    P.cam_grid = c->host.inst.empty() ? c->wf_cam_grid : 0;
+    if (own_events) c->cam_last = P.cam_grid > 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int iters = (int)ngen * (P.max_depth + 1);
     while (own_events && (int)c->it_ev.size() < 3 * iters) {
@@ -891,8 +893,10 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
         out[5] = 1;
         out[6] = 1;
     } else {
-        // [2] k_extend, [4] k_shadow (+ memset), summed over iterations; [1], [3] unused (no
-        // separate logic / shade stages); the resolve launches make up the rest of [0]
+        // [2] the closest-hit kernels (k_camera + k_extend), [4] k_shadow (+ memset), summed over
+        // iterations; [1] of [2] the k_camera launches (each generation's first iteration when
+        // camera rays run as packets), [3] their count; the resolve launches make up the rest of [0]
+        const int per_gen = c->host.max_depth + 1;
         for (int it = 0; it < c->it_recorded; ++it) {
             const hipEvent_t* ev = c->it_ev.data() + 3 * it;
             float fe = 0.f, fs = 0.f;
@@ -900,6 +904,10 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
             HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
             out[2] += fe;
             out[4] += fs;
+            if (c->cam_last && it % per_gen == 0) {
+                out[1] += fe;
+                out[3] += 1;
+            }
         }
         out[5] = c->it_recorded;
         out[6] = c->it_recorded;

@@ -591,8 +591,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // ray). Writes what k_extend writes for a camera ray: the hit point and HIT | FRESH | shade index,
 // or MISS | FRESH. Flat scenes only (two-level scenes take k_extend).
 // ------------------------------------------------------------------------------------------------
+#ifndef MFX_CAM_WAVES
+#define MFX_CAM_WAVES 4  // k_camera's register budget: waves per SIMD (a packet walk is one chain of scalar loads per wave)
+#endif
 template <bool STATS>
-__global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_camera(WfParams P) {
+__global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     extern __shared__ int lds_all[];
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;

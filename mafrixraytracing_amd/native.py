@@ -145,7 +145,7 @@ class NativeContext:
     def trace_timing(self) -> dict:
         out = np.zeros(8)
         check(self.lib.mfx_trace_timing(self._h, dptr(out)), "mfx_trace_timing")
-        return {"total_ms": out[0], "logic_ms": out[1], "extend_ms": out[2], "shade_ms": out[3],
+        return {"total_ms": out[0], "camera_ms": out[1], "extend_ms": out[2], "camera_launches": int(out[3]),
                 "shadow_ms": out[4], "iterations": int(out[5]), "launches": int(out[6]), "generations": int(out[7])}
 
     def closest_hit(self, rays: np.ndarray, tmin: float = 1e-6, tmax: float = 99999999.0):

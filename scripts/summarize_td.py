@@ -53,7 +53,7 @@ def main():
     for (i, k), v in per_dispatch(os.path.join(out, "bench")).items():
         name = k.replace("void ", "")
         if not (name.startswith("k_extend") or name.startswith("k_shadow") or name.startswith("k_resolve")
-                or name.startswith("trace_kernel")):
+                or name.startswith("k_camera") or name.startswith("trace_kernel")):
             continue
         for c, x in v.items():
             kern[name][c] += x
