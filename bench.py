@@ -208,12 +208,14 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
     """SURVEY §8(d)'s metric to the letter: Mrays/s over the wall time of mfx_sample(spp) — the trace,
     the mean kernel and the FP64 x-major RGBA readback (66 MB at 1080p) — per call."""
     from mafrixraytracing_amd.native import NativeContext
+    import numpy as np
+    frame = np.empty((arrays.width * arrays.height, 4))  # the Color[w,h] the integrator owns
     with NativeContext(arrays, seed=seed, flags=flags) as ctx:
-        ctx.sample(spp)  # warmup (pool allocation)
+        ctx.sample(spp, out=frame)  # warmup (pool and staging allocation, first touch of the frame)
         wall, rays = 0.0, 0.0
         for _ in range(calls):
             t0 = time.perf_counter()
-            ctx.sample(spp)
+            ctx.sample(spp, out=frame)
             wall += time.perf_counter() - t0
             c = ctx.ray_counts()
             rays += c[0] + c[1] + c[2]

@@ -68,8 +68,11 @@ class NativeContext:
         self.close()
 
     # -- reference API -------------------------------------------------------------------
-    def sample(self, spp: int) -> np.ndarray:
-        frame = np.empty((self.w * self.h, 4), dtype=np.float64)
+    def sample(self, spp: int, out: np.ndarray | None = None) -> np.ndarray:
+        """IPixelIntegrator.Sample(spp) into `out` (w*h x 4 doubles, x-major; allocated if None), as
+        the reference writes the Color[w,h] array it owns (Integrators.fs:160-172)."""
+        frame = out if out is not None else np.empty((self.w * self.h, 4), dtype=np.float64)
+        assert frame.dtype == np.float64 and frame.size == self.w * self.h * 4 and frame.flags.c_contiguous
         check(self.lib.mfx_sample(self._h, spp, dptr(frame)), "mfx_sample")
         return frame
 
