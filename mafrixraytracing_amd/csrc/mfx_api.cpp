@@ -69,6 +69,49 @@ const Rccl* rccl() {
     return ok ? &r : nullptr;
 }
 
+// ---- FP16 node copies (MFX_NODE16, mfx_layout.h) ----
+// The finite and infinite FP16 values in ascending order: index 0 is -inf, 0x7C00 is -0, 0x7C01 is
+// +0 and 2 * 0x7C00 + 1 is +inf (NaNs left out).
+static uint16_t half_bits_at(int k) { return k <= 0x7C00 ? (uint16_t)(0x8000 | (0x7C00 - k)) : (uint16_t)(k - 0x7C01); }
+static double half_value(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const double v = e == 31 ? INFINITY : (e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), e - 25));
+    return (h & 0x8000) ? -v : v;
+}
+// the largest FP16 value <= v (down) or the smallest >= v (up): the rounded box contains the FP32 one
+static uint16_t half_round(float v, bool up) {
+    int lo = 0, hi = 2 * 0x7C00 + 1;
+    if (up) {  // smallest k with value(k) >= v
+        while (lo < hi) {
+            const int mid = (lo + hi) / 2;
+            if (half_value(half_bits_at(mid)) >= (double)v) hi = mid;
+            else lo = mid + 1;
+        }
+    } else {  // largest k with value(k) <= v
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (half_value(half_bits_at(mid)) <= (double)v) lo = mid;
+            else hi = mid - 1;
+        }
+    }
+    return half_bits_at(lo);
+}
+// An empty child's planes are all +inf: with the node step's limit clamped to FLT_MAX (f_tlim) its
+// entry distance is +inf or its exit -inf on some axis, so no ray enters it.
+[[maybe_unused]] static void node_to_half(const MfxNode& n, MfxNodeH& h) {
+    for (int k = 0; k < 4; ++k) {
+        const bool empty = n.child[k] == MFX_CHILD_EMPTY;
+        const float* lo[3] = {n.lox, n.loy, n.loz};
+        const float* hi[3] = {n.hix, n.hiy, n.hiz};
+        uint16_t* dst[3] = {h.x, h.y, h.z};
+        for (int a = 0; a < 3; ++a) {
+            dst[a][k] = empty ? 0x7C00 : half_round(lo[a][k], false);
+            dst[a][4 + k] = empty ? 0x7C00 : half_round(hi[a][k], true);
+        }
+        h.child[k] = n.child[k];
+    }
+}
+
 template <typename T>
 hipError_t upload(T** dptr, const std::vector<T>& v) {
     size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
@@ -103,6 +146,7 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
+    MfxNodeH* d_nodes16 = nullptr;  // FP16 copies for the per-lane traversal (MFX_NODE16)
     MfxTri32* d_tri32 = nullptr;  // FP32 triangle copies of the slots (the leaf screen)
     MfxSlot* d_slots = nullptr;
     int32_t* d_slot_ref = nullptr;
@@ -184,6 +228,15 @@ struct mfx_ctx {
     hipEvent_t reduce_done = nullptr;    // repeated-device list: the primary has read every peer's buffer
 };
 
+// the nodes the per-lane traversal reads
+static const MfxTNode* tnodes_of(const mfx_ctx* c) {
+#if MFX_NODE16
+    return c->d_nodes16;
+#else
+    return c->d_nodes;
+#endif
+}
+
 // the devices of a context, primary first
 static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
     std::vector<mfx_ctx*> v{c};
@@ -216,7 +269,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_nodes16, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -265,6 +318,13 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
+#if MFX_NODE16
+    {
+        std::vector<MfxNodeH> h(c->host.nodes.size());
+        for (size_t i = 0; i < h.size(); ++i) node_to_half(c->host.nodes[i], h[i]);
+        CK(upload(&c->d_nodes16, h));
+    }
+#endif
     CK(upload(&c->d_slots, c->host.slots));
 #if MFX_LEAF_SCREEN32
     {  // v0, e1, e2 of every triangle slot rounded to FP32 (tri_skip32); spheres are never screened
@@ -640,6 +700,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
+    P.tnodes = tnodes_of(c);
     P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
@@ -779,6 +840,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
+    P.tnodes = tnodes_of(c);
     P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
@@ -1325,6 +1387,7 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         QueryParams Q;
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
+        Q.tnodes = tnodes_of(c);
         Q.tri32 = c->d_tri32;
         Q.slots = c->d_slots;
     Q.slot_ref = c->d_slot_ref;

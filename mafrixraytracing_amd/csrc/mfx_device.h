@@ -9,6 +9,7 @@
 
 struct TraceParams {
     const MfxNode* nodes;
+    const MfxTNode* tnodes;
     const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;
@@ -33,6 +34,7 @@ struct TraceParams {
 
 struct QueryParams {
     const MfxNode* nodes;
+    const MfxTNode* tnodes;
     const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;

@@ -33,9 +33,31 @@ struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache l
     int32_t pad[4];
 };
 #define MFX_CHILD_EMPTY (-0x7fffffff - 1)
+
+// The per-lane traversal's copy of a node (MFX_NODE16): the same four child boxes with every plane
+// rounded outward to FP16 (lo down, hi up; an empty child's planes +inf, never hit) and the same
+// children: 64 B, four 16-B loads per node step instead of seven. The slab tests read the halves
+// through v_fma_mix_f32 (FP16 operand, FP32 arithmetic), so the step costs no more VALU. The boxes
+// contain the FP32 ones, so the traversal stays conservative.
+#ifndef MFX_NODE16
+#define MFX_NODE16 0
+#endif
+struct alignas(16) MfxNodeH {
+    uint16_t x[8];  // lo[0..3], hi[0..3] of the four children along x (FP16 bits)
+    uint16_t y[8];
+    uint16_t z[8];
+    int32_t child[4];
+};
+#if MFX_NODE16
+typedef MfxNodeH MfxTNode;
+#else
+typedef MfxNode MfxTNode;
+#endif
 // nodes[0 .. MFX_TOP_NODES) are the BVH's top levels in breadth-first order (the trace kernels
 // keep a prefix of them in LDS); the rest follow in preorder
+#ifndef MFX_TOP_NODES
 #define MFX_TOP_NODES 128
+#endif
 
 // reference leaf header (ref_blob[]); copies of its primitives' slots follow
 struct alignas(16) MfxLeaf {

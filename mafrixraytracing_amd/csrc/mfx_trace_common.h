@@ -242,6 +242,7 @@ struct SceneView {
     const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
     const MfxInstance* inst_lds;           // LDS copy of instances [0, ninst_lds) (wavefront kernels)
     int ninst_lds;
+    const MfxTNode* __restrict__ tnodes;   // the per-lane traversal's nodes (FP16 copies with MFX_NODE16)
 };
 
 // An instance's record: from the kernel's LDS copy when it holds it, else from global memory
@@ -681,9 +682,15 @@ __device__ __forceinline__ float f_round_up(double x) {
     if ((double)f < x) f = nextafterf(f, __builtin_inff());
     return f;
 }
+// a node step's distance limit: x rounded up, at most FLT_MAX, so a box whose entry distance
+// overflows to +inf (an empty child's +inf planes, mfx_api.cpp node_to_half) is never entered
+__device__ __forceinline__ float f_tlim(double x) { return fminf(f_round_up(x), 3.402823466e38f); }
 
 #ifndef MFX_NEAR_FAR_PLANES
 #define MFX_NEAR_FAR_PLANES 0  // 1: node steps read each axis's near / far planes by the ray's direction signs
+#endif
+#if MFX_NEAR_FAR_PLANES && MFX_NODE16
+#error "MFX_NEAR_FAR_PLANES reads FP32 nodes: build it with MFX_NODE16=0"
 #endif
 
 // FP32 ray for the cluster-BVH slab tests
@@ -785,11 +792,13 @@ struct TopNodes {
     const float4* lds;
     int ntop;
 };
-__device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
+// With MFX_NODE16 a node is four columns: column c of node n at n * 4 + (c ^ ((n >> 1) & 3)).
+constexpr int kNodeCols = (int)(sizeof(MfxTNode) / 16);
+__device__ __forceinline__ int top_col(int n, int c) { return n * kNodeCols + (c ^ ((n >> 1) & (kNodeCols - 1))); }
 // block-wide copy at kernel start (all threads; ends with a barrier)
-__device__ __forceinline__ void load_top_nodes(float4* lds, const MfxNode* __restrict__ nodes, int ntop) {
+__device__ __forceinline__ void load_top_nodes(float4* lds, const MfxTNode* __restrict__ nodes, int ntop) {
     const float4* __restrict__ g = (const float4*)nodes;
-    for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
+    for (int i = threadIdx.x; i < ntop * kNodeCols; i += blockDim.x) lds[top_col(i / kNodeCols, i % kNodeCols)] = g[i];
     __syncthreads();
 }
 
@@ -814,7 +823,7 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
 }
 
 template <bool TOP = false, bool FAR = false, typename ST>
-__device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
+__device__ __forceinline__ int node_step(const MfxTNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
@@ -873,12 +882,32 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         nh += h ? 1 : 0;
     }
 #else
-    float4 lx, hx, ly, hy, lz, hz;
-    int4 ch;
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
     // reads land in the same registers, so the LDS reads wait for the global loads (measured
     // alternatives: LDS only when the whole wave is at top nodes, -0.5 to -2 %; both reads by every
     // lane into separate registers, global ones through out-of-range buffer offsets, -1.5 to -9 %).
+#if MFX_NODE16
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    mfx_i4 qx, qy, qz, qc;
+    if (TOP && node < tn.ntop) {
+        const int sw = (node >> 1) & 3;
+        const mfx_i4* t = (const mfx_i4*)tn.lds + node * 4;
+        qx = t[0 ^ sw]; qy = t[1 ^ sw]; qz = t[2 ^ sw]; qc = t[3 ^ sw];
+    } else {
+        const mfx_i4* __restrict__ q = (const mfx_i4*)(nodes + node);
+        qx = q[0]; qy = q[1]; qz = q[2]; qc = q[3];
+    }
+    const h8 X = __builtin_bit_cast(h8, qx), Y = __builtin_bit_cast(h8, qy), Z = __builtin_bit_cast(h8, qz);
+    const int4 ch = make_int4(qc.x, qc.y, qc.z, qc.w);
+    const float4 lx = make_float4((float)X[0], (float)X[1], (float)X[2], (float)X[3]);
+    const float4 hx = make_float4((float)X[4], (float)X[5], (float)X[6], (float)X[7]);
+    const float4 ly = make_float4((float)Y[0], (float)Y[1], (float)Y[2], (float)Y[3]);
+    const float4 hy = make_float4((float)Y[4], (float)Y[5], (float)Y[6], (float)Y[7]);
+    const float4 lz = make_float4((float)Z[0], (float)Z[1], (float)Z[2], (float)Z[3]);
+    const float4 hz = make_float4((float)Z[4], (float)Z[5], (float)Z[6], (float)Z[7]);
+#else
+    float4 lx, hx, ly, hy, lz, hz;
+    int4 ch;
     if (TOP && node < tn.ntop) {
         const int sw = (node >> 1) & 7;
         const float4* t = tn.lds + node * 8;
@@ -890,6 +919,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         lx = q[0]; hx = q[1]; ly = q[2]; hy = q[3]; lz = q[4]; hz = q[5];
         ch = *(const int4*)(q + 6);
     }
+#endif
 #ifdef MFX_DIAG_EXTRA_NODE_LOADS
     const float4* __restrict__ q = (const float4*)(nodes + node);
 #endif
@@ -1028,7 +1058,7 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
                                                int* stk, uint64_t* stm, Stats& st) {
     B = Best{tMax, -1, -1, false};
     const RayF rf = make_rayf(o, d);
-    float tlim = f_round_up(tMax);
+    float tlim = f_tlim(tMax);
     uint64_t mask = __ballot(act);
     const int rep = __builtin_ctzll(mask);
     int sp = 0, node = 0;
@@ -1040,7 +1070,7 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
         if (node == MFX_TRAV_EXIT) return;
         if ((mask >> __lane_id()) & 1) {  // the lanes whose ray hits the leaf's box
             leaf_hit<false, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st);
-            tlim = f_round_up(B.t);
+            tlim = f_tlim(B.t);
         }
         if (sp > 0) {
             --sp;
@@ -1064,7 +1094,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
                          Best& B, Stats& st) {
     B = Best{tMax, -1, -1, false};
     RayF rf = make_rayf(o, d);
-    float tlim = f_round_up(tMax);
+    float tlim = f_tlim(tMax);
     int sp = 0;
     int node = 0;
     int inst = -1, inst_sp = 0;
@@ -1073,7 +1103,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
+            node = node_step<false, SHADOW>(S.tnodes, node, rf, tlim, stk, sp);
             if (INST) node = inst_frame(S, node, inst, inst_sp, sp, o, d, rf);
         }
         if (node == MFX_TRAV_EXIT) return B.found;
@@ -1085,7 +1115,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
                 B.found = true;
                 return true;
             }
-            tlim = f_round_up(B.t);
+            tlim = f_tlim(B.t);
         }
         if (sp == 0) return B.found;
         node = stack[(--sp) * 64];

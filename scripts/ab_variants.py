@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """A/B timing of libmafrix_rt variants (build_variants/*.so) on the bench workload, each in its own
-process, interleaved over rounds (cdna_hip_programming.md §5.4 rule 24)."""
+process, interleaved over rounds (cdna_hip_programming.md §5.4 rule 24). MFX_AB_STATS=1 adds each
+variant's per-ray node / leaf / primitive visits (one MFX_F_COUNT_STATS sample)."""
 import glob
 import json
 import os
@@ -9,7 +10,7 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CHILD = r'''
-import sys, json, time
+import sys, json, time, os
 sys.path.insert(0, ROOT)
 import mafrixraytracing_amd.abi as abi
 abi.load_library(LIB); abi._lib = abi.load_library(LIB)
@@ -22,7 +23,14 @@ for k in range(STEPS + 1):
     ctx.accum_clear(); t = time.perf_counter(); ctx.trace_accumulate(SPP, k * SPP); ctx.sync(); dt = time.perf_counter() - t
     c = ctx.ray_counts(); ms = ctx.last_trace_ms(); tt = ctx.trace_timing()
     if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms, tt["total_ms"] - tt["extend_ms"] - tt["shadow_ms"]))
-print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest": [r[2] for r in res]}))
+st = {}
+if os.environ.get("MFX_AB_STATS") == "1":  # per-ray traversal work of one sample (per-lane camera rays)
+    os.environ["MFX_CAMERA_PACKETS"] = "0"
+    cs = NativeContext(a, seed=DEFAULT_SEED, flags=1)
+    cs.trace_accumulate(1, 0); cs.sync(); c = cs.ray_counts()
+    st = {"nodes/closest": c[4] / (c[0] + c[1]), "leaves/closest": c[5] / (c[0] + c[1]), "prims/closest": c[6] / (c[0] + c[1]),
+          "nodes/shadow": c[7] / max(c[2], 1), "leaves/shadow": c[8] / max(c[2], 1), "prims/shadow": c[9] / max(c[2], 1)}
+print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest": [r[2] for r in res], "stats": st}))
 '''
 
 
@@ -51,6 +59,8 @@ def main():
             out[os.path.basename(l)] += d["mrays"]
             print(os.path.basename(l), "round", r, ["%.1f" % x for x in d["mrays"]], "ms", ["%.2f" % x for x in d["ms"]],
                   "rest ms (resolve + memsets)", ["%.3f" % x for x in d.get("rest", [])], flush=True)
+            if d.get("stats"):
+                print(os.path.basename(l), "stats", {k: round(v, 3) for k, v in d["stats"].items()}, flush=True)
     print("SUMMARY", json.dumps({k: (max(v) if v else None) for k, v in out.items()}))
 
 
