@@ -171,6 +171,11 @@ int mfx_instancing_info(mfx_ctx* ctx, double out[8]);
  * description (MFX_F_FLATTEN honoured), plus the traversal stack bound.                       */
 int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
                              int32_t flags, double out[8], int32_t* stack_entries);
+/* Host-only: the per-lane traversal's BVH8 of a flat scene (mfx_wide.cpp), built from its BVH4 and
+ * checked (every leaf reached once, every box containing its subtree): out[0] = BVH8 nodes,
+ * out[1] = its stack bound, out[2] = the BVH4's, out[3] = BVH8 depth, out[4] = BVH4 depth,
+ * out[5] = the frame's scale, out[6] = mean entries per BVH8 node, out[7] = leaves.            */
+int mfx_wide_info(const mfx_scene_desc* scene, double out[8]);
 
 /* ---- the reference's render API --------------------------------------------------------- */
 

@@ -24,6 +24,7 @@
 #include "mfx_device.h"
 #include "mfx_scene.h"
 #include "mfx_wavefront.h"
+#include "mfx_wide.h"
 
 namespace {
 thread_local std::string g_err;
@@ -69,49 +70,6 @@ const Rccl* rccl() {
     return ok ? &r : nullptr;
 }
 
-// ---- FP16 node copies (MFX_NODE16, mfx_layout.h) ----
-// The finite and infinite FP16 values in ascending order: index 0 is -inf, 0x7C00 is -0, 0x7C01 is
-// +0 and 2 * 0x7C00 + 1 is +inf (NaNs left out).
-static uint16_t half_bits_at(int k) { return k <= 0x7C00 ? (uint16_t)(0x8000 | (0x7C00 - k)) : (uint16_t)(k - 0x7C01); }
-static double half_value(uint16_t h) {
-    const int e = (h >> 10) & 31, m = h & 1023;
-    const double v = e == 31 ? INFINITY : (e == 0 ? std::ldexp((double)m, -24) : std::ldexp((double)(1024 + m), e - 25));
-    return (h & 0x8000) ? -v : v;
-}
-// the largest FP16 value <= v (down) or the smallest >= v (up): the rounded box contains the FP32 one
-static uint16_t half_round(float v, bool up) {
-    int lo = 0, hi = 2 * 0x7C00 + 1;
-    if (up) {  // smallest k with value(k) >= v
-        while (lo < hi) {
-            const int mid = (lo + hi) / 2;
-            if (half_value(half_bits_at(mid)) >= (double)v) hi = mid;
-            else lo = mid + 1;
-        }
-    } else {  // largest k with value(k) <= v
-        while (lo < hi) {
-            const int mid = (lo + hi + 1) / 2;
-            if (half_value(half_bits_at(mid)) <= (double)v) lo = mid;
-            else hi = mid - 1;
-        }
-    }
-    return half_bits_at(lo);
-}
-// An empty child's planes are all +inf: with the node step's limit clamped to FLT_MAX (f_tlim) its
-// entry distance is +inf or its exit -inf on some axis, so no ray enters it.
-[[maybe_unused]] static void node_to_half(const MfxNode& n, MfxNodeH& h) {
-    for (int k = 0; k < 4; ++k) {
-        const bool empty = n.child[k] == MFX_CHILD_EMPTY;
-        const float* lo[3] = {n.lox, n.loy, n.loz};
-        const float* hi[3] = {n.hix, n.hiy, n.hiz};
-        uint16_t* dst[3] = {h.x, h.y, h.z};
-        for (int a = 0; a < 3; ++a) {
-            dst[a][k] = empty ? 0x7C00 : half_round(lo[a][k], false);
-            dst[a][4 + k] = empty ? 0x7C00 : half_round(hi[a][k], true);
-        }
-        h.child[k] = n.child[k];
-    }
-}
-
 template <typename T>
 hipError_t upload(T** dptr, const std::vector<T>& v) {
     size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
@@ -141,12 +99,16 @@ struct AheadBuf {
     bool reported = false;              // a call has reported the batch's rays and time
 };
 
+constexpr int kStageChunks = 4;  // host_readback's pipelined pieces
+
 struct mfx_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
-    MfxNodeH* d_nodes16 = nullptr;  // FP16 copies for the per-lane traversal (MFX_NODE16)
+    MfxNode8H* d_wide = nullptr;    // flat scenes: the per-lane traversal's BVH8 (MFX_WIDE, mfx_wide.cpp)
+    MfxWideXf wide_xf{0, 0, 0, 1};
+    int32_t wide_nodes = 0;
     MfxTri32* d_tri32 = nullptr;  // FP32 triangle copies of the slots (the leaf screen)
     MfxSlot* d_slots = nullptr;
     int32_t* d_slot_ref = nullptr;
@@ -213,6 +175,7 @@ struct mfx_ctx {
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
     unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
     uint8_t* h_stage = nullptr;         // page-locked staging of large readbacks (host_readback)
+    hipEvent_t stage_ev[kStageChunks] = {};  // host_readback: piece i is in h_stage
     size_t h_stage_bytes = 0;
     bool rep_valid = false;          // the last call was served from held frames: its stats are rep_*
     double rep_counts[16] = {0};
@@ -230,8 +193,8 @@ struct mfx_ctx {
 
 // the nodes the per-lane traversal reads
 static const MfxTNode* tnodes_of(const mfx_ctx* c) {
-#if MFX_NODE16
-    return c->d_nodes16;
+#if MFX_WIDE
+    return c->d_wide;  // null for two-level scenes, whose kernels read the BVH4
 #else
     return c->d_nodes;
 #endif
@@ -269,7 +232,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_nodes16, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_wide, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -277,6 +240,8 @@ static void free_ctx(mfx_ctx* c) {
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    for (hipEvent_t e : c->stage_ev)
+        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -318,11 +283,16 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
-#if MFX_NODE16
-    {
-        std::vector<MfxNodeH> h(c->host.nodes.size());
-        for (size_t i = 0; i < h.size(); ++i) node_to_half(c->host.nodes[i], h[i]);
-        CK(upload(&c->d_nodes16, h));
+#if MFX_WIDE
+    if (c->host.inst.empty()) {
+        MfxWideImage wi;
+        std::string e;
+        if (!mfx_build_wide(c->host.nodes, wi, e)) return fail(MFX_E_INVALID, "mfx_create: " + e);
+        c->stack_size = std::max(c->stack_size, wi.stack_entries);
+        if (c->stack_size > 96) return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
+        c->wide_xf = wi.xf;
+        c->wide_nodes = (int32_t)wi.nodes.size();
+        CK(upload(&c->d_wide, wi.nodes));
     }
 #endif
     CK(upload(&c->d_slots, c->host.slots));
@@ -433,7 +403,7 @@ static int ctx_setup(mfx_ctx* c) {
         (shd ? sbpc : ebpc) = blocks;
     }
     {  // top BVH nodes in LDS: as many as fit in the LDS the resident blocks leave over
-        int cap = std::min((int)c->host.nodes.size(), WF_NTOP_MAX);
+        int cap = std::min(c->host.inst.empty() && MFX_WIDE ? c->wide_nodes : (int)c->host.nodes.size(), WF_NTOP_MAX);
         if (const char* e = getenv("MFX_NTOP")) cap = std::max(0, std::min(cap, atoi(e)));
         for (int k = 0; k < 2; ++k) {
             const bool shd = k == 1;
@@ -668,6 +638,27 @@ int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* in
     return MFX_OK;
 }
 
+int mfx_wide_info(const mfx_scene_desc* scene, double out[8]) {
+    if (!scene || !out) return fail(MFX_E_INVALID, "null argument");
+    MfxHostScene h;
+    MfxWideImage w;
+    std::string err;
+    if (!mfx_build_scene(scene, h, err, false)) return fail(MFX_E_INVALID, "mfx_wide_info: " + err);
+    double mean = 0.0;
+    int64_t nl = 0;
+    if (!mfx_build_wide(h.nodes, w, err) || !mfx_check_wide(h.nodes, w, err, &mean, &nl))
+        return fail(MFX_E_INVALID, "mfx_wide_info: " + err);
+    out[0] = (double)w.nodes.size();
+    out[1] = w.stack_entries;
+    out[2] = h.stack_entries;
+    out[3] = w.depth;
+    out[4] = h.bvh_depth;
+    out[5] = w.xf.s;
+    out[6] = mean;
+    out[7] = (double)nl;
+    return MFX_OK;
+}
+
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
 // Allocate (or grow) the wavefront path-slot pool (SoA).
@@ -701,6 +692,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
     P.tnodes = tnodes_of(c);
+    P.wx = c->wide_xf;
     P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
@@ -841,6 +833,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
     P.tnodes = tnodes_of(c);
+    P.wx = c->wide_xf;
     P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
@@ -1042,18 +1035,33 @@ static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, h
         HIPCHECK(hipStreamSynchronize(st));
         return MFX_OK;
     }
-    HIPCHECK(hipMemcpyAsync(c->h_stage, src, bytes, hipMemcpyDeviceToHost, st));
-    HIPCHECK(hipStreamSynchronize(st));
-    const int nt = 4;
-    const size_t part = (bytes / nt + 4095) & ~(size_t)4095;
-    std::vector<std::thread> th;
-    for (int t = 1; t < nt; ++t) {
-        const size_t off = part * t;
+    // in kStageChunks pieces: the host threads copy piece i while the DMA engine brings piece i + 1
+    for (hipEvent_t& e : c->stage_ev)
+        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    const size_t piece = (bytes / kStageChunks + 4095) & ~(size_t)4095;
+    for (int i = 0; i < kStageChunks; ++i) {
+        const size_t off = piece * i;
         if (off >= bytes) break;
-        th.emplace_back([=] { std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, bytes - off)); });
+        HIPCHECK(hipMemcpyAsync(c->h_stage + off, (const uint8_t*)src + off, std::min(piece, bytes - off),
+                                hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipEventRecord(c->stage_ev[i], st));
     }
-    std::memcpy(dst, c->h_stage, std::min(part, bytes));
-    for (auto& t : th) t.join();
+    const int nt = 4;
+    for (int i = 0; i < kStageChunks; ++i) {
+        const size_t off0 = piece * i;
+        if (off0 >= bytes) break;
+        HIPCHECK(hipEventSynchronize(c->stage_ev[i]));
+        const size_t len = std::min(piece, bytes - off0);
+        const size_t part = (len / nt + 4095) & ~(size_t)4095;
+        std::vector<std::thread> th;
+        for (int t = 1; t < nt; ++t) {
+            const size_t off = off0 + part * t;
+            if (part * t >= len) break;
+            th.emplace_back([=] { std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, len - part * t)); });
+        }
+        std::memcpy((uint8_t*)dst + off0, c->h_stage + off0, std::min(part, len));
+        for (auto& t : th) t.join();
+    }
     return MFX_OK;
 }
 
@@ -1388,6 +1396,7 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
         Q.tnodes = tnodes_of(c);
+        Q.wx = c->wide_xf;
         Q.tri32 = c->d_tri32;
         Q.slots = c->d_slots;
     Q.slot_ref = c->d_slot_ref;

@@ -9,7 +9,8 @@
 
 struct TraceParams {
     const MfxNode* nodes;
-    const MfxTNode* tnodes;
+    const MfxTNode* tnodes;  // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
+    MfxWideXf wx;            // their frame
     const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;
@@ -34,7 +35,8 @@ struct TraceParams {
 
 struct QueryParams {
     const MfxNode* nodes;
-    const MfxTNode* tnodes;
+    const MfxTNode* tnodes;  // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
+    MfxWideXf wx;            // their frame
     const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;

@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes, P.wx};
     const MfxLight& LT = P.light;
     const MfxCamera& CAM = P.cam;
     const int W = P.width, H = P.height;
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes};
+    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes, Q.wx};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes};
+    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes, Q.wx};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};

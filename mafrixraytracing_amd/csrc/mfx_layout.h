@@ -34,22 +34,32 @@ struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache l
 };
 #define MFX_CHILD_EMPTY (-0x7fffffff - 1)
 
-// The per-lane traversal's copy of a node (MFX_NODE16): the same four child boxes with every plane
-// rounded outward to FP16 (lo down, hi up; an empty child's planes +inf, never hit) and the same
-// children: 64 B, four 16-B loads per node step instead of seven. The slab tests read the halves
-// through v_fma_mix_f32 (FP16 operand, FP32 arithmetic), so the step costs no more VALU. The boxes
-// contain the FP32 ones, so the traversal stays conservative.
-#ifndef MFX_NODE16
-#define MFX_NODE16 0
+// The per-lane traversal's BVH8 (MFX_WIDE; flat scenes): each node is a BVH4 node with its
+// children's children pulled up, the largest boxes first, while at most 8 entries result
+// (mfx_wide.cpp). A node is one 128-B line: the 8 child boxes with every plane stored as FP16 of
+// (plane - center) * scale, rounded outward (lo down, hi up; an empty entry's planes +inf, never
+// entered), and the 8 children (BVH4 codes: leaves keep their leaf codes). The rays are moved into
+// the same frame (o' = (o - center) * scale, d' = d * scale with a power-of-2 scale), which leaves
+// every slab distance t unchanged, and the boxes contain the FP32 ones, so the search stays
+// conservative. A wave's node loop takes fewer rounds (C2: 4.5 BVH4 steps per
+// closest ray) for the same one line per lane per step.
+#ifndef MFX_WIDE
+#define MFX_WIDE 0  // measured slower (r03n-r03q: node visits -23 to -30 %, frames -5 to -7 %): DESIGN.md §9
 #endif
-struct alignas(16) MfxNodeH {
-    uint16_t x[8];  // lo[0..3], hi[0..3] of the four children along x (FP16 bits)
-    uint16_t y[8];
-    uint16_t z[8];
-    int32_t child[4];
+#ifndef MFX_WIDE_SORT
+#define MFX_WIDE_SORT 1  // 0: the BVH8 step takes the nearest hit and pushes the others unsorted
+#endif
+struct alignas(16) MfxNode8H {
+    uint16_t lox[8], hix[8], loy[8], hiy[8], loz[8], hiz[8];  // FP16 bits
+    int32_t child[8];  // as MfxNode::child
 };
-#if MFX_NODE16
-typedef MfxNodeH MfxTNode;
+static_assert(sizeof(MfxNode8H) == 128, "one line per wide node");
+// the BVH8 frame: o' = (o - c) * s (MfxNode8H)
+struct MfxWideXf {
+    double cx, cy, cz, s;
+};
+#if MFX_WIDE
+typedef MfxNode8H MfxTNode;
 #else
 typedef MfxNode MfxTNode;
 #endif

@@ -242,7 +242,8 @@ struct SceneView {
     const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
     const MfxInstance* inst_lds;           // LDS copy of instances [0, ninst_lds) (wavefront kernels)
     int ninst_lds;
-    const MfxTNode* __restrict__ tnodes;   // the per-lane traversal's nodes (FP16 copies with MFX_NODE16)
+    const MfxTNode* __restrict__ tnodes;   // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
+    MfxWideXf wx;                          // and their frame (MfxNode8H)
 };
 
 // An instance's record: from the kernel's LDS copy when it holds it, else from global memory
@@ -689,8 +690,8 @@ __device__ __forceinline__ float f_tlim(double x) { return fminf(f_round_up(x), 
 #ifndef MFX_NEAR_FAR_PLANES
 #define MFX_NEAR_FAR_PLANES 0  // 1: node steps read each axis's near / far planes by the ray's direction signs
 #endif
-#if MFX_NEAR_FAR_PLANES && MFX_NODE16
-#error "MFX_NEAR_FAR_PLANES reads FP32 nodes: build it with MFX_NODE16=0"
+#if MFX_NEAR_FAR_PLANES && MFX_WIDE
+#error "MFX_NEAR_FAR_PLANES reads BVH4 FP32 nodes: build it with MFX_WIDE=0"
 #endif
 
 // FP32 ray for the cluster-BVH slab tests
@@ -719,6 +720,16 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
     r.pz = 64u | ((__float_as_uint(r.iz) >> 31) << 4);
 #endif
     return r;
+}
+// the FP32 search ray of a flat scene's per-lane traversal: in the BVH8's frame (MfxNode8H: o' =
+// (o - c) * s, d' = d * s, s a power of 2, so every slab distance is the world one)
+__device__ __forceinline__ RayF make_rayf_t(const SceneView& S, DV o, DV d) {
+#if MFX_WIDE
+    const double s = S.wx.s;
+    return make_rayf(dv((o.x - S.wx.cx) * s, (o.y - S.wx.cy) * s, (o.z - S.wx.cz) * s), dv(d.x * s, d.y * s, d.z * s));
+#else
+    return make_rayf(o, d);
+#endif
 }
 // the same ray from another origin (an instance frame's o - off, or back to the world's o): the
 // direction terms are the ray's own, so only the origin products are recomputed, with make_rayf's
@@ -792,13 +803,13 @@ struct TopNodes {
     const float4* lds;
     int ntop;
 };
-// With MFX_NODE16 a node is four columns: column c of node n at n * 4 + (c ^ ((n >> 1) & 3)).
-constexpr int kNodeCols = (int)(sizeof(MfxTNode) / 16);
-__device__ __forceinline__ int top_col(int n, int c) { return n * kNodeCols + (c ^ ((n >> 1) & (kNodeCols - 1))); }
-// block-wide copy at kernel start (all threads; ends with a barrier)
-__device__ __forceinline__ void load_top_nodes(float4* lds, const MfxTNode* __restrict__ nodes, int ntop) {
+__device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
+// block-wide copy at kernel start (all threads; ends with a barrier); BVH4 (MfxNode) and BVH8
+// (MfxNode8H) nodes are both eight 16-B columns
+static_assert(sizeof(MfxNode) == 128 && sizeof(MfxNode8H) == 128, "top nodes are 8 columns");
+__device__ __forceinline__ void load_top_nodes(float4* lds, const void* __restrict__ nodes, int ntop) {
     const float4* __restrict__ g = (const float4*)nodes;
-    for (int i = threadIdx.x; i < ntop * kNodeCols; i += blockDim.x) lds[top_col(i / kNodeCols, i % kNodeCols)] = g[i];
+    for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
     __syncthreads();
 }
 
@@ -823,7 +834,7 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
 }
 
 template <bool TOP = false, bool FAR = false, typename ST>
-__device__ __forceinline__ int node_step(const MfxTNode* __restrict__ nodes, int node, const RayF& r, float tlim,
+__device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
@@ -886,26 +897,6 @@ __device__ __forceinline__ int node_step(const MfxTNode* __restrict__ nodes, int
     // reads land in the same registers, so the LDS reads wait for the global loads (measured
     // alternatives: LDS only when the whole wave is at top nodes, -0.5 to -2 %; both reads by every
     // lane into separate registers, global ones through out-of-range buffer offsets, -1.5 to -9 %).
-#if MFX_NODE16
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    mfx_i4 qx, qy, qz, qc;
-    if (TOP && node < tn.ntop) {
-        const int sw = (node >> 1) & 3;
-        const mfx_i4* t = (const mfx_i4*)tn.lds + node * 4;
-        qx = t[0 ^ sw]; qy = t[1 ^ sw]; qz = t[2 ^ sw]; qc = t[3 ^ sw];
-    } else {
-        const mfx_i4* __restrict__ q = (const mfx_i4*)(nodes + node);
-        qx = q[0]; qy = q[1]; qz = q[2]; qc = q[3];
-    }
-    const h8 X = __builtin_bit_cast(h8, qx), Y = __builtin_bit_cast(h8, qy), Z = __builtin_bit_cast(h8, qz);
-    const int4 ch = make_int4(qc.x, qc.y, qc.z, qc.w);
-    const float4 lx = make_float4((float)X[0], (float)X[1], (float)X[2], (float)X[3]);
-    const float4 hx = make_float4((float)X[4], (float)X[5], (float)X[6], (float)X[7]);
-    const float4 ly = make_float4((float)Y[0], (float)Y[1], (float)Y[2], (float)Y[3]);
-    const float4 hy = make_float4((float)Y[4], (float)Y[5], (float)Y[6], (float)Y[7]);
-    const float4 lz = make_float4((float)Z[0], (float)Z[1], (float)Z[2], (float)Z[3]);
-    const float4 hz = make_float4((float)Z[4], (float)Z[5], (float)Z[6], (float)Z[7]);
-#else
     float4 lx, hx, ly, hy, lz, hz;
     int4 ch;
     if (TOP && node < tn.ntop) {
@@ -919,7 +910,6 @@ __device__ __forceinline__ int node_step(const MfxTNode* __restrict__ nodes, int
         lx = q[0]; hx = q[1]; ly = q[2]; hy = q[3]; lz = q[4]; hz = q[5];
         ch = *(const int4*)(q + 6);
     }
-#endif
 #ifdef MFX_DIAG_EXTRA_NODE_LOADS
     const float4* __restrict__ q = (const float4*)(nodes + node);
 #endif
@@ -959,6 +949,79 @@ __device__ __forceinline__ int node_step(const MfxTNode* __restrict__ nodes, int
     if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]), dp);
     if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1], dp);
     if (nh >= 4) stack.put(sp + 2, c[1], dp);
+    const bool pop = nh == 0 && sp > 0;
+    const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
+    sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
+    return next;
+}
+
+// One node step of the BVH8 (MfxNode8H): the same contract as the BVH4 step above, eight children
+// from one line: six 16-B columns of FP16 planes (read through v_fma_mix_f32) and two of
+// children; the hits sorted near to far by a 19-comparator network (misses last at +inf), the
+// nearest taken and the others pushed far-first (up to 7).
+template <bool TOP = false, bool FAR = false, typename ST>
+__device__ __forceinline__ int node_step(const MfxNode8H* __restrict__ nodes, int node, const RayF& r, float tlim,
+                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
+    const bool dp = stack.deep(sp + 7);  // this step reads sp - 1 and may write sp .. sp + 6
+    const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
+    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+    mfx_i4 q[8];
+    if (TOP && node < tn.ntop) {
+        const int sw = (node >> 1) & 7;
+        const mfx_i4* t = (const mfx_i4*)tn.lds + node * 8;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = t[k ^ sw];
+    } else {
+        const mfx_i4* __restrict__ g = (const mfx_i4*)(nodes + node);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) q[k] = g[k];
+    }
+    const h8 LX = __builtin_bit_cast(h8, q[0]), HX = __builtin_bit_cast(h8, q[1]);
+    const h8 LY = __builtin_bit_cast(h8, q[2]), HY = __builtin_bit_cast(h8, q[3]);
+    const h8 LZ = __builtin_bit_cast(h8, q[4]), HZ = __builtin_bit_cast(h8, q[5]);
+    float d[8];
+    int c[8] = {q[6].x, q[6].y, q[6].z, q[6].w, q[7].x, q[7].y, q[7].z, q[7].w};
+    int nh = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float a0 = fmaf((float)LX[k], r.ix, -r.oix), a1 = fmaf((float)HX[k], r.ix, -r.oix);
+        const float b0 = fmaf((float)LY[k], r.iy, -r.oiy), b1 = fmaf((float)HY[k], r.iy, -r.oiy);
+        const float c0 = fmaf((float)LZ[k], r.iz, -r.oiz), c1 = fmaf((float)HZ[k], r.iz, -r.oiz);
+        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+        const bool h = n <= f;
+        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
+        nh += h ? 1 : 0;
+    }
+#if MFX_WIDE_SORT
+    // optimal 8-input network (19 comparators, depth 6)
+    cswap(d[0], c[0], d[2], c[2]); cswap(d[1], c[1], d[3], c[3]); cswap(d[4], c[4], d[6], c[6]); cswap(d[5], c[5], d[7], c[7]);
+    cswap(d[0], c[0], d[4], c[4]); cswap(d[1], c[1], d[5], c[5]); cswap(d[2], c[2], d[6], c[6]); cswap(d[3], c[3], d[7], c[7]);
+    cswap(d[0], c[0], d[1], c[1]); cswap(d[2], c[2], d[3], c[3]); cswap(d[4], c[4], d[5], c[5]); cswap(d[6], c[6], d[7], c[7]);
+    cswap(d[2], c[2], d[4], c[4]); cswap(d[3], c[3], d[5], c[5]);
+    cswap(d[1], c[1], d[4], c[4]); cswap(d[3], c[3], d[6], c[6]);
+    cswap(d[1], c[1], d[2], c[2]); cswap(d[3], c[3], d[4], c[4]); cswap(d[5], c[5], d[6], c[6]);
+    // far-first pushes: stack[sp + nh - 1 - k] = c[k] for 1 <= k < nh (exec-masked stores)
+#pragma unroll
+    for (int k = 1; k < 8; ++k)
+        if (k < nh) stack.put(sp + nh - 1 - k, c[k], dp);
+#else
+    // the nearest hit child is taken next; the other hits are pushed in child order (no sort)
+    float dm = d[0];
+    int cm = c[0], km = 0;
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+        const bool s = d[k] < dm;
+        dm = s ? d[k] : dm;
+        cm = s ? c[k] : cm;
+        km = s ? k : km;
+    }
+    int at = sp;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        if (d[k] != __builtin_inff() && k != km) stack.put(at++, c[k], dp);
+    c[0] = cm;
+#endif
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
@@ -1093,7 +1156,7 @@ template <bool SHADOW, bool STATS, bool INST = false>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
                          Best& B, Stats& st) {
     B = Best{tMax, -1, -1, false};
-    RayF rf = make_rayf(o, d);
+    RayF rf = INST ? make_rayf(o, d) : make_rayf_t(S, o, d);
     float tlim = f_tlim(tMax);
     int sp = 0;
     int node = 0;
@@ -1103,7 +1166,8 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            node = node_step<false, SHADOW>(S.tnodes, node, rf, tlim, stk, sp);
+            if constexpr (INST) node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
+            else node = node_step<false, SHADOW>(S.tnodes, node, rf, tlim, stk, sp);
             if (INST) node = inst_frame(S, node, inst, inst_sp, sp, o, d, rf);
         }
         if (node == MFX_TRAV_EXIT) return B.found;

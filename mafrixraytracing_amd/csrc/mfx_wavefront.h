@@ -73,7 +73,8 @@ typedef int32_t WfMat;
 struct WfParams {
     // scene
     const MfxNode* nodes;
-    const MfxTNode* tnodes; // the per-lane traversal's nodes (FP16 copies with MFX_NODE16; == nodes otherwise)
+    const MfxTNode* tnodes; // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8; else == nodes)
+    MfxWideXf wx;           // their frame (MfxNode8H)
     const MfxTri32* tri32;  // FP32 triangle copies per slot (MFX_LEAF_SCREEN32)
     const MfxSlot* slots;
     const int32_t* slot_ref;

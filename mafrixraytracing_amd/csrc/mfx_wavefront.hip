@@ -214,6 +214,15 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.pbase = 0;
 }
 
+// one node step of the per-lane traversal: the BVH4 in two-level scenes, else the flat scene's
+// traversal image (MfxTNode)
+template <bool SHADOW, bool INST, typename ST>
+__device__ __forceinline__ int trav_node_step(const SceneView& S, int node, const RayF& rf, float tlim, const ST& stack,
+                                              int& sp, TopNodes tn) {
+    if constexpr (INST) return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
+    else return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.tnodes, node, rf, tlim, stack, sp, tn);
+}
+
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
@@ -226,7 +235,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
     // the FP32 ray and the node-test limit are recomputed each round (the same values) rather than
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
-    rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
+    rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf_t(S, T.o, T.d);
     const float tlim = f_tlim(T.B.t);  // the query's tMax until the first hit, then the best t
 #if MFX_SPECULATIVE
     // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps
@@ -238,7 +247,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (T.node >= 0) {
             if (STATS) st.nodes++;
             if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;
-            T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.tnodes, T.node, rf, tlim, stack, T.sp, tn);
+            T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
             if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         }
         if (T.node < 0 && T.node != MFX_TRAV_EXIT && T.pleaf < 0) {  // postpone the leaf, pop the next entry
@@ -271,7 +280,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (STATS && !SHADOW && T.B.found) st.after_nodes++;
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.tnodes, T.node, rf, tlim, stack, T.sp, tn);
+        T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
         if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
@@ -425,8 +434,8 @@ template <bool STATS, bool SPILL, bool INST>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
-    load_top_nodes((float4*)lds_all, P.tnodes, P.ntop_ext);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * (int)(sizeof(MfxTNode) / 4));
+    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_ext);
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
@@ -435,7 +444,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
     int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes, P.wx};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -602,7 +611,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     uint64_t* stm = (uint64_t*)lds_all + wave * P.stack_size;  // per wave: stack masks, then nodes
     int* stk = (int*)((uint64_t*)lds_all + 4 * P.stack_size) + wave * P.stack_size;
     uint32_t* red = (uint32_t*)((int*)((uint64_t*)lds_all + 4 * P.stack_size) + 4 * P.stack_size);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes, P.wx};
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
@@ -659,8 +668,8 @@ template <bool STATS, bool SPILL, int WAVES, bool INST>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
-    load_top_nodes((float4*)lds_all, P.tnodes, P.ntop_shd);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * (int)(sizeof(MfxTNode) / 4));
+    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_shd);
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
@@ -670,7 +679,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes};
+    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes, P.wx};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -1073,7 +1082,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // top nodes, stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
 static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst) {
-    const size_t stacks = (size_t)ntop * sizeof(MfxTNode) + (size_t)ninst * sizeof(MfxInstance) +
+    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) +
                           (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
