@@ -298,7 +298,7 @@ def main():
 
     import numpy as np
     from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE
-    from mafrixraytracing_amd.distributed import native_partitioned_render, step_spp
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender, step_spp
     from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
@@ -319,11 +319,14 @@ def main():
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
     pr = None
     if use_dist:
-        acc = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}")
-        pr = native_partitioned_render(ctx, acc, rank, world)
+        # two attached accumulators: frame k's RCCL reduce runs while frame k + 1 traces
+        accs = [torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}") for _ in range(2)]
+        pr = PipelinedNativeRender(ctx, accs, rank, world)
     rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
+        if pr is not None:
+            pr.drain()  # every frame's reduce has finished
         if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
@@ -544,13 +547,15 @@ def main():
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
         if ngpu == 1 and use_dist:
-            par = "one GPU through the one-process-per-GPU path (process group, attached accumulator, reduce)"
+            par = ("one GPU through the one-process-per-GPU path (process group, attached accumulators, reduce "
+                   "overlapped with the next frame's trace)")
         elif ngpu == 1:
             par = "one GPU"
         elif args.single_process:
             par = f"sample-partition x{ngpu}, one process, library RCCL reduce (mfx_options.devices)"
         else:
-            par = f"sample-partition x{ngpu}, one process per GPU, RCCL reduce via torch.distributed"
+            par = (f"sample-partition x{ngpu}, one process per GPU, RCCL reduce via torch.distributed "
+                   "(frame k's reduce overlapped with frame k+1's trace)")
         per_gpu = spp_step / ngpu
         api = ("Scene.Render pattern: mfx_render_rgba8(ctx, 1, buf) x spp, readback included"
                if args.api == "render" else "mfx_trace_accumulate of the step's spp (inputs resident in HBM)")

@@ -107,3 +107,67 @@ def native_partitioned_render(ctx, acc, rank: int, world: int) -> PartitionedRen
 
     return PartitionedRender(render_fn=render, acc=acc, rank=rank, world=world,
                              clear_fn=ctx.accum_clear, sync_fn=ctx.sync, after_reduce=sync_torch)
+
+
+class PipelinedNativeRender:
+    """Frames over two attached accumulators, so a frame's reduce overlaps the next frame's trace:
+    frame k traces into accs[k % 2] on the context's HIP stream; torch's stream waits for that trace
+    (an event on the context stream, no host sync) and runs the reduce; frame k + 2 reuses the
+    buffer only after that reduce has finished (an event on torch's stream, waited on the host just
+    before the buffer is cleared, while the GPU is still tracing frame k + 1). Each frame is the
+    same clear / trace / reduce as PartitionedRender.frame; only the waits move. drain() waits for
+    every outstanding reduce; `buffer(k)` is where frame k's reduced accumulator lands."""
+
+    def __init__(self, ctx, accs, rank: int, world: int):
+        import torch
+        self.ctx = ctx
+        self.accs = list(accs)
+        assert len(self.accs) == 2 and all(a.is_cuda for a in self.accs)
+        self.rank, self.world = rank, world
+        self.multi = len(getattr(ctx, "devices", [0])) > 1
+        self.device = self.accs[0].device
+        self.ctx_stream = torch.cuda.ExternalStream(ctx.stream(), device=self.device)
+        self.pending = [None, None]
+        self.k = 0
+
+    def buffer(self, k: int):
+        return self.accs[k % 2]
+
+    def _wait(self, i: int):
+        if self.pending[i] is not None:
+            self.pending[i].synchronize()
+            self.pending[i] = None
+
+    def frame(self, spp: int, sample_base: int, all_ranks: bool = False):
+        import torch
+        import torch.distributed as dist
+        i = self.k % 2
+        self.k += 1
+        acc = self.accs[i]
+        self._wait(i)  # frame k - 2's reduce has read this buffer
+        self.ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
+        self.ctx.accum_clear()
+        self.ctx.trace_accumulate(spp, sample_base)
+        if self.multi:
+            self.ctx.accum_reduce()
+        traced = torch.cuda.Event()
+        traced.record(self.ctx_stream)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_event(traced)
+        if dist.is_available() and dist.is_initialized():
+            work = (dist.all_reduce(acc, op=dist.ReduceOp.SUM, async_op=True) if all_ranks
+                    else dist.reduce(acc, dst=0, op=dist.ReduceOp.SUM, async_op=True))
+            work.wait()  # the current stream waits for the collective's stream (no host wait)
+        done = torch.cuda.Event()
+        done.record(cur)
+        self.pending[i] = done
+        return acc
+
+    def drain(self):
+        for i in (0, 1):
+            self._wait(i)
+        self.ctx.sync()
+
+    def close(self):
+        self.drain()
+        self.ctx.accum_attach(None)

@@ -51,14 +51,14 @@ def _plain_accumulators(name, frames, part_index=0, part_count=1):
     return out
 
 
-def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks):
+def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
     import torch.distributed as dist
 
     from conftest import scene
-    from mafrixraytracing_amd.distributed import native_partitioned_render
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender, native_partitioned_render
     from mafrixraytracing_amd.native import NativeContext
 
     torch.cuda.set_device(0)
@@ -66,21 +66,31 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks):
     a = scene(name, W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
     with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world) as ctx:
-        pr = native_partitioned_render(ctx, acc, rank, world)
         got = []
-        for spp, base in frames:
-            pr.frame(spp, base, all_ranks=all_ranks)
-            got.append(acc.cpu().numpy().copy())
-        ctx.accum_attach(None)
+        if pipelined:  # back to back, no waits between frames; the last two buffers checked after drain
+            acc1 = torch.zeros_like(acc)
+            pr = PipelinedNativeRender(ctx, [acc, acc1], rank, world)
+            for spp, base in frames:
+                pr.frame(spp, base, all_ranks=all_ranks)
+            pr.drain()
+            got = [pr.buffer(k).cpu().numpy().copy() for k in range(len(frames) - 2, len(frames))]
+            pr.close()
+        else:
+            pr = native_partitioned_render(ctx, acc, rank, world)
+            for spp, base in frames:
+                pr.frame(spp, base, all_ranks=all_ranks)
+                got.append(acc.cpu().numpy().copy())
+            ctx.accum_attach(None)
     if rank == 0:
         np.save(os.path.join(outdir, "frames.npy"), np.stack(got))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, name, frames, outdir, all_ranks):
+def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False):
     import torch.multiprocessing as mp
-    mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks),
+    mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks,
+                                           pipelined),
                        nprocs=world, join=True, start_method="spawn")
     return np.load(os.path.join(outdir, "frames.npy"))
 
@@ -95,6 +105,29 @@ def test_world1_nccl_sequence_bit_identical(gpu, tmp_path):
     want = _plain_accumulators("spot", FRAMES)
     for k in range(len(FRAMES)):
         assert np.array_equal(got[k], want[k]), k
+
+
+def test_world1_nccl_pipelined_frames_bit_identical(gpu, tmp_path):
+    """The bench's pipelined form (PipelinedNativeRender: two attached accumulators, frame k's
+    reduce on torch's stream overlapping frame k + 1's trace): frames run back to back with no host
+    wait between them, and the last two buffers — each reused once — hold exactly the plain
+    context's accumulators of their frames."""
+    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False, pipelined=True)
+    want = _plain_accumulators("spot", FRAMES)
+    for k in range(2):
+        assert np.array_equal(got[k], want[len(FRAMES) - 2 + k]), k
+
+
+def test_two_ranks_pipelined_gloo_allreduce(gpu, tmp_path):
+    """Two ranks sharing device 0, pipelined frames, gloo all_reduce: the last two frames' buffers are
+    the sums of the two partitioned contexts' accumulators."""
+    frames = [(2, 0), (3, 2), (1, 5), (2, 6)]
+    got = _spawn(2, "gloo", "cube_cornell", frames, tmp_path, True, pipelined=True)
+    p0 = _plain_accumulators("cube_cornell", frames, 0, 2)
+    p1 = _plain_accumulators("cube_cornell", frames, 1, 2)
+    for k in range(2):
+        j = len(frames) - 2 + k
+        assert np.array_equal(got[k], p0[j] + p1[j]), k
 
 
 def test_two_ranks_on_one_device_gloo_allreduce(gpu, oracle, tmp_path):
