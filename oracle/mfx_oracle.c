@@ -706,6 +706,18 @@ static V3 random_in_hemisphere_ball(V3 nm, Rng* rng) {
     return p;
 }
 
+/* The same distribution drawn directly (statistical check only): the rejection
+ * sampler above keeps a point uniform in the unit ball with n.p > 0, whose direction is uniform on
+ * the hemisphere around n; so is (cos t = u1, phi = 2 pi u2) around an orthonormal frame of n. Two
+ * draws instead of ~11.5; a different sample sequence with the same expectation. */
+static V3 direct_hemisphere_dir(V3 nm, Rng* rng) {
+    const double z = rng_next(rng), phi = TWOPI * rng_next(rng);
+    const double r = sqrt(fmax(0.0, 1.0 - z * z));
+    const V3 a = fabs(nm.x) > 0.9 ? v3(0, 1, 0) : v3(1, 0, 0);
+    const V3 t = vnormalize(vcross(a, nm)), b = vcross(nm, t);
+    return vadd(vadd(vmul(t, r * cos(phi)), vmul(b, r * sin(phi))), vmul(nm, z));
+}
+
 /* NewAreaLight.Sample_Li / GetDirection / L — Light.fs:42-59; Rect.SamplePoint Rect.fs:33-38 */
 static V3 light_sample_point(const OScene* s, Rng* rng) {
     double sel = rng_next(rng);
@@ -731,13 +743,16 @@ static HitRecord scene_hit(const OScene* s, int fast, int shadow, V3 o, V3 d, do
     return bvh_hit(&s->bvh, o, d, tMin, tMax, st);
 }
 
-static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts* rc, int fast) {
+/* mode bit 0: fast traversal; bit 1: the direct hemisphere sampler (statistical check only) */
+static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts* rc, int mode) {
+    const int fast = mode & 1;
     if (depth < 0) return c3(0, 0, 0); /* the discarded depth -1 query (:108-109) is skipped */
     HitRecord hit = scene_hit(s, fast, 0, o, d, 1e-6, 99999999., rc ? &rc->trav : NULL);
     if (hit.hit && depth >= 0) {
         /* bxdf.SampleF — Material.fs:33-36 */
         C3 a = s->albedo[hit.material];
-        V3 wi = vnormalize(random_in_hemisphere_ball(hit.normal, rng));
+        V3 wi = (mode & 2) ? direct_hemisphere_dir(vnormalize(hit.normal), rng)
+                           : vnormalize(random_in_hemisphere_ball(hit.normal, rng));
         double ei = vdot(hit.normal, wi);
         C3 col = cscale(TWOPI, cscale(ei, cscale(INVPI, a)));
         double pdf = 1.;
@@ -754,21 +769,21 @@ static C3 trace_ray(const OScene* s, V3 o, V3 d, int depth, Rng* rng, RayCounts*
         else l = cscale(vdot(unitToLight, hit.normal), light_L(s, toLight));
         /* (l / pdf_li + TraceRay(Ray(hit.point, wi), depth - 1)) * col / pdf   (:135-136) */
         if (rc && depth - 1 >= 0) rc->extension++;
-        C3 ind = trace_ray(s, hit.point, wi, depth - 1, rng, rc, fast);
+        C3 ind = trace_ray(s, hit.point, wi, depth - 1, rng, rc, mode);
         return cdivf(cmul(cadd(cdivf(l, pdf_li), ind), col), pdf);
     }
     return c3(0, 0, 0);
 }
 
 /* One path's radiance for (pixel column i, row j, global sample) — Integrators.fs:166-170 */
-static C3 render_path(const OScene* s, uint64_t seed, int i, int j, int64_t sample, RayCounts* rc, int fast) {
+static C3 render_path(const OScene* s, uint64_t seed, int i, int j, int64_t sample, RayCounts* rc, int mode) {
     Rng rng = rng_path(seed, (uint64_t)i * (uint64_t)s->height + (uint64_t)j, (uint64_t)sample);
     double u = ((double)i + rng_next(&rng)) / (double)s->width;
     double v = ((double)j + rng_next(&rng)) / (double)s->height;
     V3 o, d;
     pinhole_get_ray(&s->cam, u, v, &o, &d);
     if (rc) { rc->primary++; rc->paths++; }
-    return trace_ray(s, o, d, s->max_depth, &rng, rc, fast);
+    return trace_ray(s, o, d, s->max_depth, &rng, rc, mode);
 }
 
 /* PixelIntegrator.Sample(n) — Integrators.fs:161-172. frame is Color[w,h] x-major RGBA.
@@ -813,7 +828,8 @@ int oracle_sample(const OScene* s, uint64_t seed, int32_t spp, int64_t sample_ba
 
 /* Radiance of an explicit list of (pixel, sample) paths — for timing a bounded sample of a
  * workload (bench.py cpu_baseline) and for per-path parity tests. out[k*3+c].
- * mode 0 = strict (the reference algorithm), 1 = fast (SAH BVH2, tMax culling, any-hit shadows). */
+ * mode 0 = strict (the reference algorithm), 1 = fast (SAH BVH2, tMax culling, any-hit shadows),
+ * 2 = strict with the direct hemisphere sampler (the statistical check of SURVEY.md §8(c)). */
 int oracle_paths_mode(OScene* s, uint64_t seed, int64_t n, const int32_t* px, const int32_t* py,
                       const int64_t* sample, int32_t nthreads, int32_t mode, double* out, double* stats) {
     if (mode == 1 && !s->fast.nodes) fast_bvh_build(&s->fast, s->prims, s->nprims);
@@ -826,7 +842,7 @@ int oracle_paths_mode(OScene* s, uint64_t seed, int64_t n, const int32_t* px, co
     for (int64_t k = 0; k < n; k++) {
         RayCounts rc;
         memset(&rc, 0, sizeof(rc));
-        C3 c = render_path(s, seed, px[k], py[k], sample[k], &rc, mode == 1);
+        C3 c = render_path(s, seed, px[k], py[k], sample[k], &rc, mode);
         out[k * 3 + 0] = c.r; out[k * 3 + 1] = c.g; out[k * 3 + 2] = c.b;
         tp += rc.primary; te += rc.extension; ts += rc.shadow; tpaths += rc.paths;
     }

@@ -92,7 +92,9 @@ class OracleScene:
 
     def paths(self, px, py, samples, seed: int, nthreads: int = 0, mode: str = "strict"):
         """Radiance of explicit (pixel, sample) paths. mode "strict" = the reference algorithm;
-        "fast" = SAH BVH2 with tMax culling and any-hit shadows (a CPU-baseline figure only)."""
+        "fast" = SAH BVH2 with tMax culling and any-hit shadows (a CPU-baseline figure only);
+        "direct" = strict with the hemisphere drawn directly instead of by rejection (the same
+        distribution, a different sample sequence: the statistical check of SURVEY.md §8(c))."""
         px = np.ascontiguousarray(px, dtype=np.int32)
         py = np.ascontiguousarray(py, dtype=np.int32)
         samples = np.ascontiguousarray(samples, dtype=np.int64)
@@ -100,7 +102,7 @@ class OracleScene:
         stats = np.zeros(8, dtype=np.float64)
         lib().oracle_paths_mode(self.h, seed, len(px), iptr(px), iptr(py),
                                 samples.ctypes.data_as(C.POINTER(C.c_int64)), nthreads,
-                                {"strict": 0, "fast": 1}[mode], dptr(out), dptr(stats))
+                                {"strict": 0, "fast": 1, "direct": 2}[mode], dptr(out), dptr(stats))
         return out, stats
 
     def closest_hit(self, rays: np.ndarray, tmin=1e-6, tmax=99999999.0):
