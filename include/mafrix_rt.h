@@ -200,8 +200,9 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * image depends only on the seed and its global index); mfx_reset, an spp != 1 call or mfx_sample
  * in between make the held frames recompute from the film as it then is. mfx_stats: the first call
  * served from a batch reports the K samples' rays and device time, the others 0 rays in 0 s. K is
- * cut to what fits in a quarter of the free HBM (one buffer, no background batch, if two do not
- * fit); when not even two samples fit, the context renders one sample per call. The accumulator
+ * cut to what fits in a quarter of the free HBM, or in MFX_RENDER_AHEAD_MAX_BYTES (environment)
+ * if smaller (one buffer, no background batch, if two do not fit); when not even two samples fit,
+ * the context frees the buffers and renders one sample per call from then on. The accumulator
  * (mfx_accum_read_mean) does not hold the samples of calls served from batches.                */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 

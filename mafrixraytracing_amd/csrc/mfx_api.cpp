@@ -1136,7 +1136,8 @@ static int ahead_alloc(mfx_ctx* c) {
     const size_t per_sample = plane + frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
     size_t fr = 0, tot = 0;
     HIPCHECK(hipMemGetInfo(&fr, &tot));
-    const size_t budget = fr / 4;  // both buffers within a quarter of the free HBM
+    size_t budget = fr / 4;  // both buffers within a quarter of the free HBM
+    if (const char* e = getenv("MFX_RENDER_AHEAD_MAX_BYTES")) budget = std::min(budget, (size_t)atoll(e));
     int nbuf = 2;
     int64_t k = c->render_ahead;
     if ((size_t)k * per_sample + fixed > budget / 2) {
@@ -1275,6 +1276,13 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
             rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
         else if (Y.epoch != c->film_epoch || Y.k0 != 0)  // held, but its frames assumed another film
             rc = ahead_frames(c, Y, 0, X.film_out, count_end);
+        // This call is served: a background batch that does not fit is not its failure (a NOMEM
+        // here would make the caller render the call a second time). Y stays empty; the call
+        // that needs it launches it, and falls back to one sample per call if it still fails.
+        if (rc == MFX_E_NOMEM) {
+            Y.n = 0;
+            rc = MFX_OK;
+        }
         if (rc) return rc;
     }
     return MFX_OK;
@@ -1309,7 +1317,12 @@ int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
         HIPCHECK(hipSetDevice(c->device));
         const int rc = ahead_render(c, rgba);
         if (rc != MFX_E_NOMEM) return rc;
-        c->render_ahead = 0;  // no room for the planes: this context renders one sample per call
+        // no room for the batch (nothing of this call was served): this context renders one
+        // sample per call from now on; the film comes back to d_film and the buffers are freed
+        c->render_ahead = 0;
+        const int rb = ahead_break(c);
+        if (rb) return rb;
+        ahead_free(c);
     }
     int rc = ahead_break(c);
     if (rc) return rc;

@@ -57,6 +57,25 @@ def test_render_ahead_pipeline_survives_interleaved_calls(gpu):
         assert np.array_equal(c1.film_mean(), c2.film_mean())
 
 
+@pytest.mark.parametrize("budget,label", [(1024, "none fits: one sample per call"),
+                                          (1 << 20, "one buffer, no background batch")])
+def test_render_ahead_memory_fallbacks(gpu, monkeypatch, budget, label):
+    """Render-ahead under a memory budget (MFX_RENDER_AHEAD_MAX_BYTES caps the quarter of free HBM
+    the buffers may take): with no room for two samples the context falls back to one sample per
+    call (the buffers freed, the film kept); with room for one buffer only it serves batches with
+    no background trace. Either way every frame and the film are the one-sample path's."""
+    from mafrixraytracing_amd.native import NativeContext
+    monkeypatch.setenv("MFX_RENDER_AHEAD_MAX_BYTES", str(budget))
+    a = scene("spot", 67, 37)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, render_ahead=16) as c2:
+        for k in range(40):
+            if k == 23:
+                c1.reset()
+                c2.reset()
+            assert np.array_equal(c1.render_rgba8(1), c2.render_rgba8(1)), (label, k)
+        assert np.array_equal(c1.film_mean(), c2.film_mean()), label
+
+
 def test_render_ahead_stats_account_for_whole_batches(gpu):
     """The batch call reports K samples' rays and device time; held calls report 0 rays in 0 s;
     over K calls the rays equal K one-sample calls'."""
