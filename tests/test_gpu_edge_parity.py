@@ -63,6 +63,33 @@ def test_soup_closest_and_shadow_exact(gpu, oracle, n, grid):
         assert (op >= 0).mean() > 0.01
 
 
+@pytest.mark.parametrize("scale,offset", [(1e3, 5e3), (0.05, 0.0), (1.0, 3e4)])
+def test_soup_far_from_unit_scale_exact(gpu, oracle, scale, offset):
+    """The FP32 search stays conservative away from unit scale: the soup and its rays scaled by
+    1e3 and moved 5e3 off the origin, shrunk to 0.05 (smaller, and the reference's absolute
+    |div| < 1e-6 cull, Trangle.fs:130, leaves nothing to hit), and moved 3e4 away (FP32 spacing
+    2^-9 there against triangles 0.05 across). Closest hits, normals and occlusion equal the
+    oracle's."""
+    from mafrixraytracing_amd.native import NativeContext
+    rng = np.random.default_rng(400)
+    a = soup(3000, rng, grid=True)
+    a.prims["p"] = a.prims["p"] * scale + offset
+    rays = edge_rays(6000, rng, True)
+    rays[:, :3] = rays[:, :3] * scale + offset
+    o = oracle.OracleScene(a)
+    ot, op, on = o.closest_hit(rays)
+    tmax = rng.uniform(0.05, 3.0, size=len(rays)) * scale
+    occ_o = o.any_hit(rays, tmax)
+    with NativeContext(a) as ctx:
+        gt, gp, gn = ctx.closest_hit(rays)
+        occ_g = ctx.any_hit(rays, tmax)
+    assert np.array_equal(gp, op), f"prim mismatch on {(gp != op).sum()} rays"
+    assert np.array_equal(gt, ot)
+    assert np.array_equal(gn, on)
+    assert np.array_equal(occ_g, occ_o), f"occlusion mismatch on {(occ_g != occ_o).sum()} rays"
+    assert (op >= 0).mean() > 0.01
+
+
 @pytest.mark.parametrize("n", [777, 5000])
 def test_soup_image_parity(gpu, oracle, n):
     from mafrixraytracing_amd.native import NativeContext
