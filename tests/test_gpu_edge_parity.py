@@ -90,6 +90,31 @@ def test_soup_far_from_unit_scale_exact(gpu, oracle, scale, offset):
     assert (op >= 0).mean() > 0.01
 
 
+@pytest.mark.parametrize("name", ["cube_cornell", "spot"])
+def test_scene_moved_far_from_origin_image_exact(gpu, oracle, name):
+    """A whole scene (geometry, light and camera) moved (1e4, -3e3, 2e4) away: the FP32 search's
+    widening grows with the coordinates and the FP64 paths see larger rounding
+    (self-hits near tMin = 1e-6 among them); the 4-spp image is still the oracle's bit for bit."""
+    from conftest import scene
+    from mafrixraytracing_amd.abi import SceneArrays
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, 48, 27)
+    off = np.array([1e4, -3e3, 2e4])
+    assert np.all(a.prims["kind"] != 2)  # (a sphere's p[1] is its radius, not a point)
+    prims = a.prims.copy()
+    prims["p"] = prims["p"] + off
+    light = dict(a.light, p=[list(np.asarray(q) + off) for q in a.light["p"]])
+    cam = dict(a.camera, position=list(np.asarray(a.camera["position"]) + off))
+    b = SceneArrays(prims, a.albedo, light, cam, a.width, a.height, a.max_depth)
+    ref, st = oracle.OracleScene(b).sample(4, SEED, with_stats=True)
+    with NativeContext(b, seed=SEED) as ctx:
+        img = ctx.sample(4)
+        counts = ctx.ray_counts()
+    assert tuple(counts[:3]) == tuple(st[:3])
+    assert np.array_equal(img, ref), np.abs(img - ref).max()
+    assert img[:, :3].max() > 0
+
+
 @pytest.mark.parametrize("n", [777, 5000])
 def test_soup_image_parity(gpu, oracle, n):
     from mafrixraytracing_amd.native import NativeContext
