@@ -286,6 +286,12 @@ def main():
         sys.exit(relaunch_distributed(args))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # Rehearsal of the N-rank job on a one-GPU box (tests/test_gpu_distributed.py): every rank on
+    # device MFX_BENCH_DEVICE, the process group over MFX_BENCH_BACKEND (gloo: RCCL refuses two ranks
+    # on one device). The driver's run sets neither: one GPU per rank, nccl (= RCCL).
+    if os.environ.get("MFX_BENCH_DEVICE") is not None:
+        local = int(os.environ["MFX_BENCH_DEVICE"])
+    backend = os.environ.get("MFX_BENCH_BACKEND", "nccl")
     ngpu = args.gpus if args.single_process else world  # GPUs of the job
     if args.api == "render" and world > 1:
         sys.exit("--api render is one process (use --single-process for N > 1)")
@@ -307,7 +313,7 @@ def main():
         import torch
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group(backend="nccl")  # RCCL over xGMI
+        dist.init_process_group(backend=backend)  # nccl = RCCL over xGMI
 
     arrays = load_scene_file(args.scene)
     W, H = arrays.width, arrays.height
@@ -338,7 +344,7 @@ def main():
             for _ in range(spp_step):
                 ctx.render_rgba8(1, out=rbuf)
         elif pr is not None:  # one process per GPU: trace own partition, RCCL reduce via torch
-            pr.frame(spp_step, base)
+            pr.frame(spp_step, base, all_ranks=backend == "gloo")  # (gloo reduces CUDA tensors with all_reduce)
         else:  # one GPU, or one context over the device list (the library's RCCL reduce)
             ctx.accum_clear()
             ctx.trace_accumulate(spp_step, base)

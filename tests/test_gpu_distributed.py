@@ -167,3 +167,27 @@ def test_bench_multiprocess_path_under_torchrun(gpu, tmp_path):
     assert "process group" in line["config"]["parallelism"]
     # rays per step are a property of the sample set: equal whichever path traced it
     assert line["rays_per_step"] == plain["rays_per_step"] > 0
+
+
+def test_bench_two_ranks_rehearsal_under_torchrun(gpu):
+    """The driver's N-GPU launch rehearsed on one GPU: bench.py under torch.distributed.run with 2
+    ranks, both on device 0 over gloo (MFX_BENCH_DEVICE / MFX_BENCH_BACKEND; RCCL refuses two ranks
+    on one device). The whole world > 1 path runs — partitions, pipelined frames and reduces, the
+    barrier, max-over-ranks timing, the rays summed over ranks — and the line reports 2 GPUs,
+    weak scaling, and the rays of the 2x larger sample set (equal to a 1-rank run of that set)."""
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    env = dict(os.environ, MFX_BENCH_DEVICE="0", MFX_BENCH_BACKEND="gloo")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--spp", "2"] + common
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["config"]["global_spp_per_step"] == 4
+    # one process, the same 4-spp-per-step sample set: the same rays per step
+    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--spp", "4"] + common, capture_output=True,
+                        text=True, timeout=300, cwd=ROOT)
+    assert r1.returncode == 0, r1.stderr[-3000:]
+    one = json.loads(r1.stdout.strip().splitlines()[-1])
+    assert line["rays_per_step"] == one["rays_per_step"] > 0
+
