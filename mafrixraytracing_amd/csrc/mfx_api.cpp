@@ -106,7 +106,7 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
-    void* d_tnodes = nullptr;       // flat scenes: the per-lane traversal's nodes (MFX_WIDE / MFX_NODE16, mfx_wide.cpp)
+    MfxNode8H* d_wide = nullptr;    // flat scenes: the per-lane traversal's BVH8 (MFX_WIDE, mfx_wide.cpp)
     MfxWideXf wide_xf{0, 0, 0, 1};
     int32_t wide_nodes = 0;
     MfxTri32* d_tri32 = nullptr;  // FP32 triangle copies of the slots (the leaf screen)
@@ -193,8 +193,8 @@ struct mfx_ctx {
 
 // the nodes the per-lane traversal reads
 static const MfxTNode* tnodes_of(const mfx_ctx* c) {
-#if MFX_TNODE_XF
-    return (const MfxTNode*)c->d_tnodes;  // null for two-level scenes, whose kernels read the BVH4
+#if MFX_WIDE
+    return c->d_wide;  // null for two-level scenes, whose kernels read the BVH4
 #else
     return c->d_nodes;
 #endif
@@ -232,7 +232,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_tnodes, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_wide, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -292,14 +292,7 @@ static int ctx_setup(mfx_ctx* c) {
         if (c->stack_size > 96) return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
         c->wide_xf = wi.xf;
         c->wide_nodes = (int32_t)wi.nodes.size();
-        CK(upload((MfxNode8H**)&c->d_tnodes, wi.nodes));
-    }
-#elif MFX_NODE16
-    if (c->host.inst.empty()) {
-        std::vector<MfxNodeH> h;
-        std::string e;
-        if (!mfx_build_half4(c->host.nodes, h, c->wide_xf, e)) return fail(MFX_E_INVALID, "mfx_create: " + e);
-        CK(upload((MfxNodeH**)&c->d_tnodes, h));
+        CK(upload(&c->d_wide, wi.nodes));
     }
 #endif
     CK(upload(&c->d_slots, c->host.slots));

@@ -58,30 +58,11 @@ static_assert(sizeof(MfxNode8H) == 128, "one line per wide node");
 struct MfxWideXf {
     double cx, cy, cz, s;
 };
-// The per-lane traversal's BVH4 with FP16 planes (MFX_NODE16; flat scenes): the BVH4's nodes,
-// indices and children unchanged, every plane stored as FP16 in the BVH8's scene frame (centre,
-// power-of-2 scale), rounded outward; 64 B, four 16-B loads per node step instead of seven.
-#ifndef MFX_NODE16
-#define MFX_NODE16 0
-#endif
-struct alignas(16) MfxNodeH {
-    uint16_t x[8];  // lo[0..3], hi[0..3] of the four children along x (FP16 bits)
-    uint16_t y[8];
-    uint16_t z[8];
-    int32_t child[4];  // as MfxNode::child
-};
-static_assert(sizeof(MfxNodeH) == 64, "four columns per FP16 node");
-#if MFX_WIDE && MFX_NODE16
-#error "MFX_WIDE and MFX_NODE16 are alternatives"
-#endif
 #if MFX_WIDE
 typedef MfxNode8H MfxTNode;
-#elif MFX_NODE16
-typedef MfxNodeH MfxTNode;
 #else
 typedef MfxNode MfxTNode;
 #endif
-#define MFX_TNODE_XF (MFX_WIDE || MFX_NODE16)  // the per-lane nodes are stored in the scene frame
 // nodes[0 .. MFX_TOP_NODES) are the BVH's top levels in breadth-first order (the trace kernels
 // keep a prefix of them in LDS); the rest follow in preorder
 #ifndef MFX_TOP_NODES

@@ -690,8 +690,8 @@ __device__ __forceinline__ float f_tlim(double x) { return fminf(f_round_up(x), 
 #ifndef MFX_NEAR_FAR_PLANES
 #define MFX_NEAR_FAR_PLANES 0  // 1: node steps read each axis's near / far planes by the ray's direction signs
 #endif
-#if MFX_NEAR_FAR_PLANES && MFX_TNODE_XF
-#error "MFX_NEAR_FAR_PLANES reads BVH4 FP32 nodes: build it with MFX_WIDE=0 MFX_NODE16=0"
+#if MFX_NEAR_FAR_PLANES && MFX_WIDE
+#error "MFX_NEAR_FAR_PLANES reads BVH4 FP32 nodes: build it with MFX_WIDE=0"
 #endif
 
 // FP32 ray for the cluster-BVH slab tests
@@ -724,7 +724,7 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
 // the FP32 search ray of a flat scene's per-lane traversal: in the BVH8's frame (MfxNode8H: o' =
 // (o - c) * s, d' = d * s, s a power of 2, so every slab distance is the world one)
 __device__ __forceinline__ RayF make_rayf_t(const SceneView& S, DV o, DV d) {
-#if MFX_TNODE_XF
+#if MFX_WIDE
     const double s = S.wx.s;
     return make_rayf(dv((o.x - S.wx.cx) * s, (o.y - S.wx.cy) * s, (o.z - S.wx.cz) * s), dv(d.x * s, d.y * s, d.z * s));
 #else
@@ -803,16 +803,13 @@ struct TopNodes {
     const float4* lds;
     int ntop;
 };
-// (an FP16 BVH4 node, MfxNodeH, is four columns: column c at n * 4 + (c ^ ((n >> 1) & 3)))
-template <int COLS = 8>
-__device__ __forceinline__ int top_col(int n, int c) { return n * COLS + (c ^ ((n >> 1) & (COLS - 1))); }
+__device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
 // block-wide copy at kernel start (all threads; ends with a barrier); BVH4 (MfxNode) and BVH8
-// (MfxNode8H) nodes are eight 16-B columns, FP16 BVH4 nodes (MfxNodeH) four
+// (MfxNode8H) nodes are both eight 16-B columns
 static_assert(sizeof(MfxNode) == 128 && sizeof(MfxNode8H) == 128, "top nodes are 8 columns");
-template <int COLS = 8>
 __device__ __forceinline__ void load_top_nodes(float4* lds, const void* __restrict__ nodes, int ntop) {
     const float4* __restrict__ g = (const float4*)nodes;
-    for (int i = threadIdx.x; i < ntop * COLS; i += blockDim.x) lds[top_col<COLS>(i / COLS, i % COLS)] = g[i];
+    for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
     __syncthreads();
 }
 
@@ -954,75 +951,6 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     if (nh >= 4) stack.put(sp + 2, c[1], dp);
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
-    sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
-    return next;
-}
-
-// A lane's prefetched node (MFX_NODE_PREFETCH): the FP16 node on top of its stack after its last
-// step — the next pop — loaded at the end of that step, so a step that starts from a pop (after a
-// leaf, or after a step that hit nothing) finds its node in registers.
-#ifndef MFX_NODE_PREFETCH
-#define MFX_NODE_PREFETCH 0
-#endif
-struct NodePf {
-    mfx_i4 q[4];
-    int id;  // the node q holds (-1: none)
-};
-
-// One node step of the FP16 BVH4 (MfxNodeH, MFX_NODE16): the BVH4 step with four 16-B loads, the
-// planes read through v_fma_mix_f32 (FP16 operand, FP32 arithmetic) in the scene frame.
-// PF: take the node from pf when it holds it, and prefetch the next pop into it.
-template <bool TOP = false, bool FAR = false, bool PF = false, typename ST>
-__device__ __forceinline__ int node_step(const MfxNodeH* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0},
-                                         NodePf* pf = nullptr) {
-    const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
-    const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    mfx_i4 qx, qy, qz, qc;
-    if (PF && node == pf->id) {
-        qx = pf->q[0]; qy = pf->q[1]; qz = pf->q[2]; qc = pf->q[3];
-    } else if (TOP && node < tn.ntop) {
-        const int sw = (node >> 1) & 3;
-        const mfx_i4* t = (const mfx_i4*)tn.lds + node * 4;
-        qx = t[0 ^ sw]; qy = t[1 ^ sw]; qz = t[2 ^ sw]; qc = t[3 ^ sw];
-    } else {
-        const mfx_i4* __restrict__ q = (const mfx_i4*)(nodes + node);
-        qx = q[0]; qy = q[1]; qz = q[2]; qc = q[3];
-    }
-    const h8 X = __builtin_bit_cast(h8, qx), Y = __builtin_bit_cast(h8, qy), Z = __builtin_bit_cast(h8, qz);
-    float d[4];
-    int c[4] = {qc.x, qc.y, qc.z, qc.w};
-    int nh = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const float a0 = fmaf((float)X[k], r.ix, -r.oix), a1 = fmaf((float)X[4 + k], r.ix, -r.oix);
-        const float b0 = fmaf((float)Y[k], r.iy, -r.oiy), b1 = fmaf((float)Y[4 + k], r.iy, -r.oiy);
-        const float c0 = fmaf((float)Z[k], r.iz, -r.oiz), c1 = fmaf((float)Z[4 + k], r.iz, -r.oiz);
-        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-        const bool h = n <= f;
-        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
-        nh += h ? 1 : 0;
-    }
-    cswap(d[0], c[0], d[1], c[1]);
-    cswap(d[2], c[2], d[3], c[3]);
-    cswap(d[0], c[0], d[2], c[2]);
-    cswap(d[1], c[1], d[3], c[3]);
-    cswap(d[1], c[1], d[2], c[2]);
-    if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]), dp);
-    if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1], dp);
-    if (nh >= 4) stack.put(sp + 2, c[1], dp);
-    const bool pop = nh == 0 && sp > 0;
-    const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
-    if (PF) {  // the stack's top after this step: the nearest pushed child, the old top, or the one below it
-        const int nt = nh >= 2 ? c[1] : (nh == 1 ? (sp > 0 ? top : -1) : (sp >= 2 ? stack.get(sp - 2, dp) : -1));
-        if (nt >= (TOP ? tn.ntop : 0) && nt != pf->id) {
-            const mfx_i4* __restrict__ q = (const mfx_i4*)(nodes + nt);
-            pf->q[0] = q[0]; pf->q[1] = q[1]; pf->q[2] = q[2]; pf->q[3] = q[3];
-            pf->id = nt;
-        }
-    }
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
     return next;
 }

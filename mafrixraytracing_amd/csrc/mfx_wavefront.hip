@@ -199,7 +199,6 @@ struct Trav {
     int inst_sp;  // and the stack depth at which it entered (entries below belong to the world)
     int pleaf;  // MFX_SPECULATIVE: a postponed leaf's code (-1: none)
     int pbase;  // and the slot base of its frame (two-level scenes)
-    NodePf pf;  // MFX_NODE_PREFETCH: the next pop's node, prefetched
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
@@ -213,22 +212,15 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.inst_sp = 0;
     T.pleaf = -1;
     T.pbase = 0;
-    T.pf.id = -1;
 }
-
-constexpr int kTCols = (int)(sizeof(MfxTNode) / 16);  // 16-B columns of a per-lane traversal node
 
 // one node step of the per-lane traversal: the BVH4 in two-level scenes, else the flat scene's
 // traversal image (MfxTNode)
 template <bool SHADOW, bool INST, typename ST>
 __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, const RayF& rf, float tlim, const ST& stack,
-                                              int& sp, TopNodes tn, NodePf& pf) {
+                                              int& sp, TopNodes tn) {
     if constexpr (INST) return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
-#if MFX_NODE16 && MFX_NODE_PREFETCH
-    else return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1, true>(S.tnodes, node, rf, tlim, stack, sp, tn, &pf);
-#else
     else return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.tnodes, node, rf, tlim, stack, sp, tn);
-#endif
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
@@ -255,7 +247,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (T.node >= 0) {
             if (STATS) st.nodes++;
             if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;
-            T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn, T.pf);
+            T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
             if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         }
         if (T.node < 0 && T.node != MFX_TRAV_EXIT && T.pleaf < 0) {  // postpone the leaf, pop the next entry
@@ -288,7 +280,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (STATS && !SHADOW && T.B.found) st.after_nodes++;
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn, T.pf);
+        T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
         if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
@@ -442,9 +434,8 @@ template <bool STATS, bool SPILL, bool INST>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
-    if (INST) load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
-    else load_top_nodes<kTCols>((float4*)lds_all, P.tnodes, P.ntop_ext);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * (INST ? 32 : 4 * kTCols));
+    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_ext);
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
@@ -677,9 +668,8 @@ template <bool STATS, bool SPILL, int WAVES, bool INST>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
-    if (INST) load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
-    else load_top_nodes<kTCols>((float4*)lds_all, P.tnodes, P.ntop_shd);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * (INST ? 32 : 4 * kTCols));
+    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_shd);
+    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int lane = lane_id();
@@ -1092,7 +1082,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // top nodes, stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
 static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst) {
-    const size_t stacks = (size_t)ntop * (ninst ? sizeof(MfxNode) : sizeof(MfxTNode)) + (size_t)ninst * sizeof(MfxInstance) +
+    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) +
                           (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;

@@ -83,67 +83,6 @@ uint16_t plane(float v, double c, double s, bool up) {
 }
 }  // namespace
 
-// The frame of the FP16 planes: the centre of the root's box, and a power-of-2 scale that puts
-// every (finite) plane of the image within 2^15 of it.
-static MfxWideXf scene_frame(const std::vector<MfxNode>& n4) {
-    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-    bool any = false;
-    const MfxNode& r = n4[0];
-    for (int k = 0; k < 4; ++k) {
-        if (r.child[k] == MFX_CHILD_EMPTY) continue;
-        any = true;
-        const float rl[3] = {r.lox[k], r.loy[k], r.loz[k]}, rh[3] = {r.hix[k], r.hiy[k], r.hiz[k]};
-        for (int a = 0; a < 3; ++a) {
-            lo[a] = std::min(lo[a], (double)rl[a]);
-            hi[a] = std::max(hi[a], (double)rh[a]);
-        }
-    }
-    double c[3] = {0, 0, 0};
-    if (any)
-        for (int a = 0; a < 3; ++a) c[a] = (double)(float)(0.5 * lo[a] + 0.5 * hi[a]);
-    double maxabs = 0.0;
-    for (const MfxNode& n : n4)
-        for (int k = 0; k < 4; ++k) {
-            if (n.child[k] == MFX_CHILD_EMPTY) continue;
-            const float nl[3] = {n.lox[k], n.loy[k], n.loz[k]}, nh[3] = {n.hix[k], n.hiy[k], n.hiz[k]};
-            for (int a = 0; a < 3; ++a)
-                maxabs = std::max({maxabs, std::fabs((double)nl[a] - c[a]), std::fabs((double)nh[a] - c[a])});
-        }
-    double s = 1.0;
-    if (maxabs > 0.0 && std::isfinite(maxabs)) {
-        int ex;
-        (void)std::frexp(maxabs, &ex);  // maxabs < 2^ex
-        s = std::ldexp(1.0, std::max(-60, std::min(60, 15 - ex)));
-    }
-    return MfxWideXf{c[0], c[1], c[2], s};
-}
-
-bool mfx_build_half4(const std::vector<MfxNode>& n4, std::vector<MfxNodeH>& out, MfxWideXf& xf, std::string& err) {
-    if (n4.empty()) {
-        err = "empty BVH4 image";
-        return false;
-    }
-    xf = scene_frame(n4);
-    const double c[3] = {xf.cx, xf.cy, xf.cz};
-    out.resize(n4.size());
-    for (size_t i = 0; i < n4.size(); ++i) {
-        const MfxNode& n = n4[i];
-        MfxNodeH& h = out[i];
-        const float* lo[3] = {n.lox, n.loy, n.loz};
-        const float* hi[3] = {n.hix, n.hiy, n.hiz};
-        uint16_t* dst[3] = {h.x, h.y, h.z};
-        for (int k = 0; k < 4; ++k) {
-            const bool empty = n.child[k] == MFX_CHILD_EMPTY;
-            for (int a = 0; a < 3; ++a) {
-                dst[a][k] = empty ? 0x7C00 : plane(lo[a][k], c[a], xf.s, false);
-                dst[a][4 + k] = empty ? 0x7C00 : plane(hi[a][k], c[a], xf.s, true);
-            }
-            h.child[k] = n.child[k];
-        }
-    }
-    return true;
-}
-
 bool mfx_build_wide(const std::vector<MfxNode>& n4, MfxWideImage& out, std::string& err) {
     out = MfxWideImage{};
     const int N4 = (int)n4.size();
@@ -220,8 +159,27 @@ bool mfx_build_wide(const std::vector<MfxNode>& n4, MfxWideImage& out, std::stri
     out.stack_entries = std::max(1, bound[0]);
     out.depth = depth[0];
     // ---- frame: centre of the root's box, a power-of-2 scale that puts every plane within 2^15 ----
-    out.xf = scene_frame(n4);
-    const double c[3] = {out.xf.cx, out.xf.cy, out.xf.cz}, s = out.xf.s;
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (const Ent& x : ents[0])
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo[a], (double)x.lo[a]);
+            hi[a] = std::max(hi[a], (double)x.hi[a]);
+        }
+    double c[3] = {0, 0, 0};
+    if (!ents[0].empty())
+        for (int a = 0; a < 3; ++a) c[a] = (double)(float)(0.5 * lo[a] + 0.5 * hi[a]);
+    double maxabs = 0.0;
+    for (const auto& e : ents)
+        for (const Ent& x : e)
+            for (int a = 0; a < 3; ++a)
+                maxabs = std::max({maxabs, std::fabs((double)x.lo[a] - c[a]), std::fabs((double)x.hi[a] - c[a])});
+    double s = 1.0;
+    if (maxabs > 0.0 && std::isfinite(maxabs)) {
+        int ex;
+        (void)std::frexp(maxabs, &ex);  // maxabs < 2^ex
+        s = std::ldexp(1.0, std::max(-60, std::min(60, 15 - ex)));
+    }
+    out.xf = MfxWideXf{c[0], c[1], c[2], s};
     // ---- encode ----
     out.nodes.resize(W);
     for (int w = 0; w < W; ++w) {

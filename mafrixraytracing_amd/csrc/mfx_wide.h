@@ -18,9 +18,6 @@ struct MfxWideImage {
 // BVH4 (root 0, flat scene: no instance codes) -> BVH8. False with `err` set on a malformed image.
 bool mfx_build_wide(const std::vector<MfxNode>& n4, MfxWideImage& out, std::string& err);
 
-// BVH4 -> the same BVH4 with FP16 planes in the scene frame (MfxNodeH, MFX_NODE16).
-bool mfx_build_half4(const std::vector<MfxNode>& n4, std::vector<MfxNodeH>& out, MfxWideXf& xf, std::string& err);
-
 // The image's invariants against the BVH4 it came from (every leaf once; boxes contain their
 // subtrees); false with `err` set otherwise.
 bool mfx_check_wide(const std::vector<MfxNode>& n4, const MfxWideImage& w, std::string& err, double* mean_entries,
