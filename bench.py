@@ -66,7 +66,7 @@ CONFIG_FLAGS = {"C5T": 32}  # mafrixraytracing_amd.abi.MFX_F_TWO_LEVEL
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS),
                     help="BASELINE.json workload (C2 default: the metric's configuration)")
