@@ -143,17 +143,6 @@ struct mfx_ctx {
     // of the free HBM.
     int64_t wf_pool_max = 1 << 28;
     unsigned long long* d_wfctl = nullptr;  // [WF_NCTL] chunk heads
-    // Generation pipeline (MFX_GEN_STREAMS = 2): a frame's generations alternate between two path
-    // pools, each traced on its own stream, so one generation's launches run in the other's launch
-    // tails; the resolves stay in generation order (each waits for the previous one's event)
-    int gen_streams = 1;
-    hipStream_t stream2 = nullptr;
-    WfParams wf2{};
-    void* wf_mem2 = nullptr;
-    int32_t wf_pool2 = 0;
-    unsigned long long* d_wfctl2 = nullptr;
-    int32_t* d_spill2 = nullptr;
-    hipEvent_t gen_done[2] = {};     // per stream: its last generation's resolve has run
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
     int generations = 0;
@@ -244,15 +233,11 @@ static void free_ctx(mfx_ctx* c) {
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     void* bufs[] = {c->d_nodes, c->d_wide, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo,
-                    c->wf_mem2, c->d_wfctl2, c->d_spill2};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     ahead_free(c);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
-    if (c->stream2) (void)hipStreamDestroy(c->stream2);
-    for (hipEvent_t e : c->gen_done)
-        if (e) (void)hipEventDestroy(e);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->stage_ev)
@@ -464,13 +449,6 @@ static int ctx_setup(mfx_ctx* c) {
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
         const int deep = c->stack_size - std::min(c->wf_stack_lds_ext, c->wf_stack_lds_shd);
         CK(hipMalloc((void**)&c->d_spill, sizeof(int32_t) * lanes * std::max(1, deep)));
-        if (const char* e = getenv("MFX_GEN_STREAMS")) c->gen_streams = atoi(e) == 2 ? 2 : 1;
-        if (c->gen_streams == 2) {
-            CK(hipStreamCreateWithFlags(&c->stream2, hipStreamNonBlocking));
-            CK(hipMalloc((void**)&c->d_wfctl2, WF_NCTL * sizeof(unsigned long long)));
-            CK(hipMalloc((void**)&c->d_spill2, sizeof(int32_t) * lanes * std::max(1, deep)));
-            for (hipEvent_t& e : c->gen_done) CK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        }
     }
     CK(hipMalloc((void**)&c->d_vscratch, sizeof(double) * 6 * (size_t)(c->host.max_depth + 1) * c->grid * 256));
 #undef CK
@@ -684,33 +662,30 @@ int mfx_wide_info(const mfx_scene_desc* scene, double out[8]) {
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
 // Allocate (or grow) the wavefront path-slot pool (SoA).
-static int wf_ensure_pool(mfx_ctx* c, int32_t pool, int which = 0) {
-    void*& mem = which ? c->wf_mem2 : c->wf_mem;
-    int32_t& have = which ? c->wf_pool2 : c->wf_pool;
-    WfParams& W = which ? c->wf2 : c->wf;
-    if (pool <= have) return MFX_OK;
-    if (mem) (void)hipFree(mem);
-    mem = nullptr;
-    have = 0;
+static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
+    if (pool <= c->wf_pool) return MFX_OK;
+    if (c->wf_mem) (void)hipFree(c->wf_mem);
+    c->wf_mem = nullptr;
+    c->wf_pool = 0;
     const size_t P = (size_t)pool;
     const int nv = c->host.max_depth + 1;  // vertices per path
     const size_t bytes = P * (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4) + 64 * 256;
-    hipError_t e = hipMalloc(&mem, bytes);
+    hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
-    char* p = (char*)mem;
+    char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
-    double** dbl[6] = {&W.ox, &W.oy, &W.oz, &W.dx, &W.dy, &W.dz};
+    double** dbl[6] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz};
     for (double** d : dbl) *d = (double*)take(P * 8);
-    W.vei = (double*)take(P * 8 * nv);
-    W.vls = (double*)take(P * 8 * 2 * nv);
-    W.vmat = (WfMat*)take(P * sizeof(WfMat) * nv);
-    W.vstride = (int64_t)P;
-    W.key = (uint64_t*)take(P * 8);
-    W.rn = (uint32_t*)take(P * 4);
-    W.depth = (int32_t*)take(P * 4);
-    W.state = (int32_t*)take(P * 4);
-    have = pool;
+    c->wf.vei = (double*)take(P * 8 * nv);
+    c->wf.vls = (double*)take(P * 8 * 2 * nv);
+    c->wf.vmat = (WfMat*)take(P * sizeof(WfMat) * nv);
+    c->wf.vstride = (int64_t)P;
+    c->wf.key = (uint64_t*)take(P * 8);
+    c->wf.rn = (uint32_t*)take(P * 4);
+    c->wf.depth = (int32_t*)take(P * 4);
+    c->wf.state = (int32_t*)take(P * 4);
+    c->wf_pool = pool;
     return MFX_OK;
 }
 
@@ -746,13 +721,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
     const int64_t total = per_sample * ns;
     // generations of whole 64-path windows (one 8x8 tile of one sample each: the camera-ray packets)
-    int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
-    // generation pipeline: at least two generations, each pool at most half the one-pool budget
-    const bool two = c->gen_streams == 2 && total >= 2 * 4096;
-    if (two) gen_max = std::min<int64_t>((total + 1) / 2, std::max<int64_t>(4096, c->wf_pool_max / 2 / 4096 * 4096));
+    const int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
     const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
     int rc = wf_ensure_pool(c, pool);
-    if (!rc && two) rc = wf_ensure_pool(c, pool, 1);
     if (rc) return rc;
     WfParams P = c->wf;
     fill_scene_params(c, P);
@@ -790,38 +761,26 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         c->it_ev.push_back(e);
     }
     HIPCHECK(hipEventRecord(own_events ? c->ev0 : e0, c->stream));
-    // the second stream starts behind everything enqueued before this trace (clears, counter resets)
-    if (two) HIPCHECK(hipStreamWaitEvent(c->stream2, own_events ? c->ev0 : e0, 0));
     int it = 0;
     for (int64_t g = 0; g < ngen; ++g) {
-        const int sid = two ? (int)(g & 1) : 0;
-        hipStream_t st = sid ? c->stream2 : c->stream;
-        {  // this generation's pool, chunk heads and spill stacks
-            const WfParams& W = sid ? c->wf2 : c->wf;
-            P.ox = W.ox; P.oy = W.oy; P.oz = W.oz; P.dx = W.dx; P.dy = W.dy; P.dz = W.dz;
-            P.vei = W.vei; P.vls = W.vls; P.vmat = W.vmat; P.vstride = W.vstride;
-            P.key = W.key; P.rn = W.rn; P.depth = W.depth; P.state = W.state;
-            P.ctl = sid ? c->d_wfctl2 : c->d_wfctl;
-            P.spill = sid ? c->d_spill2 : c->d_spill;
-        }
         P.path_base = g * gen_max;
         P.base_smp = P.path_base / per_sample;
         P.base_q = P.path_base % per_sample;
         P.total = std::min<int64_t>(gen_max, total - P.path_base);
         P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
-        HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, st));
+        HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
         for (int d = 0; d <= P.max_depth; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;
             if (!own_events) {
-                HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, st, nullptr));
+                HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;
             }
             hipEvent_t* ev = c->it_ev.data() + 3 * it;
-            HIPCHECK(hipEventRecord(ev[0], st));
-            HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, st, ev + 1));
-            HIPCHECK(hipEventRecord(ev[2], st));
+            HIPCHECK(hipEventRecord(ev[0], c->stream));
+            HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, ev + 1));
+            HIPCHECK(hipEventRecord(ev[2], c->stream));
             if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
-                HIPCHECK(hipStreamSynchronize(st));
+                HIPCHECK(hipStreamSynchronize(c->stream));
                 unsigned long long h[WF_NCTR * WF_SHARDS];
                 HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
                 double r[WF_NCTR] = {0};
@@ -837,13 +796,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
                         r[16], r[17]);
             }
         }
-        // the accumulator takes the generations in order: this resolve after the previous one
-        if (two && g > 0) HIPCHECK(hipStreamWaitEvent(st, c->gen_done[sid ^ 1], 0));
-        HIPCHECK(mfx_wf_resolve(P, st));
-        if (two) HIPCHECK(hipEventRecord(c->gen_done[sid], st));
+        HIPCHECK(mfx_wf_resolve(P, c->stream));
     }
-    // the context's stream ends behind the second stream's last generation
-    if (two && ngen > 1) HIPCHECK(hipStreamWaitEvent(c->stream, c->gen_done[1], 0));
     if (!own_events) {
         HIPCHECK(hipEventRecord(e1, c->stream));
         return MFX_OK;
