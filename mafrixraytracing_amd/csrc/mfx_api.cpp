@@ -137,12 +137,18 @@ struct mfx_ctx {
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
+    // MFX_RAY_QUEUE: the ray queues, and the first iteration (0-based) whose k_shadow moves the
+    // continuing paths to one (-1: every iteration in place; MFX_RAY_QUEUE=0 / MFX_QUEUE_FROM=d)
+    WfQueue wq[2]{};
+    int wf_queue_from = MFX_RAY_QUEUE ? -2 : -1;  // -2: automatic (wf_queue_auto)
+    int wf_queue_auto = 1;  // from the last trace's live paths per iteration (note_live); 1 before any
+    int32_t wf_qchunk = 256;  // entries per chunk fetch on a ray queue (MFX_QCHUNK)
     // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
     // slots, 15 GB) runs the frame as one generation: no kernel ends with a partly filled pool
     // (+11 % on C2 over 32 M slots). Capped at 2^28 slots (31 GB of the 288 GB) and at a quarter
     // of the free HBM.
     int64_t wf_pool_max = 1 << 28;
-    unsigned long long* d_wfctl = nullptr;  // [WF_NCTL] chunk heads
+    unsigned long long* d_wfctl = nullptr;  // [WF_CTL_ALLOC] queue 0 counts, chunk heads, queue 1 counts
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
     int generations = 0;
@@ -332,7 +338,7 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
     CK(hipMalloc((void**)&c->d_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
-    CK(hipMalloc((void**)&c->d_wfctl, WF_NCTL * sizeof(unsigned long long)));
+    CK(hipMalloc((void**)&c->d_wfctl, WF_CTL_ALLOC * sizeof(unsigned long long)));
     {
         size_t mfree = 0, mtotal = 0;
         if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
@@ -344,6 +350,11 @@ static int ctx_setup(mfx_ctx* c) {
     }
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
+    if (const char* qf = getenv("MFX_QUEUE_FROM")) c->wf_queue_from = MFX_RAY_QUEUE ? std::max(-2, atoi(qf)) : -1;
+    if (const char* qc = getenv("MFX_QCHUNK")) c->wf_qchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(qc) / 64 * 64));
+    if (const char* rq = getenv("MFX_RAY_QUEUE")) {
+        if (atoi(rq) == 0) c->wf_queue_from = -1;
+    }
     if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
     if (const char* ck = getenv("MFX_CHUNK")) {
         c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
@@ -685,8 +696,58 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     c->wf.rn = (uint32_t*)take(P * 4);
     c->wf.depth = (int32_t*)take(P * 4);
     c->wf.state = (int32_t*)take(P * 4);
+#if MFX_RAY_QUEUE
+    // queue 0: its own arrays; queue 1: the pool's ray arrays (o, d, key, rn: dead once the
+    // iterations run on queues) and its own depth, state and slot words
+    WfQueue& q0 = c->wq[0];
+    double** q0d[6] = {&q0.ox, &q0.oy, &q0.oz, &q0.dx, &q0.dy, &q0.dz};
+    for (double** d : q0d) *d = (double*)take(P * 8);
+    q0.key = (uint64_t*)take(P * 8);
+    q0.rn = (uint32_t*)take(P * 4);
+    WfQueue& q1 = c->wq[1];
+    q1.ox = c->wf.ox; q1.oy = c->wf.oy; q1.oz = c->wf.oz;
+    q1.dx = c->wf.dx; q1.dy = c->wf.dy; q1.dz = c->wf.dz;
+    q1.key = c->wf.key;
+    q1.rn = c->wf.rn;
+    for (WfQueue* q : {&q0, &q1}) {
+        q->depth = (int32_t*)take(P * 4);
+        q->state = (int32_t*)take(P * 4);
+        q->slot = (int32_t*)take(P * 4);
+    }
+    q0.count = c->d_wfctl;                                  // WF_CTL_Q0
+    q1.count = c->d_wfctl - WF_CTL_Q0 + WF_CTL_Q1;
+#endif
     c->wf_pool = pool;
     return MFX_OK;
+}
+
+// Iteration d's arrays (MFX_RAY_QUEUE, mfx_wavefront.h WfParams): the pool itself up to iteration
+// q = wf_queue_from, whose k_shadow moves the continuing paths to queue 0; iteration d > q reads
+// queue (d - q - 1) & 1 and writes the other. d = -1: the pool (k_resolve).
+static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
+    const WfParams& A = c->wf;
+    P.ox = A.ox; P.oy = A.oy; P.oz = A.oz; P.dx = A.dx; P.dy = A.dy; P.dz = A.dz;
+    P.key = A.key; P.rn = A.rn; P.depth = A.depth; P.state = A.state;
+    P.fstate = A.state;
+    P.fdepth = A.depth;
+    P.qslot = nullptr;
+    P.qcount = nullptr;
+    P.ncount = nullptr;
+    const int q = c->wf_queue_from == -2 ? c->wf_queue_auto : c->wf_queue_from;
+    if (q < 0 || d < 0) return;
+    if (d > q) {
+        const WfQueue& R = c->wq[(d - q - 1) & 1];
+        P.ox = R.ox; P.oy = R.oy; P.oz = R.oz; P.dx = R.dx; P.dy = R.dy; P.dz = R.dz;
+        P.key = R.key; P.rn = R.rn; P.depth = R.depth; P.state = R.state;
+        P.qslot = R.slot;
+        P.qcount = R.count;
+    }
+    if (d >= q && d < P.max_depth) {
+        const WfQueue& N = c->wq[(d - q) & 1];
+        P.nox = N.ox; P.noy = N.oy; P.noz = N.oz; P.ndx = N.dx; P.ndy = N.dy; P.ndz = N.dz;
+        P.nkey = N.key; P.nrn = N.rn; P.ndepth = N.depth; P.nstate = N.state; P.nslot = N.slot;
+        P.ncount = N.count;
+    }
 }
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
@@ -727,7 +788,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     if (rc) return rc;
     WfParams P = c->wf;
     fill_scene_params(c, P);
-    P.ctl = c->d_wfctl;
+    P.ctl = c->d_wfctl - WF_CTL_Q0;
     P.counters = counters ? counters : c->d_counters;
     const bool own_events = e0 == nullptr;
     P.seed = c->seed;
@@ -749,6 +810,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     // the last big chunks of a launch are a larger share of it (r03e/r03f: 8 spp +6 %, 64 spp -1 %)
     P.chunk = c->wf_chunk_env ? c->wf_chunk : (total <= ((int64_t)1 << 25) ? 512 : c->wf_chunk);
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
+    const int32_t chunk0 = P.chunk;
     P.planes = planes;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     P.cam_grid = c->host.inst.empty() ? c->wf_cam_grid : 0;
@@ -771,6 +833,10 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
         for (int d = 0; d <= P.max_depth; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;
+            P.iter = d;
+            wf_queue_views(c, P, d);
+            // a queue's entries are all live rays: smaller chunks keep the launch's tail short
+            P.chunk = P.qcount && !c->wf_chunk_env ? c->wf_qchunk : chunk0;
             if (!own_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;
@@ -786,6 +852,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
                 double r[WF_NCTR] = {0};
                 for (int k = 0; k < WF_SHARDS; ++k)
                     for (int q = 0; q < WF_NCTR; ++q) r[q] += (double)h[WF_NCTR * k + q];
+                for (int q = WF_CTR_ITER + 1; q < WF_CTR_ITER + WF_ITER_CTRS; ++q) r[1] += r[q];
                 float fe = 0.f, fs = 0.f;
                 HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
@@ -796,6 +863,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
                         r[16], r[17]);
             }
         }
+        wf_queue_views(c, P, -1);  // k_resolve reads the pool's final state and depth words
         HIPCHECK(mfx_wf_resolve(P, c->stream));
     }
     if (!own_events) {
@@ -1095,6 +1163,29 @@ static void sum_counters(const unsigned long long* h, double out[16]) {
         for (int g = 0; g < WF_SHARDS; ++g) v += (double)h[WF_NCTR * g + k];
         out[k] += v;
     }
+    for (int d = 1; d < WF_ITER_CTRS; ++d)  // k_extend's per-iteration extension-ray counters
+        for (int g = 0; g < WF_SHARDS; ++g) out[1] += (double)h[WF_NCTR * g + WF_CTR_ITER + d];
+}
+
+// MFX_RAY_QUEUE: the share of a trace's paths still live after each iteration (its extension rays
+// over its paths), from counters read back after the trace; wf_trace moves the paths to ray queues
+// from the first iteration that leaves fewer than WF_QUEUE_LIVE of them (the later bounces are the
+// sparse ones). The decision only moves data: images are the same either way.
+#define WF_QUEUE_LIVE 0.35
+static void note_live(mfx_ctx* c, const unsigned long long* h) {
+    double paths = 0, it[WF_ITER_CTRS] = {0};
+    for (int g = 0; g < WF_SHARDS; ++g) {
+        paths += (double)h[WF_NCTR * g + 0];
+        for (int d = 1; d < WF_ITER_CTRS; ++d) it[d] += (double)h[WF_NCTR * g + WF_CTR_ITER + d];
+    }
+    if (paths <= 0 || it[1] <= 0) return;  // no wavefront trace (megakernel), or no path went on
+    int from = -1;
+    for (int d = 0; d + 1 < WF_ITER_CTRS && d < c->host.max_depth; ++d)
+        if (it[d + 1] / paths < WF_QUEUE_LIVE) {
+            from = d;
+            break;
+        }
+    c->wf_queue_auto = from;
 }
 
 int mfx_ray_counts(mfx_ctx* c, double out[16]) {
@@ -1110,6 +1201,7 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
         HIPCHECK(hipMemcpyAsync(h, d->d_counters, sizeof(h), hipMemcpyDeviceToHost, d->stream));
         HIPCHECK(hipStreamSynchronize(d->stream));
         sum_counters(h, out);
+        note_live(d, h);
     }
     out[3] = out[0];  // paths == primary rays
     return MFX_OK;
@@ -1255,6 +1347,7 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
                                 hipMemcpyDeviceToHost, c->copy_stream));
         HIPCHECK(hipStreamSynchronize(c->copy_stream));
         sum_counters(c->h_counters, c->rep_counts);
+        note_live(c, c->h_counters);
         c->rep_counts[3] = c->rep_counts[0];
         float f = 0.f;
         HIPCHECK(hipEventElapsedTime(&f, X.t0, X.t1));

@@ -51,11 +51,20 @@
 #ifndef WF_LOOKAHEAD
 #define WF_LOOKAHEAD 4  // windows whose state words a scan loads in one round
 #endif
-#define WF_NCTR 24  // counters per shard: [0..2] rays, [4..9] traversal statistics, [10..17] diagnostics
+#define WF_NCTR 24  // counters per shard: [0..2] rays, [4..9] traversal statistics, [10..17] diagnostics,
+                    // [WF_CTR_ITER + d] extension rays of iteration d (1 <= d < WF_ITER_CTRS; [1]
+                    // holds the others, and the host's sums add these into it)
+#define WF_CTR_ITER 18
+#define WF_ITER_CTRS 6
 // control words (unsigned long long) in WfParams.ctl
 #define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
 #define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
 #define WF_NCTL (2 * WF_SHARDS)
+// the ray queues' shard counts sit on either side of the heads, so one memset per iteration clears
+// the heads and the next queue's counts: [WF_CTL_Q0 | heads | WF_CTL_Q1], P.ctl = the heads
+#define WF_CTL_Q0 (-WF_SHARDS)
+#define WF_CTL_Q1 (WF_NCTL)
+#define WF_CTL_ALLOC (WF_NCTL + 2 * WF_SHARDS)
 
 // A vertex record's material: 16 bits (k_resolve reads every vertex level's array nearly whole, so
 // its bytes are the kernel's cost); scenes are limited to 65,536 materials (mfx_create checks).
@@ -99,6 +108,20 @@ struct WfParams {
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)
     int32_t* state;
+    // Ray queues (MFX_RAY_QUEUE; null: every iteration works on the slot pool in place). From the
+    // second iteration on, the arrays above are a queue's: entry i holds a continuing path's ray,
+    // key, draw count, depth word and state, and qslot[i] names its slot, which keeps the path's
+    // vertex records (vei, vmat, vls) and its final state and depth word (fstate, fdepth: what
+    // k_resolve reads). k_shadow appends the paths that continue to the next queue (n*), so the
+    // sparse later bounces read and write dense memory instead of scattered slots.
+    const int32_t* qslot;             // entry -> slot (null: entry = slot, the pool itself)
+    const unsigned long long* qcount; // [WF_SHARDS] entries of each shard range of this iteration's queue (null: the pool)
+    int32_t *fstate, *fdepth;         // the slot pool's state / depth words (== state / depth in place)
+    double *nox, *noy, *noz, *ndx, *ndy, *ndz;  // the next queue (null: continue in place)
+    uint64_t* nkey;
+    uint32_t* nrn;
+    int32_t *ndepth, *nstate, *nslot;
+    unsigned long long* ncount;       // [WF_SHARDS] its counts (beside ctl; zeroed with the heads)
     // control
     unsigned long long* ctl;              // [WF_NCTL]
     unsigned long long* counters;         // [WF_SHARDS][WF_NCTR] ray / traversal counters
@@ -120,12 +143,19 @@ struct WfParams {
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
     int32_t cam_grid;                     // > 0: a generation's camera rays run k_camera (packets) on this grid
+    int32_t iter;                         // the iteration (0 = camera rays); k_extend counts its rays per iteration
 };
 
+#ifndef MFX_RAY_QUEUE
+#define MFX_RAY_QUEUE 1  // continuing paths move to dense ray queues after the first vertex (MFX_RAY_QUEUE=0 at run time: in place)
+#endif
 // 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
-// and the material (4 B)
-#define WF_DOUBLES_PER_SLOT(nvert) (7 + 3 * (nvert))
-#define WF_WORDS_PER_SLOT(nvert) (3 + (nvert))  // rn, depth, state + the vertices' materials
+// and the material (4 B); with ray queues, two queues of o, d, key (8 B) and rn, depth, state,
+// slot (4 B) per slot
+// (queue 0 its own o, d, key, rn, depth, state, slot; queue 1 reuses the pool's o, d, key and rn,
+// dead after the pool's last iteration, plus its own depth, state and slot)
+#define WF_DOUBLES_PER_SLOT(nvert) (7 + 3 * (nvert) + (MFX_RAY_QUEUE ? 7 : 0))
+#define WF_WORDS_PER_SLOT(nvert) (3 + (nvert) + (MFX_RAY_QUEUE ? 7 : 0))  // rn, depth, state + the vertices' materials
 
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)
@@ -141,6 +171,14 @@ struct WfParams {
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu);
 // resident blocks per CU of k_camera (camera-ray packets)
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu);
+// a ray queue's arrays (MFX_RAY_QUEUE): entries in the pool's shard ranges, counts per shard
+struct WfQueue {
+    double *ox, *oy, *oz, *dx, *dy, *dz;
+    uint64_t* key;
+    uint32_t* rn;
+    int32_t *depth, *state, *slot;
+    unsigned long long* count;  // [WF_SHARDS]
+};
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels (ev may be null)
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);

@@ -113,10 +113,11 @@ static_assert(WF_SHARDS == 64, "shard masks are one bit per lane of a wave");
 // stale value can only report a closed shard as open: the caller's atomic then fails and it asks
 // again. This replaces walking the shards with one returning atomic each, which cost every wave
 // up to 64 serialized round trips at the end of each kernel.
-__device__ __forceinline__ uint64_t open_shards(const unsigned long long* ctr, int64_t cap) {
+__device__ __forceinline__ uint64_t open_shards(const unsigned long long* ctr, int cap) {
     const unsigned long long v = __hip_atomic_load(ctr + lane_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return __ballot((int64_t)v < cap);
+    return __ballot((int64_t)v < (int64_t)cap);
 }
+
 // the first open shard at or after `home` (cyclically); `open` must be non-zero
 __device__ __forceinline__ int next_open(uint64_t open, int home) {
     const uint64_t r = home ? ((open >> home) | (open << (64 - home))) : open;
@@ -134,21 +135,24 @@ struct Scanner {
     int nbuf;
     // Make [win_next, win_end) non-empty; false once every chunk has been taken. A wave takes
     // chunks from its block's home shard while it lasts, then from the next open shard.
+    // qcount: a ray queue's per-shard entry counts (MFX_RAY_QUEUE: a queue fills shard g's range from
+    // its start); null: whole shards
     __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
-                                           const int32_t* __restrict__ state) {
+                                           const int32_t* __restrict__ state, const unsigned long long* qcount) {
         if (win_next < win_end) return true;
         if (exhausted) return false;
         while (true) {
             unsigned long long c = 0;
             if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
             c = __shfl(c, 0);
-            if ((int64_t)c < shard_size) {
+            const int cap = qcount ? (int)qcount[shard] : shard_size;
+            if ((int64_t)c < cap) {
                 win_next = shard * shard_size + (int)c;
-                win_end = shard * shard_size + min((int)c + chunk, shard_size);
+                win_end = shard * shard_size + min((int)c + chunk, cap);
                 fill(state);
                 return true;
             }
-            const uint64_t open = open_shards(heads, shard_size);
+            const uint64_t open = open_shards(heads, qcount ? (int)qcount[lane_id()] : shard_size);
             if (open == 0) {
                 exhausted = true;
                 return false;
@@ -328,12 +332,15 @@ __device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x,
 #define WF_EXT_PEND 128  // k_extend per-wave pending list: slot indices (sign bit: camera ray)
 #define WF_SHD_LIST 128  // k_shadow per-wave shade list entries
 
-// Per-wave LDS list of k_shadow's pending shadow rays: slot index, a flag word and 6 doubles
-// (direction, tmax, the direct term's operands cs and solid), each field a 64-entry column
-// (conflict-free).
+__device__ __forceinline__ bool cont0(int vflag) { return (vflag & 1) != 0; }  // k_shadow: the path continues
+
+// Per-wave LDS list of k_shadow's pending shadow rays: ray index, a flag word, the path's slot and
+// its next-queue entry (MFX_RAY_QUEUE) and 6 doubles (direction, tmax, the direct term's operands
+// cs and solid), each field a 64-entry column (conflict-free).
 struct PendShd {
     static constexpr int BYTES = 64 * (4 + 4 + 8 * 6);
-    int* slot;
+    int* slot;  // the shadow ray's origin, the hit point: its index in the ray arrays, or (a path
+                // that continues into the next queue, MFX_RAY_QUEUE) its entry there
     int* flag;
     double* v;  // v[f * 64 + entry]
     __device__ __forceinline__ PendShd(uint8_t* base) {
@@ -430,7 +437,9 @@ __device__ __forceinline__ DV hemisphere_ball_wave(bool own, DV nm, uint64_t key
 // ------------------------------------------------------------------------------------------------
 // k_extend: closest hit for NEED_EXT slots; in a generation's first iteration FREE slots start paths
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool SPILL, bool INST>
+// Q: the instance for the iterations on ray queues (MFX_RAY_QUEUE; P.qcount); the in-place one
+// has none of their code
+template <bool STATS, bool SPILL, bool INST, bool Q>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
@@ -469,7 +478,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 // list at least 64 slots to trace (or all that are left) from as many windows as it
                 // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -573,7 +582,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     }
     unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 0, c_primary, red);
-    block_add<4>(cnt + 1, c_ext, red);
+    // extension rays: per iteration where it has a counter (the paths that went on; the host adds
+    // them into counter 1)
+    block_add<4>(cnt + (P.iter > 0 && P.iter < WF_ITER_CTRS ? WF_CTR_ITER + P.iter : 1), c_ext, red);
     if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
         atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
@@ -617,7 +628,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
-    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state)) {
+    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr)) {
         const int j = sc.win_next + lane;
         const int sj = sc.word();
         sc.advance(P.state);
@@ -664,7 +675,8 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
-template <bool STATS, bool SPILL, int WAVES, bool INST>
+// Q: the instance that reads a ray queue (P.qslot) or writes the next one (P.ncount), MFX_RAY_QUEUE
+template <bool STATS, bool SPILL, int WAVES, bool INST, bool Q>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
@@ -710,14 +722,26 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state)) {
+                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
                     const int sv = sj & WF_STATE_MASK;
                     const bool hit = (sv & ~WF_FRESH) == WF_HIT;
-                    if (sv == (WF_MISS | WF_FRESH)) P.state[j] = WF_FREE;
-                    else if (sv == WF_MISS) P.state[j] = WF_DONE;
+                    if (sv == (WF_MISS | WF_FRESH)) {
+                        P.state[j] = WF_FREE;
+                    } else if (sv == WF_MISS) {
+                        if (Q && P.qslot) {  // a queue entry: its slot finishes (a path with no lit vertex stays unfinished)
+                            const int dw = P.depth[j];
+                            if (dw >> WF_LIT_SHIFT) {
+                                const int jr = P.qslot[j];
+                                P.fdepth[jr] = dw;
+                                P.fstate[jr] = WF_DONE;
+                            }
+                        } else {
+                            P.state[j] = WF_DONE;
+                        }
+                    }
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
@@ -734,7 +758,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 //      (Integrators.fs:109-136) each; every one yields a shadow ray ----
                 const int cnt = nshade < 64 ? nshade : 64;
                 const bool own = lane < cnt;
-                int j = 0, mat = 0;
+                int j = 0, mat = 0, jr = 0, dw = 0;
                 bool first = false;
                 DV hp = dv(0, 0, 0), nm = dv(0, 0, 0);
                 uint64_t key = 0;
@@ -743,6 +767,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     j = shl[lane] & 0x7fffffff;
                     first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
                     const int slot = shl[WF_SHD_LIST + lane];
+                    jr = (Q && P.qslot) ? P.qslot[j] : j;
+                    dw = first ? P.max_depth : P.depth[j];  // remaining depth | lit mask << 8
                     hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
@@ -762,6 +788,24 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     key = P.key[j];
 #endif
                     rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
+                }
+                // the depth -1 query's result is discarded (Integrators.fs:109): never traced
+                const bool cn = own && (dw & 0xff) - 1 >= 0;
+                // MFX_RAY_QUEUE: a continuing path's entry in the next queue, in the range of its
+                // source shard (capacity: that shard's size), one atomic per shard in the batch
+                int qi = 0;
+                if (Q && P.ncount) {
+                    const int g = cn ? j / shard_size : 0;
+                    uint64_t rem = __ballot(cn);
+                    while (rem) {
+                        const int gl = __shfl(g, __builtin_ctzll(rem));
+                        const uint64_t gm = __ballot(cn && g == gl);
+                        unsigned long long base = 0;
+                        if (lane == __builtin_ctzll(gm)) base = atomicAdd(P.ncount + gl, (unsigned long long)__popcll(gm));
+                        base = __shfl(base, __builtin_ctzll(gm));
+                        if (cn && g == gl) qi = gl * shard_size + (int)base + __popcll(gm & lanes_below());
+                        rem &= ~gm;
+                    }
                 }
                 // LambertianBrdf.SampleF — Material.fs:33-36; GetRandomInUnitSphere :9-14
 #if MFX_HEMI_WAVE && !defined(MFX_DIAG_ONE_TRIAL)
@@ -800,18 +844,22 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const double dist2 = toLight.x * toLight.x + toLight.y * toLight.y + toLight.z * toLight.z;
                     const double solid = fabs(cos_o) * LT.area / dist2;
                     const double cs = vdot(unit, nm);
-                    const int dw = first ? P.max_depth : P.depth[j];  // remaining depth | lit mask << 8
                     const int v = P.max_depth - (dw & 0xff);          // this vertex's index
                     // the operands of col = INVPI * a * ei * TwoPi (Material.fs:36), c_v (k_resolve)
-                    P.vei[v * P.vstride + j] = ei;
-                    P.vmat[v * P.vstride + j] = (WfMat)mat;
+                    P.vei[v * P.vstride + jr] = ei;
+                    P.vmat[v * P.vstride + jr] = (WfMat)mat;
                     // l / pdf_li with l = (unit . n) * L(hit, toLight) (Integrators.fs:52, Light.fs:48-56)
                     // is the vertex's a_v if the shadow ray is unoccluded; L is black for cos_o >= 0.
                     // Its operands cs and solid travel with the shadow ray.
                     const bool lightable = cos_o < 0.;
-                    // the depth -1 query's result is discarded (Integrators.fs:109): never traced
-                    const bool cn = (dw & 0xff) - 1 >= 0;
-                    if (cn) {  // what the next vertex reads (its depth word is written after the shadow ray)
+                    if (Q && cn && P.ncount) {  // the next vertex's ray in the next queue (its depth word and
+                                           // state are written after the shadow ray)
+                        P.nox[qi] = hp.x; P.noy[qi] = hp.y; P.noz[qi] = hp.z;
+                        P.ndx[qi] = wi.x; P.ndy[qi] = wi.y; P.ndz[qi] = wi.z;
+                        P.nkey[qi] = key;
+                        P.nrn[qi] = rn;
+                        P.nslot[qi] = jr;
+                    } else if (cn) {  // what the next vertex reads, in place
 #if MFX_KEY_RECOMPUTE
                         if (first) P.key[j] = key;
 #endif
@@ -819,7 +867,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                         P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
                     }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
-                    pd.slot[lane] = j;
+                    pd.slot[lane] = (Q && cn && P.ncount) ? qi : j;
                     // bits 24..26: the next ray's direction octant (MFX_OCTANT_SORT)
                     const int oct = (wi.x < 0. ? 1 : 0) | (wi.y < 0. ? 2 : 0) | (wi.z < 0. ? 4 : 0);
                     pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff) | (oct << 24);
@@ -848,9 +896,15 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 s = pd.slot[e];
                 vflag = pd.flag[e];
                 scs = pd.v[4 * 64 + e]; ssolid = pd.v[5 * 64 + e];
-                // origin = the hit point k_extend stored (a cache hit: the shading just read it)
-                trav_begin(T, S, dv(P.ox[s], P.oy[s], P.oz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
+                // origin = the hit point k_extend stored (a cache hit: the shading just read it), or
+                // its copy in the next queue
+                const bool nq = Q && (vflag & 1) && P.ncount;
+                const double* hx = nq ? P.nox : P.ox;
+                const double* hy = nq ? P.noy : P.oy;
+                const double* hz = nq ? P.noz : P.oz;
+                trav_begin(T, S, dv(hx[s], hy[s], hz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            pd.v[3 * 64 + e]);
+
 #ifdef MFX_DIAG_OCCLUSION
                 T.n0 = st.nodes;
                 T.l0 = st.clusters;
@@ -885,8 +939,12 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
 #endif
             const int v = (vflag >> 2) & 15;
             int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
+            // MFX_RAY_QUEUE: s is the path's next-queue entry (it continues) or its entry in this
+            // iteration's queue; its slot is read back where the slot's records are written
+            const bool nq = Q && cont0(vflag) && P.ncount;
             if (!T.B.found && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
-                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + s;
+                const int jr = nq ? P.nslot[s] : ((Q && P.qslot) ? P.qslot[s] : s);
+                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + jr;
                 vl[0] = scs;
                 vl[P.vstride] = ssolid;
                 mask |= 1 << v;
@@ -894,8 +952,21 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             const bool cont = (vflag & 1) != 0;
             // continue with the next vertex's remaining depth; or finished: k_resolve folds the
             // recorded vertices (none lit: nothing to add, FREE)
-            if (cont || mask) P.depth[s] = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-            P.state[s] = cont ? (WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT)) : (mask ? WF_DONE : WF_FREE);
+            const int dwn = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
+            const int need = WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT);
+            if (nq) {
+                P.ndepth[s] = dwn;
+                P.nstate[s] = need;
+            } else if (Q && (P.ncount || P.qslot)) {  // finished; the pool's slot keeps its final words
+                if (mask) {
+                    const int jr = P.qslot ? P.qslot[s] : s;
+                    P.fdepth[jr] = dwn;
+                    P.fstate[jr] = WF_DONE;
+                }
+            } else {
+                if (cont || mask) P.depth[s] = dwn;
+                P.state[s] = cont ? need : (mask ? WF_DONE : WF_FREE);
+            }
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
@@ -1102,29 +1173,39 @@ hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int n
     const size_t lds = wf_lds_bytes(stack_lds, shadow, ntop, std::min(ninst, WF_INST_LDS));
     const void* k;
     if (shadow)
-        k = inst ? (spill ? (const void*)k_shadow<false, true, 4, true> : (const void*)k_shadow<false, false, 4, true>)
-                 : (spill ? (const void*)k_shadow<false, true, 4, false> : (const void*)k_shadow<false, false, 4, false>);
+        k = inst ? (spill ? (const void*)k_shadow<false, true, 4, true, false> : (const void*)k_shadow<false, false, 4, true, false>)
+                 : (spill ? (const void*)k_shadow<false, true, 4, false, false> : (const void*)k_shadow<false, false, 4, false, false>);
     else
-        k = inst ? (spill ? (const void*)k_extend<false, true, true> : (const void*)k_extend<false, false, true>)
-                 : (spill ? (const void*)k_extend<false, true, false> : (const void*)k_extend<false, false, false>);
+        k = inst ? (spill ? (const void*)k_extend<false, true, true, false> : (const void*)k_extend<false, false, true, false>)
+                 : (spill ? (const void*)k_extend<false, true, false, false> : (const void*)k_extend<false, false, false, false>);
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds);
     *blocks_per_cu = std::min(*blocks_per_cu, wf_lds_blocks(lds));
     return e;
 }
 
+template <bool SPILL, bool INST, bool Q>
+static void launch_extend_q(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
+    if (stats)
+        hipLaunchKernelGGL((k_extend<true, SPILL, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+    else
+        hipLaunchKernelGGL((k_extend<false, SPILL, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+}
 template <bool SPILL, bool INST>
 static void launch_extend(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
+    if (P.qcount) launch_extend_q<SPILL, INST, true>(P, grid, stats, st, lds);
+    else launch_extend_q<SPILL, INST, false>(P, grid, stats, st, lds);
+}
+template <bool SPILL, int WAVES, bool INST, bool Q>
+static void launch_shadow_q(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (stats)
-        hipLaunchKernelGGL((k_extend<true, SPILL, INST>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST, Q>), dim3(grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_extend<false, SPILL, INST>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST, Q>), dim3(grid), dim3(256), lds, st, P);
 }
 template <bool SPILL, int WAVES, bool INST>
 static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
-    if (stats)
-        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
-    else
-        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
+    if (P.qslot || P.ncount) launch_shadow_q<SPILL, WAVES, INST, true>(P, grid, stats, st, lds);
+    else launch_shadow_q<SPILL, WAVES, INST, false>(P, grid, stats, st, lds);
 }
 
 static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64; }
@@ -1165,7 +1246,14 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     const int ni = P.inst ? P.ninst_lds : 0;
     const size_t lds_e = wf_lds_bytes(P.stack_lds_ext, false, P.ntop_ext, ni);
     const size_t lds_s = wf_lds_bytes(P.stack_lds_shd, true, P.ntop_shd, ni);
-    hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
+    // the chunk heads and, beside them (WF_CTL_Q0 / WF_CTL_Q1), the next queue's shard counts
+    unsigned long long* z = P.ctl;
+    size_t nz = WF_NCTL;
+    if (P.ncount) {
+        nz += WF_SHARDS;
+        if (P.ncount < P.ctl) z = P.ncount;
+    }
+    hipError_t e = hipMemsetAsync(z, 0, nz * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     e = P.inst ? launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s)
                : launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s);

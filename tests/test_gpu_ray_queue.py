@@ -1,0 +1,69 @@
+"""Ray queues (MFX_RAY_QUEUE): from the iteration MFX_QUEUE_FROM on, k_shadow moves the
+paths that continue into dense queues, and the later iterations read and write those instead of
+the scattered slots. The choice only moves data, so every mode must give the oracle's image bit for
+bit with the same ray counts: in place (-1), queues from the first vertex (0) or the second (1, 2),
+automatic (-2: the live share per iteration of the previous trace decides), small chunks, odd
+films, max_depth 5 (three queue hand-overs, both queues reused), two-level instancing, several
+generations (a small pool), and the render-ahead planes."""
+import os
+
+import numpy as np
+import pytest
+
+from conftest import SEED, scene
+
+pytestmark = pytest.mark.gpu
+
+MODES = ["-1", "0", "1", "2", "-2"]
+
+
+def _ctx(a, env, **kw):
+    from mafrixraytracing_amd.native import NativeContext
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:  # the library reads these at context creation
+        return NativeContext(a, seed=SEED, **kw)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                del os.environ[k]
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth", [
+    ("spot", 67, 45, 6, 3), ("cube_cornell", 40, 32, 4, 3), ("renault", 48, 40, 3, 3),
+    ("spot16_instanced@2l", 56, 40, 3, 3), ("cornell", 33, 31, 3, 5), ("two_spheres_plane", 32, 32, 4, 4)])
+def test_queue_modes_match_oracle(gpu, oracle, name, w, h, spp, depth):
+    a = scene(name, w, h, max_depth=depth)
+    o = oracle.OracleScene(a)
+    # Sample(n) keeps the sample stream running: the second call renders samples n .. 2n - 1
+    refs = [o.sample(spp, SEED, sample_base=k * spp, with_stats=True) for k in range(2)]
+    for mode in MODES:
+        for chunk in ("256", "64"):
+            with _ctx(a, {"MFX_QUEUE_FROM": mode, "MFX_QCHUNK": chunk}) as ctx:
+                for k, (ref, st) in enumerate(refs):  # the second call: the automatic mode has the first one's counts
+                    img = ctx.sample(spp)
+                    c = ctx.ray_counts()
+                    assert (c[0], c[1], c[2]) == (st[0], st[1], st[2]), (mode, chunk, k, c[:3], st[:3])
+                    assert np.array_equal(img, ref), (mode, chunk, k, np.abs(img - ref).max())
+
+
+def test_queue_modes_over_generations(gpu, oracle):
+    """A pool of 4096 slots: the frame runs in many generations, each with its own queues."""
+    a = scene("spot", 64, 48, max_depth=3)
+    ref = oracle.OracleScene(a).sample(5, SEED)
+    for mode in ("-1", "0", "1"):
+        with _ctx(a, {"MFX_QUEUE_FROM": mode, "MFX_POOL": "4096"}) as ctx:
+            assert np.array_equal(ctx.sample(5), ref), mode
+
+
+def test_queue_render_ahead_frames(gpu):
+    """Render-ahead batches (planes written by k_resolve) with queues equal the in-place frames."""
+    a = scene("spot", 48, 32)
+    frames = {}
+    for mode in ("-1", "1"):
+        with _ctx(a, {"MFX_QUEUE_FROM": mode}, render_ahead=8) as ctx:
+            frames[mode] = [ctx.render_rgba8(1).copy() for _ in range(10)]
+    for x, y in zip(frames["-1"], frames["1"]):
+        assert np.array_equal(x, y)
