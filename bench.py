@@ -459,35 +459,47 @@ def main():
             def td_roofline(kname, kms, launches):
                 """The bound these kernels sit under: vector-memory line requests. achieved = the PMC
                 pass's TCP line lookups per launch over this run's HIP-event launch time; peak = the
-                td_gather peak case's lookups per GPU clock x the clock the PMC pass ran at."""
+                td_gather peak case's lookups per GPU clock x the clock the PMC pass ran at. A kernel's
+                instances (in place / ray queues, MFX_RAY_QUEUE) are pooled: per launch = their sums over
+                their launches, as the HIP-event average pools them."""
                 if not tdroof:
                     return None
                 base = kname.split("<")[0]
-                for kk, kv in tdroof["kernels"].items():
-                    if kk.split("<")[0] == base:
-                        lines = kv["line_lookups_per_launch"]
-                        ach = lines / (kms / launches / 1e3) / 1e9
-                        peak = tdroof["peak"]["lines_per_clock"] * kv["clock_mhz"] * 1e6 / 1e9
-                        return {"bound": "td", "achieved": round(ach, 2), "peak": round(peak, 2),
-                                "unit": "G line-lookups/s", "frac": round(ach / peak, 4),
-                                "frac_pmc_pass": round(kv["frac_of_peak"], 4),
-                                "td_busy_frac": round(kv["td_busy_frac"], 4),
-                                "td_busy_frac_peak_case": round(tdroof["peak"]["td_busy_frac"], 4),
-                                "lines_per_launch": lines, "l2_reads_per_launch": kv["l2_reads_per_launch"],
-                                "clock_mhz_pmc_pass": round(kv["clock_mhz"], 1),
-                                "peak_case": tdroof["peak"]["case"],
-                                "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
-                return None
+                ks = [kv for kk, kv in tdroof["kernels"].items() if kk.split("<")[0] == base]
+                if not ks:
+                    return None
+                n = sum(kv.get("launches", 1.0) for kv in ks)
+                tot = lambda f: sum(kv[f] * kv.get("launches", 1.0) for kv in ks)
+                lines = tot("line_lookups_per_launch") / n
+                clocks = tot("gpu_clocks_per_launch") if all("gpu_clocks_per_launch" in kv for kv in ks) else None
+                ms = tot("ms_per_launch") if all("ms_per_launch" in kv for kv in ks) else None
+                mhz = clocks / ms / 1e3 if clocks and ms else ks[0]["clock_mhz"]
+                busy = tot("td_busy_per_launch") / clocks if clocks and all("td_busy_per_launch" in kv for kv in ks) \
+                    else ks[0]["td_busy_frac"]
+                ach = lines / (kms / launches / 1e3) / 1e9
+                peak = tdroof["peak"]["lines_per_clock"] * mhz * 1e6 / 1e9
+                pass_frac = (lines * n / clocks) / tdroof["peak"]["lines_per_clock"] if clocks else ks[0]["frac_of_peak"]
+                return {"bound": "td", "achieved": round(ach, 2), "peak": round(peak, 2),
+                        "unit": "G line-lookups/s", "frac": round(ach / peak, 4),
+                        "frac_pmc_pass": round(pass_frac, 4),
+                        "td_busy_frac": round(busy, 4),
+                        "td_busy_frac_peak_case": round(tdroof["peak"]["td_busy_frac"], 4),
+                        "lines_per_launch": lines, "l2_reads_per_launch": tot("l2_reads_per_launch") / n,
+                        "clock_mhz_pmc_pass": round(mhz, 1), "instances": len(ks),
+                        "peak_case": tdroof["peak"]["case"],
+                        "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
 
             def kernel_roofline(kname, kms, krays, launches, bray):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
                 achieved = krays * bray / (kms / 1e3) / 1e9
                 traffic = None
-                if tdata:  # rocprof names the instance: k_shadow<false> or k_shadow<false, SPILL>
+                if tdata:  # rocprof names the instance: k_shadow<false> or k_shadow<false, SPILL, ...>;
+                    # the instances' bytes pooled over their launches (in place / ray queues)
                     base = kname.split(">")[0]
-                    for kk, kv in tdata.get("kernels", {}).items():
-                        if kk == kname or kk.startswith(base + ","):
-                            traffic = kv.get("hbm_bytes_per_launch")
+                    ks = [kv for kk, kv in tdata.get("kernels", {}).items() if kk == kname or kk.startswith(base + ",")]
+                    nl = sum(kv.get("launches_profiled", 1) for kv in ks)
+                    if ks and nl:
+                        traffic = sum(kv.get("hbm_bytes_per_launch", 0.0) * kv.get("launches_profiled", 1) for kv in ks) / nl
                 return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                         "td": td_roofline(kname, kms, launches),
