@@ -474,8 +474,9 @@ def main():
                 clocks = tot("gpu_clocks_per_launch") if all("gpu_clocks_per_launch" in kv for kv in ks) else None
                 ms = tot("ms_per_launch") if all("ms_per_launch" in kv for kv in ks) else None
                 mhz = clocks / ms / 1e3 if clocks and ms else ks[0]["clock_mhz"]
-                busy = tot("td_busy_per_launch") / clocks if clocks and all("td_busy_per_launch" in kv for kv in ks) \
-                    else ks[0]["td_busy_frac"]
+                # busy share of the TDs, weighted by each instance's clocks
+                busy = sum(kv["td_busy_frac"] * kv["gpu_clocks_per_launch"] * kv.get("launches", 1.0) for kv in ks) / clocks \
+                    if clocks else ks[0]["td_busy_frac"]
                 ach = lines / (kms / launches / 1e3) / 1e9
                 peak = tdroof["peak"]["lines_per_clock"] * mhz * 1e6 / 1e9
                 pass_frac = (lines * n / clocks) / tdroof["peak"]["lines_per_clock"] if clocks else ks[0]["frac_of_peak"]
