@@ -67,3 +67,14 @@ def test_queue_render_ahead_frames(gpu):
             frames[mode] = [ctx.render_rgba8(1).copy() for _ in range(10)]
     for x, y in zip(frames["-1"], frames["1"]):
         assert np.array_equal(x, y)
+
+
+def test_queue_pool_growth(gpu, oracle):
+    """A context whose pool grows between calls (2 spp, then 7 spp of a larger share) re-points
+    its queues at the new pool: both calls equal the oracle."""
+    a = scene("spot", 40, 24)
+    o = oracle.OracleScene(a)
+    with _ctx(a, {"MFX_QUEUE_FROM": "1"}) as ctx:
+        assert np.array_equal(ctx.sample(2), o.sample(2, SEED, sample_base=0))
+        assert np.array_equal(ctx.sample(7), o.sample(7, SEED, sample_base=2))
+        assert np.array_equal(ctx.sample(2), o.sample(2, SEED, sample_base=9))
