@@ -10,7 +10,8 @@
 // in its state, so no ray queue (and no hot queue-tail atomic) exists:
 //   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
 //   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (a lit vertex recorded) or FREE (none)
-//   MISS -(k_shadow)-> DONE, or FREE for a camera ray's miss
+//   MISS stays: a finished path (its depth word holds the lit vertices; k_resolve folds it), black
+//   for a camera ray's MISS | FRESH (MFX_MISS_IN_PLACE; else k_shadow rewrites it DONE / FREE)
 // A path's radiance is not summed forward. Each vertex v records the operands of its BRDF factor
 // c_v = col (the cosine ei and the material) and, when its shadow ray reaches the light, those of
 // its direct term a_v = l / pdf_li (the cosine cs and the solid-angle factor), and k_resolve

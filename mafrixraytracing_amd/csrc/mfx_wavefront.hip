@@ -39,6 +39,10 @@
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 
+#ifndef MFX_MISS_IN_PLACE
+#define MFX_MISS_IN_PLACE 1  // k_shadow leaves the pool's MISS words as they are; k_resolve reads them
+#endif
+
 #ifndef MFX_SHADOW_ORDER
 #define MFX_SHADOW_ORDER 1  // shadow rays' child order: 0 near-first, 1 far-first (by exit distance)
 #endif
@@ -728,6 +732,18 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const int sj = sc.word();
                     const int sv = sj & WF_STATE_MASK;
                     const bool hit = (sv & ~WF_FRESH) == WF_HIT;
+#if MFX_MISS_IN_PLACE
+                    // a pool slot's miss stays as k_extend wrote it: k_resolve takes MISS as finished
+                    // (its depth word holds the lit vertices) and a camera ray's MISS | FRESH as black
+                    if (Q && P.qslot && sv == WF_MISS) {  // a queue entry: its slot finishes (no lit vertex: stays unfinished)
+                        const int dw = P.depth[j];
+                        if (dw >> WF_LIT_SHIFT) {
+                            const int jr = P.qslot[j];
+                            P.fdepth[jr] = dw;
+                            P.fstate[jr] = WF_DONE;
+                        }
+                    }
+#else
                     if (sv == (WF_MISS | WF_FRESH)) {
                         P.state[j] = WF_FREE;
                     } else if (sv == WF_MISS) {
@@ -742,6 +758,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                             P.state[j] = WF_DONE;
                         }
                     }
+#endif
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
@@ -1121,7 +1138,8 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         int mask[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            mask[u] = (sw[u] & WF_STATE_MASK) == WF_DONE ? (P.depth[jv[u]] >> WF_LIT_SHIFT) & 0xffff : 0;
+            mask[u] = ((sw[u] & WF_STATE_MASK) == WF_DONE || (MFX_MISS_IN_PLACE && (sw[u] & WF_STATE_MASK) == WF_MISS))
+                          ? (P.depth[jv[u]] >> WF_LIT_SHIFT) & 0xffff : 0;
         PathRec R[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) load_path(P, jv[u], mask[u], R[u]);
