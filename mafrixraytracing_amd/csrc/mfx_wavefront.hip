@@ -357,7 +357,7 @@ struct PendShd {
 #ifndef MFX_KEY_RECOMPUTE
 // k_shadow derives a camera ray's path key from its slot (as k_extend did) instead of reading it:
 // k_extend stores no keys, and only continuing paths get theirs stored, at their first vertex
-#define MFX_KEY_RECOMPUTE 1  // r02bs: C2 +0.9 to +2.5 %, C3 +2.5 to +4.3 %, C4 +0.5 to +0.8 %
+#define MFX_KEY_RECOMPUTE 1  // r02bs: C2 +0.9 to +2.5 %, C3 +2.5 to +4.3 %, C4 +0.5 to +0.8 %; 2 (every vertex) r03av: -0.3 to -1.2 %
 #endif
 #ifndef MFX_HEMI_WAVE
 #define MFX_HEMI_WAVE 1  // k_shadow: the rejection sampler's stragglers' trials spread over the whole wave
@@ -792,10 +792,12 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     else nm = ld3(sh.n);
                     mat = sh.material;
 #if MFX_KEY_RECOMPUTE
-                    if (first) {  // the key k_extend derived for this camera ray (same expressions)
+                    // the key k_extend derived for the path's camera ray (same expressions): at the
+                    // first vertex (MFX_KEY_RECOMPUTE 1) or at every one (2: keys are never stored)
+                    if (first || MFX_KEY_RECOMPUTE == 2) {
                         int x, y;
                         int64_t smp;
-                        path_pixel(P, P.path_base + j, x, y, smp);
+                        path_pixel(P, P.path_base + jr, x, y, smp);
                         const int64_t pixel = (int64_t)x * P.height + y;
                         key = path_key(P.seed, (uint64_t)pixel, (uint64_t)(P.sample_base + P.part_index + smp * P.part_count));
                     } else {
@@ -873,11 +875,11 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                                            // state are written after the shadow ray)
                         P.nox[qi] = hp.x; P.noy[qi] = hp.y; P.noz[qi] = hp.z;
                         P.ndx[qi] = wi.x; P.ndy[qi] = wi.y; P.ndz[qi] = wi.z;
-                        P.nkey[qi] = key;
+                        if (MFX_KEY_RECOMPUTE != 2) P.nkey[qi] = key;
                         P.nrn[qi] = rn;
                         P.nslot[qi] = jr;
                     } else if (cn) {  // what the next vertex reads, in place
-#if MFX_KEY_RECOMPUTE
+#if MFX_KEY_RECOMPUTE == 1
                         if (first) P.key[j] = key;
 #endif
                         P.rn[j] = rn;
