@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MFX_ABI_VERSION 4
+#define MFX_ABI_VERSION 5
 #define MFX_MAX_DEVICES 64
 #define MFX_MAX_RENDER_AHEAD 1024
 
@@ -125,7 +125,8 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
                                traversal); the same world scene, hits and images */
 #define MFX_F_TWO_LEVEL 32  /* mfx_create_instanced: keep the two-level traversal. Default (neither flag):
                                flattened when the flat image fits MFX_FLATTEN_MAX_BYTES (env; default
-                               2 GiB at 512 B per traversal slot of the expansion), two-level otherwise */
+                               2 GiB at 512 B per traversal slot of the expansion) and a sixteenth of
+                               the device's free memory, two-level otherwise. Both flags: MFX_E_INVALID */
 
 /* One entry of an instanced scene (mfx_create_instanced; an extension: the reference has no
  * instancing, its scenes are flat lists). The world primitive list — the index space Bvh.Build
@@ -171,11 +172,6 @@ int mfx_instancing_info(mfx_ctx* ctx, double out[8]);
  * description (MFX_F_FLATTEN honoured), plus the traversal stack bound.                       */
 int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
                              int32_t flags, double out[8], int32_t* stack_entries);
-/* Host-only: the per-lane traversal's BVH8 of a flat scene (mfx_wide.cpp), built from its BVH4 and
- * checked (every leaf reached once, every box containing its subtree): out[0] = BVH8 nodes,
- * out[1] = its stack bound, out[2] = the BVH4's, out[3] = BVH8 depth, out[4] = BVH4 depth,
- * out[5] = the frame's scale, out[6] = mean entries per BVH8 node, out[7] = leaves.            */
-int mfx_wide_info(const mfx_scene_desc* scene, double out[8]);
 
 /* ---- the reference's render API --------------------------------------------------------- */
 
@@ -312,13 +308,6 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
  * left to the FP64 test) and the vertex-box proof's (1 proved to pass, 0 not proved). Wherever a
  * shortcut decides it must agree with the FP64 answer.                                         */
 int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out);
-
-/* Device self-test of the FP32 triangle screen the leaf test can put in front of the FP64
- * Triangle.Hit (Trangle.fs:120-155; MFX_LEAF_SCREEN32 builds): rec = n records of 18 doubles
- * (origin[3], direction[3], v0[3], e1[3], e2[3], tMin, beyond, tMax); out = 3 doubles per record:
- * the FP64 test's hit (0/1) and t, and the screen's skip (1: it claims the FP64 test misses, or hits
- * at beyond < t < tMax). A skip where the FP64 test hits at t <= beyond or t >= tMax is an error.  */
-int mfx_tri_screen_selftest(int32_t device, int64_t n, const double* rec, double* out);
 
 /* ---- misc -------------------------------------------------------------------------------- */
 const char* mfx_last_error(void);

@@ -25,7 +25,7 @@ MFX_F_FLATTEN = 16
 MFX_F_TWO_LEVEL = 32
 MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
-MFX_ABI_VERSION = 4
+MFX_ABI_VERSION = 5
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
@@ -168,8 +168,6 @@ def _bind(lib):
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
         "mfx_fp64_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp, _dp, _dp]),
         "mfx_aabb_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _ip]),
-        "mfx_tri_screen_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _dp]),
-        "mfx_wide_info": (C.c_int, [_P(MfxSceneDesc), _dp]),
         "mfx_build_leaves": (C.c_int, [_P(MfxSceneDesc), _ip, _ip, _ip, _ip, _ip]),
         "mfx_build_info": (C.c_int, [C.c_void_p, _dp, _P(C.c_uint64)]),
         "mfx_last_error": (C.c_char_p, []),
@@ -184,11 +182,11 @@ def _bind(lib):
 
 
 EXPORTED_SYMBOLS = [
-    "mfx_create", "mfx_create_instanced", "mfx_expand_instances", "mfx_instancing_info", "mfx_build_instanced_info", "mfx_wide_info", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
+    "mfx_create", "mfx_create_instanced", "mfx_expand_instances", "mfx_instancing_info", "mfx_build_instanced_info", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
     "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
-    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_tri_screen_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 
 _lib = None
@@ -272,20 +270,4 @@ def build_instanced_info(arrays: SceneArrays, flags: int = 0) -> dict:
                                        iptr(st)), "mfx_build_instanced_info")
     r = {k: int(v) for k, v in zip(INSTANCING_KEYS, out)}
     r["stack"] = int(st[0])
-    return r
-
-
-WIDE_KEYS = ("nodes", "stack", "stack4", "depth", "depth4", "scale", "mean_entries", "leaves")
-
-
-def wide_info(arrays: SceneArrays) -> dict:
-    """Host-only: the per-lane traversal's BVH8 of a flat scene, built and checked by the library
-    (mfx_wide_info; raises if an invariant fails)."""
-    lib = load_library()
-    d = arrays.desc()
-    out = np.zeros(8)
-    check(lib.mfx_wide_info(C.byref(d), dptr(out)), "mfx_wide_info")
-    r = dict(zip(WIDE_KEYS, out.tolist()))
-    for k in ("nodes", "stack", "stack4", "depth", "depth4", "leaves"):
-        r[k] = int(r[k])
     return r

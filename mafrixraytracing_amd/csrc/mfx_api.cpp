@@ -24,7 +24,6 @@
 #include "mfx_device.h"
 #include "mfx_scene.h"
 #include "mfx_wavefront.h"
-#include "mfx_wide.h"
 
 namespace {
 thread_local std::string g_err;
@@ -106,10 +105,6 @@ struct mfx_ctx {
     hipStream_t stream = nullptr;
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
-    MfxNode8H* d_wide = nullptr;    // flat scenes: the per-lane traversal's BVH8 (MFX_WIDE, mfx_wide.cpp)
-    MfxWideXf wide_xf{0, 0, 0, 1};
-    int32_t wide_nodes = 0;
-    MfxTri32* d_tri32 = nullptr;  // FP32 triangle copies of the slots (the leaf screen)
     MfxSlot* d_slots = nullptr;
     int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
@@ -197,15 +192,6 @@ struct mfx_ctx {
     hipEvent_t reduce_done = nullptr;    // repeated-device list: the primary has read every peer's buffer
 };
 
-// the nodes the per-lane traversal reads
-static const MfxTNode* tnodes_of(const mfx_ctx* c) {
-#if MFX_WIDE
-    return c->d_wide;  // null for two-level scenes, whose kernels read the BVH4
-#else
-    return c->d_nodes;
-#endif
-}
-
 // the devices of a context, primary first
 static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
     std::vector<mfx_ctx*> v{c};
@@ -238,7 +224,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
-    void* bufs[] = {c->d_nodes, c->d_wide, c->d_tri32, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
+    void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
@@ -289,38 +275,7 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
-#if MFX_WIDE
-    if (c->host.inst.empty()) {
-        MfxWideImage wi;
-        std::string e;
-        if (!mfx_build_wide(c->host.nodes, wi, e)) return fail(MFX_E_INVALID, "mfx_create: " + e);
-        c->stack_size = std::max(c->stack_size, wi.stack_entries);
-        if (c->stack_size > 96) return fail(MFX_E_INVALID, "mfx_create: BVH too deep for the LDS traversal stack");
-        c->wide_xf = wi.xf;
-        c->wide_nodes = (int32_t)wi.nodes.size();
-        CK(upload(&c->d_wide, wi.nodes));
-    }
-#endif
     CK(upload(&c->d_slots, c->host.slots));
-#if MFX_LEAF_SCREEN32
-    {  // v0, e1, e2 of every triangle slot rounded to FP32 (tri_skip32); spheres are never screened
-        std::vector<MfxTri32> t32(c->host.slots.size());
-        for (size_t i = 0; i < t32.size(); ++i) {
-            const MfxSlot& sl = c->host.slots[i];
-            MfxTri32& t = t32[i];
-            for (int k = 0; k < 3; ++k) {
-                t.v0[k] = (float)sl.a[k];
-                t.e1[k] = (float)sl.b[k];
-                t.e2[k] = (float)sl.c[k];
-            }
-            const int kind = (sl.info >> MFX_INFO_KIND_SHIFT) & 3;
-            t.flags = kind == MFX_KIND_SPHERE ? MFX_T32_NOSCREEN
-                                              : (kind == MFX_KIND_RECT && !(sl.info & MFX_INFO_RECT2) ? MFX_T32_RECT : 0);
-            t.pad[0] = t.pad[1] = 0.f;
-        }
-        CK(upload(&c->d_tri32, t32));
-    }
-#endif
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
@@ -414,7 +369,7 @@ static int ctx_setup(mfx_ctx* c) {
         (shd ? sbpc : ebpc) = blocks;
     }
     {  // top BVH nodes in LDS: as many as fit in the LDS the resident blocks leave over
-        int cap = std::min(c->host.inst.empty() && MFX_WIDE ? c->wide_nodes : (int)c->host.nodes.size(), WF_NTOP_MAX);
+        int cap = std::min((int)c->host.nodes.size(), WF_NTOP_MAX);
         if (const char* e = getenv("MFX_NTOP")) cap = std::max(0, std::min(cap, atoi(e)));
         for (int k = 0; k < 2; ++k) {
             const bool shd = k == 1;
@@ -469,14 +424,16 @@ static int ctx_setup(mfx_ctx* c) {
 // Two-level or flat for an instanced scene. The flat image (one BVH over the expansion) is the faster
 // search (C5: 5,088 vs 4,729 Mrays/s, r02bt) and exactly the same results, so it is taken whenever it
 // fits the budget: traversal slots of the expansion x 512 B (slot, shade record, nodes and reference
-// leaves) <= MFX_FLATTEN_MAX_BYTES (default 2 GiB; C5 is 93,698 slots, 48 MB). MFX_F_TWO_LEVEL keeps
-// the instances two-level regardless; MFX_F_FLATTEN flattens regardless.
+// leaves) <= MFX_FLATTEN_MAX_BYTES (default 2 GiB; C5 is 93,698 slots, 48 MB) and, on a device,
+// <= a sixteenth of its free memory. MFX_F_TWO_LEVEL keeps the instances two-level regardless;
+// MFX_F_FLATTEN flattens regardless (both: rejected, MFX_E_INVALID, by the callers).
 static bool flatten_instances(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
-                              int32_t flags) {
+                              int32_t flags, size_t device_free = 0) {
     if (flags & MFX_F_FLATTEN) return true;
     if (!instances || (flags & MFX_F_TWO_LEVEL)) return false;
     double budget = 2.0 * 1024 * 1024 * 1024;
     if (const char* e = getenv("MFX_FLATTEN_MAX_BYTES")) budget = atof(e);
+    if (device_free > 0) budget = std::min(budget, (double)device_free / 16.0);
     double slots = 0.0;
     for (int32_t i = 0; i < ninstances; ++i) {
         const int64_t f = instances[i].first, n = instances[i].count;
@@ -497,6 +454,8 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
     if (opt->render_ahead < 0 || opt->render_ahead > MFX_MAX_RENDER_AHEAD)
         return fail(MFX_E_INVALID, "mfx_create: render_ahead out of range");
     if (scene->nmat > WF_MAT_MAX) return fail(MFX_E_INVALID, "mfx_create: more than 65,536 materials");
+    if ((opt->flags & MFX_F_FLATTEN) && (opt->flags & MFX_F_TWO_LEVEL))
+        return fail(MFX_E_INVALID, "mfx_create: MFX_F_FLATTEN and MFX_F_TWO_LEVEL exclude each other");
     int ndev = 0;
     HIPCHECK(hipGetDeviceCount(&ndev));
     std::vector<int> devlist;
@@ -506,12 +465,14 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         if (d < 0 || d >= ndev) return fail(MFX_E_DEVICE, "mfx_create: no such HIP device");
     const int G = (int)devlist.size();
     HIPCHECK(hipSetDevice(devlist[0]));
+    size_t dev_free = 0, dev_total = 0;
+    if (hipMemGetInfo(&dev_free, &dev_total) != hipSuccess) dev_free = 0;
     mfx_ctx* c = new mfx_ctx();
     std::string err;
     // the traversal BVH is built on the first device unless the caller asks for the host build
     // (the same tree either way: tests/test_gpu_build.py); the other devices get copies
     if (!mfx_build_scene(scene, c->host, err, (opt->flags & MFX_F_HOST_BVH) == 0, instances, ninstances,
-                         flatten_instances(scene, instances, ninstances, opt->flags))) {
+                         flatten_instances(scene, instances, ninstances, opt->flags, dev_free))) {
         delete c;
         const bool dev = err.rfind("GPU BVH build", 0) == 0;
         return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
@@ -642,31 +603,12 @@ int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* in
     MfxHostScene h;
     std::string err;
     if (!scene) return fail(MFX_E_INVALID, "null argument");
+    if ((flags & MFX_F_FLATTEN) && (flags & MFX_F_TWO_LEVEL))
+        return fail(MFX_E_INVALID, "mfx_build_instanced_info: MFX_F_FLATTEN and MFX_F_TWO_LEVEL exclude each other");
     if (!mfx_build_scene(scene, h, err, false, instances, ninstances, flatten_instances(scene, instances, ninstances, flags)))
         return fail(MFX_E_INVALID, "mfx_build_instanced_info: " + err);
     instancing_info(h, out);
     if (stack_entries) *stack_entries = h.stack_entries;
-    return MFX_OK;
-}
-
-int mfx_wide_info(const mfx_scene_desc* scene, double out[8]) {
-    if (!scene || !out) return fail(MFX_E_INVALID, "null argument");
-    MfxHostScene h;
-    MfxWideImage w;
-    std::string err;
-    if (!mfx_build_scene(scene, h, err, false)) return fail(MFX_E_INVALID, "mfx_wide_info: " + err);
-    double mean = 0.0;
-    int64_t nl = 0;
-    if (!mfx_build_wide(h.nodes, w, err) || !mfx_check_wide(h.nodes, w, err, &mean, &nl))
-        return fail(MFX_E_INVALID, "mfx_wide_info: " + err);
-    out[0] = (double)w.nodes.size();
-    out[1] = w.stack_entries;
-    out[2] = h.stack_entries;
-    out[3] = w.depth;
-    out[4] = h.bvh_depth;
-    out[5] = w.xf.s;
-    out[6] = mean;
-    out[7] = (double)nl;
     return MFX_OK;
 }
 
@@ -752,9 +694,6 @@ static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
-    P.tnodes = tnodes_of(c);
-    P.wx = c->wide_xf;
-    P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
@@ -900,9 +839,6 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
-    P.tnodes = tnodes_of(c);
-    P.wx = c->wide_xf;
-    P.tri32 = c->d_tri32;
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;
@@ -1501,9 +1437,6 @@ static int run_query(mfx_ctx* c, int64_t n, const double* rays, double tmin, dou
         QueryParams Q;
         std::memset(&Q, 0, sizeof(Q));
         Q.nodes = c->d_nodes;
-        Q.tnodes = tnodes_of(c);
-        Q.wx = c->wide_xf;
-        Q.tri32 = c->d_tri32;
         Q.slots = c->d_slots;
     Q.slot_ref = c->d_slot_ref;
         Q.ref_blob = c->d_ref_blob;
@@ -1621,22 +1554,6 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
     for (void* p : {(void*)da, (void*)db, (void*)dd, (void*)ds})
         if (p) (void)hipFree(p);
     if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("fp64 selftest: ") + hipGetErrorString(e));
-    return MFX_OK;
-}
-
-int mfx_tri_screen_selftest(int32_t device, int64_t n, const double* rec, double* out) {
-    if (n <= 0 || !rec || !out) return fail(MFX_E_INVALID, "bad selftest arguments");
-    HIPCHECK(hipSetDevice(device));
-    double *dr = nullptr, *dout = nullptr;
-    hipError_t e = hipMalloc((void**)&dr, sizeof(double) * 18 * n);
-    if (e == hipSuccess) e = hipMalloc((void**)&dout, sizeof(double) * 3 * n);
-    if (e == hipSuccess) e = hipMemcpy(dr, rec, sizeof(double) * 18 * n, hipMemcpyHostToDevice);
-    if (e == hipSuccess) e = mfx_launch_tri_screen_selftest(dr, n, dout, nullptr);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
-    if (e == hipSuccess) e = hipMemcpy(out, dout, sizeof(double) * 3 * n, hipMemcpyDeviceToHost);
-    if (dr) (void)hipFree(dr);
-    if (dout) (void)hipFree(dout);
-    if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("tri screen selftest: ") + hipGetErrorString(e));
     return MFX_OK;
 }
 

@@ -9,9 +9,6 @@
 
 struct TraceParams {
     const MfxNode* nodes;
-    const MfxTNode* tnodes;  // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
-    MfxWideXf wx;            // their frame
-    const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
@@ -35,9 +32,6 @@ struct TraceParams {
 
 struct QueryParams {
     const MfxNode* nodes;
-    const MfxTNode* tnodes;  // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
-    MfxWideXf wx;            // their frame
-    const MfxTri32* tri32;
     const MfxSlot* slots;
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
@@ -67,6 +61,5 @@ hipError_t mfx_launch_accum_add(double* dst, const double* src, int64_t n, hipSt
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo,
                                     hipStream_t st);
 hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st);
-hipError_t mfx_launch_tri_screen_selftest(const double* rec, int64_t n, double* out, hipStream_t st);
 
 #endif

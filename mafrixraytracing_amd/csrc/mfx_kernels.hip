@@ -35,7 +35,7 @@ __global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     int* stack = lds + wave * P.stack_size * 64 + lane;
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes, P.wx};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
     const MfxLight& LT = P.light;
     const MfxCamera& CAM = P.cam;
     const int W = P.width, H = P.height;
@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(256) closest_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes, Q.wx};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
@@ -283,7 +283,7 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     int* stack = lds + wave * Q.stack_size * 64 + lane;
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= Q.n) return;
-    const SceneView S{Q.nodes, Q.tri32, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0, Q.tnodes, Q.wx};
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0};
     const DV o = ld3(Q.rays + 6 * k), d = ld3(Q.rays + 6 * k + 3);
     Best B;
     Stats st{0, 0, 0};
@@ -403,37 +403,6 @@ __global__ void aabb_selftest_kernel(const double* rec, int64_t n, int32_t* out)
     out[3 * k + 2] = tri_box_pass(ld3(r + 14), ld3(r + 17), ld3(r + 20), o, d, r[12], r[13]) ? 1 : 0;
 }
 
-// The FP32 triangle screen (tri_skip32) against the exact FP64 test (tri_hit64): rec = 18 doubles
-// per case (o, d, v0, e1, e2, tMin, beyond, tMax); out = 3 per case: the FP64 test's hit (0/1), its
-// t, and the screen's skip (1: claims the slot cannot change a leaf result). Wherever skip is 1 the
-// FP64 test must miss, or hit at beyond < t < tMax.
-__global__ void tri_screen_selftest_kernel(const double* rec, int64_t n, double* out) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const double* r = rec + 18 * k;
-    const DV o = ld3(r), d = ld3(r + 3);
-    SlotR sl;
-    sl.a = ld3(r + 6);
-    sl.b = ld3(r + 9);
-    sl.c = ld3(r + 12);
-    sl.first = 0;
-    sl.info = 0;
-    double t = 0.0;
-    const bool hit = tri_hit64(sl, o, d, r[15], t);
-    MfxTri32 T;
-    for (int c = 0; c < 3; ++c) {
-        T.v0[c] = (float)r[6 + c];
-        T.e1[c] = (float)r[9 + c];
-        T.e2[c] = (float)r[12 + c];
-    }
-    T.flags = 0;
-    T.pad[0] = T.pad[1] = 0.f;
-    const bool skip = tri_skip32(&T, ray32(o, d), (float)r[15], (float)r[16], (float)r[17]);
-    out[3 * k] = hit ? 1.0 : 0.0;
-    out[3 * k + 1] = t;
-    out[3 * k + 2] = skip ? 1.0 : 0.0;
-}
-
 // ----------------------------------------------------------------------------------------------
 // Host-side launchers (called from mfx_api.cpp)
 // ----------------------------------------------------------------------------------------------
@@ -520,11 +489,6 @@ hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n,
 
 hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st) {
     hipLaunchKernelGGL(aabb_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, out);
-    return hipGetLastError();
-}
-
-hipError_t mfx_launch_tri_screen_selftest(const double* rec, int64_t n, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(tri_screen_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, out);
     return hipGetLastError();
 }
 

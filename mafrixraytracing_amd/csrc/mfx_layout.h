@@ -27,6 +27,14 @@
 #define MFX_KIND_RECT 1
 #define MFX_KIND_SPHERE 2
 
+// Diagnostic-only kernel options (timing stamps, occlusion statistics, the stage-removal timing
+// builds of scripts/diag_variant.py) exist only in a build with -DMFX_DIAG; the shipped library
+// has none of them.
+#if !defined(MFX_DIAG) && (defined(MFX_DIAG_STAMPS) || defined(MFX_DIAG_OCCLUSION) || \
+                           defined(MFX_DIAG_SKIP_SHADOW_TRAV) || defined(MFX_DIAG_ONE_TRIAL))
+#error "MFX_DIAG_* options need a -DMFX_DIAG build"
+#endif
+
 struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache line)
     float lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
     int32_t child[4];  // >= 0 node index, < 0 ~(leaf code), MFX_CHILD_EMPTY (box lo = hi = FLT_MAX: never hit)
@@ -34,35 +42,6 @@ struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache l
 };
 #define MFX_CHILD_EMPTY (-0x7fffffff - 1)
 
-// The per-lane traversal's BVH8 (MFX_WIDE; flat scenes): each node is a BVH4 node with its
-// children's children pulled up, the largest boxes first, while at most 8 entries result
-// (mfx_wide.cpp). A node is one 128-B line: the 8 child boxes with every plane stored as FP16 of
-// (plane - center) * scale, rounded outward (lo down, hi up; an empty entry's planes +inf, never
-// entered), and the 8 children (BVH4 codes: leaves keep their leaf codes). The rays are moved into
-// the same frame (o' = (o - center) * scale, d' = d * scale with a power-of-2 scale), which leaves
-// every slab distance t unchanged, and the boxes contain the FP32 ones, so the search stays
-// conservative. A wave's node loop takes fewer rounds (C2: 4.5 BVH4 steps per
-// closest ray) for the same one line per lane per step.
-#ifndef MFX_WIDE
-#define MFX_WIDE 0  // measured slower (r03n-r03q: node visits -23 to -30 %, frames -5 to -7 %): DESIGN.md §9
-#endif
-#ifndef MFX_WIDE_SORT
-#define MFX_WIDE_SORT 1  // 0: the BVH8 step takes the nearest hit and pushes the others unsorted
-#endif
-struct alignas(16) MfxNode8H {
-    uint16_t lox[8], hix[8], loy[8], hiy[8], loz[8], hiz[8];  // FP16 bits
-    int32_t child[8];  // as MfxNode::child
-};
-static_assert(sizeof(MfxNode8H) == 128, "one line per wide node");
-// the BVH8 frame: o' = (o - c) * s (MfxNode8H)
-struct MfxWideXf {
-    double cx, cy, cz, s;
-};
-#if MFX_WIDE
-typedef MfxNode8H MfxTNode;
-#else
-typedef MfxNode MfxTNode;
-#endif
 // nodes[0 .. MFX_TOP_NODES) are the BVH's top levels in breadth-first order (the trace kernels
 // keep a prefix of them in LDS); the rest follow in preorder
 #ifndef MFX_TOP_NODES
@@ -102,23 +81,6 @@ struct alignas(16) MfxSlot {
 // leaf child code: ~((first slot << 3) | (slots - 1)), at most 8 slots (4 primitives, rects take 2)
 #define MFX_LEAF_SLOTS_MAX 8
 #define MFX_SLOTS_MAX (1 << 27)  // leaf codes stay below MFX_INST_FLAG
-
-// FP32 copy of a traversal slot's triangle (v0, e1, e2 rounded to nearest) for the conservative
-// screen in front of the exact FP64 test (mfx_trace_common.h: tri_skip32): 48 B, three 16-B loads
-// instead of the FP64 slot's five. flags: MFX_T32_NOSCREEN (a sphere: never screened), MFX_T32_RECT
-// (first half of a rect: the next slot is its second half).
-struct alignas(16) MfxTri32 {
-    float v0[3];
-    float e1[3];
-    float e2[3];
-    int32_t flags;
-    float pad[2];
-};
-#ifndef MFX_LEAF_SCREEN32
-#define MFX_LEAF_SCREEN32 0  // 1: the FP32 screen in front of every slot's FP64 test (r03c: -27 to -33 %, spills)
-#endif
-#define MFX_T32_NOSCREEN 1
-#define MFX_T32_RECT 2
 
 struct alignas(16) MfxShade {
     double n[3];        // face normal of this triangle slot; a sphere's centre

@@ -110,11 +110,6 @@ __device__ __forceinline__ DV hemisphere_ball(DV nm, uint64_t key, uint32_t& rn)
 
 __device__ __forceinline__ double rng_next(uint64_t key, uint32_t& n) {
     n += 1;
-#ifdef MFX_DIAG_CHEAP_RNG
-    uint32_t h = (uint32_t)key ^ (uint32_t)(key >> 32) ^ (n * 0x9e3779b9u);
-    h ^= h >> 16; h *= 0x7feb352du; h ^= h >> 15; h *= 0x846ca68bu; h ^= h >> 16;
-    return (double)h * (1.0 / 4294967296.0);
-#endif
     uint64_t z = mix64(key + (uint64_t)n * 0x9e3779b97f4a7c15ULL);
     return (double)(z >> 11) * (1.0 / 9007199254740992.0);
 }
@@ -235,15 +230,12 @@ __device__ __forceinline__ bool sphere_hit64(const MfxSlot& s, DV o, DV d, doubl
 
 struct SceneView {
     const MfxNode* __restrict__ nodes;
-    const MfxTri32* __restrict__ tri32;    // FP32 copies of the slots' triangles (the leaf screen)
     const MfxSlot* __restrict__ slots;     // traversal leaves: runs of MfxSlot records
     const int32_t* __restrict__ slot_ref;  // per slot: 16-byte offset of its reference leaf in ref_blob
     const uint8_t* __restrict__ ref_blob;  // reference leaves: MfxLeaf + slot copies
     const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
     const MfxInstance* inst_lds;           // LDS copy of instances [0, ninst_lds) (wavefront kernels)
     int ninst_lds;
-    const MfxTNode* __restrict__ tnodes;   // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8)
-    MfxWideXf wx;                          // and their frame (MfxNode8H)
 };
 
 // An instance's record: from the kernel's LDS copy when it holds it, else from global memory
@@ -483,67 +475,6 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
     return ok;
 }
 
-// FP32 copy of the ray for tri_skip32 (o and d rounded to nearest)
-struct Ray32 {
-    float o[3], d[3];
-};
-__device__ __forceinline__ Ray32 ray32(DV o, DV d) {
-    return Ray32{{(float)o.x, (float)o.y, (float)o.z}, {(float)d.x, (float)d.y, (float)d.z}};
-}
-
-// The exact FP64 Triangle.Hit (tri_hit64, Trangle.fs:120-155) of this slot certainly cannot change
-// the leaf's result: it returns false (|div| < 1e-6, b1 < 0, b1 > 1, b2 < 0, b1 + b2 >= 1 or
-// t <= tMin), or a t certainly above `beyond` (the best hit of a closest query; +inf otherwise) and
-// below tMax (so no whole-reference-leaf evaluation either). false: undecided, the FP64 test runs.
-// Every quantity the FP64 test compares — div, and b1, b2, t times |div| with div's sign — is a
-// polynomial of degree <= 3 in o, v0, d, e1, e2. Computed in FP32 from the inputs rounded to
-// nearest, it differs from the FP64 test's value by less than 2^-16 Q + 1e-30, Q the polynomial
-// over the inputs' magnitudes (|o| + |v0| for o - v0): at most 3 input roundings of 2^-24 per
-// factor (o - v0 counts two) and 7 operation roundings along any term bound the FP32 error by
-// 12 * 2^-24 Q, the FP64 test's own error is below 2^-48 Q, and FP32 underflow adds at most 2^-126
-// per operation, so 2^-16 keeps a factor of 16. A decision is taken only when it holds for every
-// value in those intervals, with another 2^-20 for the FP64 quotients' roundings and for tMin /
-// beyond / tMax rounded to FP32. Magnitudes bound the values, so an overflow makes a margin
-// infinite; NaN and infinite values fail every comparison below and leave the slot undecided.
-__device__ __forceinline__ bool tri_skip32(const MfxTri32* __restrict__ p, const Ray32& r, float tmin, float beyond,
-                                           float tmax) {
-    const float4* __restrict__ q = (const float4*)p;
-    const float4 q0 = q[0], q1 = q[1], q2 = q[2];
-    if (__float_as_int(q2.y) & MFX_T32_NOSCREEN) return false;
-    const float E = 0x1p-16f, A = 1e-30f, U = 1.f + 0x1p-20f, L = 1.f - 0x1p-20f;
-    const float vx = q0.x, vy = q0.y, vz = q0.z, ax = q0.w, ay = q1.x, az = q1.y, bx = q1.z, by = q1.w, bz = q2.x;
-    const float dx = r.d[0], dy = r.d[1], dz = r.d[2];
-    const float adx = fabsf(dx), ady = fabsf(dy), adz = fabsf(dz);
-    // s1 = d x e2, div = s1 . e1
-    const float s1x = dy * bz - dz * by, s1y = dz * bx - dx * bz, s1z = dx * by - dy * bx;
-    const float S1x = ady * fabsf(bz) + adz * fabsf(by), S1y = adz * fabsf(bx) + adx * fabsf(bz),
-                S1z = adx * fabsf(by) + ady * fabsf(bx);
-    const float div = s1x * ax + s1y * ay + s1z * az;
-    const float Ed = E * (S1x * fabsf(ax) + S1y * fabsf(ay) + S1z * fabsf(az)) + A;
-    const float adv = fabsf(div);
-    if (adv + Ed < 1e-6f * L) return true;  // culled
-    const float lo = adv - Ed, hi = (adv + Ed) * U;
-    if (!(lo > 1e-6f * U)) return false;    // near the cull, or div's sign unknown
-    const float sg = div < 0.f ? -1.f : 1.f;
-    // dd = o - v0; b1 |div| = sg (dd . s1)
-    const float ddx = r.o[0] - vx, ddy = r.o[1] - vy, ddz = r.o[2] - vz;
-    const float Dx = fabsf(r.o[0]) + fabsf(vx), Dy = fabsf(r.o[1]) + fabsf(vy), Dz = fabsf(r.o[2]) + fabsf(vz);
-    const float n1 = sg * (ddx * s1x + ddy * s1y + ddz * s1z), E1 = E * (Dx * S1x + Dy * S1y + Dz * S1z) + A;
-    if (n1 + E1 < -A) return true;  // b1 < 0
-    if (n1 - E1 > hi) return true;  // b1 > 1
-    // s2 = dd x e1; b2 |div| = sg (d . s2), t |div| = sg (e2 . s2)
-    const float s2x = ddy * az - ddz * ay, s2y = ddz * ax - ddx * az, s2z = ddx * ay - ddy * ax;
-    const float S2x = Dy * fabsf(az) + Dz * fabsf(ay), S2y = Dz * fabsf(ax) + Dx * fabsf(az),
-                S2z = Dx * fabsf(ay) + Dy * fabsf(ax);
-    const float n2 = sg * (dx * s2x + dy * s2y + dz * s2z), E2 = E * (adx * S2x + ady * S2y + adz * S2z) + A;
-    if (n2 + E2 < -A) return true;                 // b2 < 0
-    if ((n1 - E1) + (n2 - E2) > hi) return true;   // b1 + b2 >= 1 (reached only with 0 <= b1 <= 1, b2 >= 0)
-    const float nt = sg * (bx * s2x + by * s2y + bz * s2z),
-                Et = E * (fabsf(bx) * S2x + fabsf(by) * S2y + fabsf(bz) * S2z) + A;
-    if (nt + Et < 0.f || nt + Et < tmin * L * lo) return true;                      // t <= tMin
-    return nt - Et > beyond * U * hi && nt + Et < tmax * L * lo;                     // beyond the best hit
-}
-
 // One traversal leaf (1..4 primitives of possibly different reference leaves; child code = first
 // slot << 3 | slots - 1). Each primitive hit is a candidate for its reference leaf's result: with
 // t < tMax the reference leaf's minBy result is a hit of t no larger (the leaf's other primitives
@@ -564,28 +495,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     if (STATS) st.clusters++;
     bool improved = false;
     constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
-#if MFX_LEAF_SCREEN32
-    const Ray32 r32 = ray32(o, d);
-    const float tmin32 = (float)tMin, tmax32 = (float)tMax;
-#endif
     for (int k = 0; k < n; ++k) {
-#if MFX_LEAF_SCREEN32
-        {  // slots the FP64 test certainly rejects (a rect: both halves) are skipped unread
-            const float beyond = (!SHADOW && B.found) ? (float)B.t : __builtin_inff();
-            const MfxTri32* t32 = S.tri32 + s0 + k;
-            if (tri_skip32(t32, r32, tmin32, beyond, tmax32)) {
-                if (!(__float_as_int(((const float4*)t32)[2].y) & MFX_T32_RECT)) {
-                    if (STATS) st.prims++;
-                    continue;
-                }
-                if (tri_skip32(t32 + 1, r32, tmin32, beyond, tmax32)) {
-                    if (STATS) st.prims++;
-                    ++k;
-                    continue;
-                }
-            }
-        }
-#endif
 #if MFX_LEAF_PRELOAD
         SlotR r = UNI ? load_slot_u(sl + k) : load_slot(sl + k);
         // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)
@@ -661,9 +571,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
 #endif
         if (PRE == 2) {
             const double blo[3] = {bx0.x, bx0.y, bx1.x}, bhi[3] = {bx1.y, bx2.x, bx2.y};
-#ifndef MFX_DIAG_NO_LEAFBOX  // timing experiment only: the reference leaf's box test assumed to pass
             if (!aabb_hit(blo, bhi, o, d, tMin, tMax)) continue;
-#endif
         } else if (UNI) {
             double blo[3], bhi[3];
             load_box_u(sl + hs, blo, bhi);
@@ -687,21 +595,9 @@ __device__ __forceinline__ float f_round_up(double x) {
 // overflows to +inf (an empty child's +inf planes, mfx_api.cpp node_to_half) is never entered
 __device__ __forceinline__ float f_tlim(double x) { return fminf(f_round_up(x), 3.402823466e38f); }
 
-#ifndef MFX_NEAR_FAR_PLANES
-#define MFX_NEAR_FAR_PLANES 0  // 1: node steps read each axis's near / far planes by the ray's direction signs
-#endif
-#if MFX_NEAR_FAR_PLANES && MFX_WIDE
-#error "MFX_NEAR_FAR_PLANES reads BVH4 FP32 nodes: build it with MFX_WIDE=0"
-#endif
-
 // FP32 ray for the cluster-BVH slab tests
 struct RayF {
     float ix, iy, iz, oix, oiy, oiz;
-#if MFX_NEAR_FAR_PLANES
-    // byte offsets in an MfxNode of each axis's near-plane column (lo if the direction component
-    // is >= +0, else hi); the far plane's column is the other one (offset ^ 16)
-    uint32_t px, py, pz;
-#endif
 };
 __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
     // tiny direction components clamped so 1/d stays finite (no 0*inf NaNs)
@@ -713,23 +609,7 @@ __device__ __forceinline__ RayF make_rayf(DV o, DV d) {
     RayF r;
     r.ix = 1.0f / dx; r.iy = 1.0f / dy; r.iz = 1.0f / dz;
     r.oix = (float)o.x * r.ix; r.oiy = (float)o.y * r.iy; r.oiz = (float)o.z * r.iz;
-#if MFX_NEAR_FAR_PLANES
-    // the sign of 1/d is the sign of the clamped d (-0.0 -> -tiny: hi is near)
-    r.px = (__float_as_uint(r.ix) >> 31) << 4;
-    r.py = 32u | ((__float_as_uint(r.iy) >> 31) << 4);
-    r.pz = 64u | ((__float_as_uint(r.iz) >> 31) << 4);
-#endif
     return r;
-}
-// the FP32 search ray of a flat scene's per-lane traversal: in the BVH8's frame (MfxNode8H: o' =
-// (o - c) * s, d' = d * s, s a power of 2, so every slab distance is the world one)
-__device__ __forceinline__ RayF make_rayf_t(const SceneView& S, DV o, DV d) {
-#if MFX_WIDE
-    const double s = S.wx.s;
-    return make_rayf(dv((o.x - S.wx.cx) * s, (o.y - S.wx.cy) * s, (o.z - S.wx.cz) * s), dv(d.x * s, d.y * s, d.z * s));
-#else
-    return make_rayf(o, d);
-#endif
 }
 // the same ray from another origin (an instance frame's o - off, or back to the world's o): the
 // direction terms are the ray's own, so only the origin products are recomputed, with make_rayf's
@@ -804,9 +684,8 @@ struct TopNodes {
     int ntop;
 };
 __device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
-// block-wide copy at kernel start (all threads; ends with a barrier); BVH4 (MfxNode) and BVH8
-// (MfxNode8H) nodes are both eight 16-B columns
-static_assert(sizeof(MfxNode) == 128 && sizeof(MfxNode8H) == 128, "top nodes are 8 columns");
+// block-wide copy at kernel start (all threads; ends with a barrier); a node is eight 16-B columns
+static_assert(sizeof(MfxNode) == 128, "top nodes are 8 columns");
 __device__ __forceinline__ void load_top_nodes(float4* lds, const void* __restrict__ nodes, int ntop) {
     const float4* __restrict__ g = (const float4*)nodes;
     for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
@@ -838,61 +717,6 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
-#if MFX_NEAR_FAR_PLANES
-    // Each axis's slab values are read in (near, far) order: the near plane is lo for a direction
-    // component >= 0, hi otherwise, chosen by the load's per-lane column offset (RayF::px..pz).
-    // For a box with lo <= hi the rounded values keep that order (fma is monotone in the plane,
-    // the factor's sign fixed), so near = min(a0, a1) and far = max(a0, a1) bit for bit and the
-    // per-axis min / max pairs disappear; the empty child (lo = hi = FLT_MAX) still never hits.
-    // The slab FMAs run two children per v_pk_fma_f32.
-    typedef float f2 __attribute__((ext_vector_type(2)));
-    float4 nxv, fxv, nyv, fyv, nzv, fzv;
-    int4 ch;
-    const uint32_t nb = (uint32_t)node * 128u;
-    if (TOP && node < tn.ntop) {
-        // LDS column c of node n sits at byte n * 128 + ((c ^ sw) << 4) (top_col)
-        const uint32_t sw = (((uint32_t)node >> 1) & 7u) << 4;
-        const char* t = (const char*)tn.lds + nb;
-        nxv = *(const float4*)(t + (r.px ^ sw)); fxv = *(const float4*)(t + (r.px ^ 16u ^ sw));
-        nyv = *(const float4*)(t + (r.py ^ sw)); fyv = *(const float4*)(t + (r.py ^ 16u ^ sw));
-        nzv = *(const float4*)(t + (r.pz ^ sw)); fzv = *(const float4*)(t + (r.pz ^ 16u ^ sw));
-        const float4 c4 = *(const float4*)(t + (96u ^ sw));
-        ch = make_int4(__float_as_int(c4.x), __float_as_int(c4.y), __float_as_int(c4.z), __float_as_int(c4.w));
-    } else {
-        const char* __restrict__ g = (const char*)nodes;
-        nxv = *(const float4*)(g + (nb | r.px)); fxv = *(const float4*)(g + (nb | (r.px ^ 16u)));
-        nyv = *(const float4*)(g + (nb | r.py)); fyv = *(const float4*)(g + (nb | (r.py ^ 16u)));
-        nzv = *(const float4*)(g + (nb | r.pz)); fzv = *(const float4*)(g + (nb | (r.pz ^ 16u)));
-        ch = *(const int4*)(g + nb + 96u);
-    }
-    const f2 ix2 = {r.ix, r.ix}, iy2 = {r.iy, r.iy}, iz2 = {r.iz, r.iz};
-    const f2 ox2 = {-r.oix, -r.oix}, oy2 = {-r.oiy, -r.oiy}, oz2 = {-r.oiz, -r.oiz};
-    f2 An[3][2], Af[3][2];
-    An[0][0] = __builtin_elementwise_fma((f2){nxv.x, nxv.y}, ix2, ox2);
-    An[0][1] = __builtin_elementwise_fma((f2){nxv.z, nxv.w}, ix2, ox2);
-    Af[0][0] = __builtin_elementwise_fma((f2){fxv.x, fxv.y}, ix2, ox2);
-    Af[0][1] = __builtin_elementwise_fma((f2){fxv.z, fxv.w}, ix2, ox2);
-    An[1][0] = __builtin_elementwise_fma((f2){nyv.x, nyv.y}, iy2, oy2);
-    An[1][1] = __builtin_elementwise_fma((f2){nyv.z, nyv.w}, iy2, oy2);
-    Af[1][0] = __builtin_elementwise_fma((f2){fyv.x, fyv.y}, iy2, oy2);
-    Af[1][1] = __builtin_elementwise_fma((f2){fyv.z, fyv.w}, iy2, oy2);
-    An[2][0] = __builtin_elementwise_fma((f2){nzv.x, nzv.y}, iz2, oz2);
-    An[2][1] = __builtin_elementwise_fma((f2){nzv.z, nzv.w}, iz2, oz2);
-    Af[2][0] = __builtin_elementwise_fma((f2){fzv.x, fzv.y}, iz2, oz2);
-    Af[2][1] = __builtin_elementwise_fma((f2){fzv.z, fzv.w}, iz2, oz2);
-    float d[4];
-    int c[4] = {ch.x, ch.y, ch.z, ch.w};
-    int nh = 0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const int p = k >> 1, e = k & 1;
-        const float n = fmaxf(fmaxf(An[0][p][e], An[1][p][e]), fmaxf(An[2][p][e], 0.0f));
-        const float f = fminf(fminf(Af[0][p][e], Af[1][p][e]), fminf(Af[2][p][e], tlim));
-        const bool h = n <= f;
-        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
-        nh += h ? 1 : 0;
-    }
-#else
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
     // reads land in the same registers, so the LDS reads wait for the global loads (measured
     // alternatives: LDS only when the whole wave is at top nodes, -0.5 to -2 %; both reads by every
@@ -910,17 +734,6 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         lx = q[0]; hx = q[1]; ly = q[2]; hy = q[3]; lz = q[4]; hz = q[5];
         ch = *(const int4*)(q + 6);
     }
-#ifdef MFX_DIAG_EXTRA_NODE_LOADS
-    const float4* __restrict__ q = (const float4*)(nodes + node);
-#endif
-#ifdef MFX_DIAG_EXTRA_NODE_LOADS  // timing experiment: MFX_DIAG_EXTRA_NODE_LOADS more 16-B loads per step
-#pragma unroll
-    for (int k = 0; k < MFX_DIAG_EXTRA_NODE_LOADS; ++k) {
-        const int z = __float_as_int(tlim) == 0x7fffffff ? 1 : 0;  // a runtime 0 the compiler cannot fold
-        const int4 x = *((const int4*)(q + (k % 7)) + z);
-        if ((x.x ^ x.y ^ x.z ^ x.w) == 0x7fedcba9) ch.x = 0;  // never true for real node data
-    }
-#endif
     float d[4];
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     int nh = 0;
@@ -938,7 +751,6 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         d[k] = h ? (FAR ? -f : n) : __builtin_inff();
         nh += h ? 1 : 0;
     }
-#endif
     cswap(d[0], c[0], d[1], c[1]);
     cswap(d[2], c[2], d[3], c[3]);
     cswap(d[0], c[0], d[2], c[2]);
@@ -949,79 +761,6 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]), dp);
     if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1], dp);
     if (nh >= 4) stack.put(sp + 2, c[1], dp);
-    const bool pop = nh == 0 && sp > 0;
-    const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
-    sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
-    return next;
-}
-
-// One node step of the BVH8 (MfxNode8H): the same contract as the BVH4 step above, eight children
-// from one line: six 16-B columns of FP16 planes (read through v_fma_mix_f32) and two of
-// children; the hits sorted near to far by a 19-comparator network (misses last at +inf), the
-// nearest taken and the others pushed far-first (up to 7).
-template <bool TOP = false, bool FAR = false, typename ST>
-__device__ __forceinline__ int node_step(const MfxNode8H* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
-    const bool dp = stack.deep(sp + 7);  // this step reads sp - 1 and may write sp .. sp + 6
-    const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
-    typedef _Float16 h8 __attribute__((ext_vector_type(8)));
-    mfx_i4 q[8];
-    if (TOP && node < tn.ntop) {
-        const int sw = (node >> 1) & 7;
-        const mfx_i4* t = (const mfx_i4*)tn.lds + node * 8;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = t[k ^ sw];
-    } else {
-        const mfx_i4* __restrict__ g = (const mfx_i4*)(nodes + node);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) q[k] = g[k];
-    }
-    const h8 LX = __builtin_bit_cast(h8, q[0]), HX = __builtin_bit_cast(h8, q[1]);
-    const h8 LY = __builtin_bit_cast(h8, q[2]), HY = __builtin_bit_cast(h8, q[3]);
-    const h8 LZ = __builtin_bit_cast(h8, q[4]), HZ = __builtin_bit_cast(h8, q[5]);
-    float d[8];
-    int c[8] = {q[6].x, q[6].y, q[6].z, q[6].w, q[7].x, q[7].y, q[7].z, q[7].w};
-    int nh = 0;
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const float a0 = fmaf((float)LX[k], r.ix, -r.oix), a1 = fmaf((float)HX[k], r.ix, -r.oix);
-        const float b0 = fmaf((float)LY[k], r.iy, -r.oiy), b1 = fmaf((float)HY[k], r.iy, -r.oiy);
-        const float c0 = fmaf((float)LZ[k], r.iz, -r.oiz), c1 = fmaf((float)HZ[k], r.iz, -r.oiz);
-        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-        const bool h = n <= f;
-        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
-        nh += h ? 1 : 0;
-    }
-#if MFX_WIDE_SORT
-    // optimal 8-input network (19 comparators, depth 6)
-    cswap(d[0], c[0], d[2], c[2]); cswap(d[1], c[1], d[3], c[3]); cswap(d[4], c[4], d[6], c[6]); cswap(d[5], c[5], d[7], c[7]);
-    cswap(d[0], c[0], d[4], c[4]); cswap(d[1], c[1], d[5], c[5]); cswap(d[2], c[2], d[6], c[6]); cswap(d[3], c[3], d[7], c[7]);
-    cswap(d[0], c[0], d[1], c[1]); cswap(d[2], c[2], d[3], c[3]); cswap(d[4], c[4], d[5], c[5]); cswap(d[6], c[6], d[7], c[7]);
-    cswap(d[2], c[2], d[4], c[4]); cswap(d[3], c[3], d[5], c[5]);
-    cswap(d[1], c[1], d[4], c[4]); cswap(d[3], c[3], d[6], c[6]);
-    cswap(d[1], c[1], d[2], c[2]); cswap(d[3], c[3], d[4], c[4]); cswap(d[5], c[5], d[6], c[6]);
-    // far-first pushes: stack[sp + nh - 1 - k] = c[k] for 1 <= k < nh (exec-masked stores)
-#pragma unroll
-    for (int k = 1; k < 8; ++k)
-        if (k < nh) stack.put(sp + nh - 1 - k, c[k], dp);
-#else
-    // the nearest hit child is taken next; the other hits are pushed in child order (no sort)
-    float dm = d[0];
-    int cm = c[0], km = 0;
-#pragma unroll
-    for (int k = 1; k < 8; ++k) {
-        const bool s = d[k] < dm;
-        dm = s ? d[k] : dm;
-        cm = s ? c[k] : cm;
-        km = s ? k : km;
-    }
-    int at = sp;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-        if (d[k] != __builtin_inff() && k != km) stack.put(at++, c[k], dp);
-    c[0] = cm;
-#endif
     const bool pop = nh == 0 && sp > 0;
     const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
     sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
@@ -1156,7 +895,7 @@ template <bool SHADOW, bool STATS, bool INST = false>
 __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMax, int* __restrict__ stack,
                          Best& B, Stats& st) {
     B = Best{tMax, -1, -1, false};
-    RayF rf = INST ? make_rayf(o, d) : make_rayf_t(S, o, d);
+    RayF rf = make_rayf(o, d);
     float tlim = f_tlim(tMax);
     int sp = 0;
     int node = 0;
@@ -1166,8 +905,7 @@ __device__ bool traverse(const SceneView& S, DV o, DV d, double tMin, double tMa
         // ---- internal nodes ----
         while (node >= 0) {
             if (STATS) st.nodes++;
-            if constexpr (INST) node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
-            else node = node_step<false, SHADOW>(S.tnodes, node, rf, tlim, stk, sp);
+            node = node_step<false, SHADOW>(S.nodes, node, rf, tlim, stk, sp);
             if (INST) node = inst_frame(S, node, inst, inst_sp, sp, o, d, rf);
         }
         if (node == MFX_TRAV_EXIT) return B.found;

@@ -11,7 +11,7 @@
 //   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
 //   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (a lit vertex recorded) or FREE (none)
 //   MISS stays: a finished path (its depth word holds the lit vertices; k_resolve folds it), black
-//   for a camera ray's MISS | FRESH (MFX_MISS_IN_PLACE; else k_shadow rewrites it DONE / FREE)
+//   for a camera ray's MISS | FRESH
 // A path's radiance is not summed forward. Each vertex v records the operands of its BRDF factor
 // c_v = col (the cosine ei and the material) and, when its shadow ray reaches the light, those of
 // its direct term a_v = l / pdf_li (the cosine cs and the solid-angle factor), and k_resolve
@@ -39,7 +39,6 @@
 #define WF_DONE 8   // finished with a lit vertex: k_resolve folds its vertices and adds them to its pixel
 #define WF_STATE_MASK 15
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
-#define WF_OCT_SHIFT 28   // WF_NEED_EXT state word: the ray's direction octant << WF_OCT_SHIFT (MFX_OCTANT_SORT)
 // depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
 // shadow ray reached the light); so at most WF_MAX_VERTS vertices (max_depth < WF_MAX_VERTS)
 #define WF_MAX_VERTS 16
@@ -57,35 +56,30 @@
                     // holds the others, and the host's sums add these into it)
 #define WF_CTR_ITER 18
 #define WF_ITER_CTRS 6
-// control words (unsigned long long) in WfParams.ctl
-#define WF_CTL_EXT 0               // [WF_SHARDS] k_extend slot-chunk heads
-#define WF_CTL_SHD (WF_SHARDS)     // [WF_SHARDS] k_shadow slot-chunk heads
-#define WF_NCTL (2 * WF_SHARDS)
+// control words (unsigned long long) in WfParams.ctl. Shard g's counter of each array sits at
+// [g * WF_HS]: device-scope atomics execute at the memory side one at a time per line, so each
+// shard's counter has lines of its own (adjacent counters shared 4 lines between 64 shards, and the
+// wave convoys at the end of every launch serialized on them)
+#ifndef WF_HS
+#define WF_HS 32  // unsigned long longs from one shard's counter to the next (256 B)
+#endif
+#define WF_CTL_EXT 0                       // [WF_SHARDS * WF_HS] k_extend slot-chunk heads
+#define WF_CTL_SHD (WF_SHARDS * WF_HS)     // [WF_SHARDS * WF_HS] k_shadow slot-chunk heads
+#define WF_NCTL (2 * WF_SHARDS * WF_HS)
 // the ray queues' shard counts sit on either side of the heads, so one memset per iteration clears
 // the heads and the next queue's counts: [WF_CTL_Q0 | heads | WF_CTL_Q1], P.ctl = the heads
-#define WF_CTL_Q0 (-WF_SHARDS)
+#define WF_CTL_Q0 (-WF_SHARDS * WF_HS)
 #define WF_CTL_Q1 (WF_NCTL)
-#define WF_CTL_ALLOC (WF_NCTL + 2 * WF_SHARDS)
+#define WF_CTL_ALLOC (WF_NCTL + 2 * WF_SHARDS * WF_HS)
 
 // A vertex record's material: 16 bits (k_resolve reads every vertex level's array nearly whole, so
 // its bytes are the kernel's cost); scenes are limited to 65,536 materials (mfx_create checks).
-#ifndef MFX_VMAT16
-#define MFX_VMAT16 1
-#endif
-#if MFX_VMAT16
 typedef uint16_t WfMat;
 #define WF_MAT_MAX 65536
-#else
-typedef int32_t WfMat;
-#define WF_MAT_MAX 0x7fffffff
-#endif
 
 struct WfParams {
     // scene
     const MfxNode* nodes;
-    const MfxTNode* tnodes; // the per-lane traversal's nodes of a flat scene (MFX_WIDE: the BVH8; else == nodes)
-    MfxWideXf wx;           // their frame (MfxNode8H)
-    const MfxTri32* tri32;  // FP32 triangle copies per slot (MFX_LEAF_SCREEN32)
     const MfxSlot* slots;
     const int32_t* slot_ref;
     const uint8_t* ref_blob;
@@ -116,13 +110,13 @@ struct WfParams {
     // k_resolve reads). k_shadow appends the paths that continue to the next queue (n*), so the
     // sparse later bounces read and write dense memory instead of scattered slots.
     const int32_t* qslot;             // entry -> slot (null: entry = slot, the pool itself)
-    const unsigned long long* qcount; // [WF_SHARDS] entries of each shard range of this iteration's queue (null: the pool)
+    const unsigned long long* qcount; // [WF_SHARDS * WF_HS] entries of each shard range of this iteration's queue (null: the pool)
     int32_t *fstate, *fdepth;         // the slot pool's state / depth words (== state / depth in place)
     double *nox, *noy, *noz, *ndx, *ndy, *ndz;  // the next queue (null: continue in place)
     uint64_t* nkey;
     uint32_t* nrn;
     int32_t *ndepth, *nstate, *nslot;
-    unsigned long long* ncount;       // [WF_SHARDS] its counts (beside ctl; zeroed with the heads)
+    unsigned long long* ncount;       // [WF_SHARDS * WF_HS] its counts (beside ctl; zeroed with the heads)
     // control
     unsigned long long* ctl;              // [WF_NCTL]
     unsigned long long* counters;         // [WF_SHARDS][WF_NCTR] ray / traversal counters
@@ -178,7 +172,7 @@ struct WfQueue {
     uint64_t* key;
     uint32_t* rn;
     int32_t *depth, *state, *slot;
-    unsigned long long* count;  // [WF_SHARDS]
+    unsigned long long* count;  // [WF_SHARDS * WF_HS]
 };
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels (ev may be null)
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,

@@ -39,20 +39,8 @@
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 
 
-#ifndef MFX_MISS_IN_PLACE
-#define MFX_MISS_IN_PLACE 1  // k_shadow leaves the pool's MISS words as they are; k_resolve reads them
-#endif
-
 #ifndef MFX_SHADOW_ORDER
 #define MFX_SHADOW_ORDER 1  // shadow rays' child order: 0 near-first, 1 far-first (by exit distance)
-#endif
-
-#ifndef MFX_OCTANT_SORT
-#define MFX_OCTANT_SORT 0  // 1: k_extend's pending extension rays grouped by direction octant (r02ae: -1 to -2 %)
-#endif
-
-#ifndef MFX_SPECULATIVE
-#define MFX_SPECULATIVE 0  // 1: postpone a lane's first leaf and keep stepping (trav_step)
 #endif
 
 #ifndef MFX_NODE_LANES_MIN
@@ -118,7 +106,7 @@ static_assert(WF_SHARDS == 64, "shard masks are one bit per lane of a wave");
 // again. This replaces walking the shards with one returning atomic each, which cost every wave
 // up to 64 serialized round trips at the end of each kernel.
 __device__ __forceinline__ uint64_t open_shards(const unsigned long long* ctr, int cap) {
-    const unsigned long long v = __hip_atomic_load(ctr + lane_id(), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long v = __hip_atomic_load(ctr + lane_id() * WF_HS, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return __ballot((int64_t)v < (int64_t)cap);
 }
 
@@ -128,9 +116,13 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
     return (home + __builtin_ctzll(r)) & (WF_SHARDS - 1);
 }
 
+#ifndef WF_SPREAD
+#define WF_SPREAD 1  // a wave whose shard closed picks the next open shard from a per-wave pseudo-random start
+#endif
 struct Scanner {
     int win_next, win_end, shard;
     bool exhausted;
+    uint32_t spread;  // WF_SPREAD: the wave's pseudo-random walk over the shards
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
     // work are skipped with no further memory round trip. Slots of a taken chunk change only
@@ -147,21 +139,29 @@ struct Scanner {
         if (exhausted) return false;
         while (true) {
             unsigned long long c = 0;
-            if (lane_id() == 0) c = atomicAdd(heads + shard, (unsigned long long)chunk);
+            if (lane_id() == 0) c = atomicAdd(heads + shard * WF_HS, (unsigned long long)chunk);
             c = __shfl(c, 0);
-            const int cap = qcount ? (int)qcount[shard] : shard_size;
+            const int cap = qcount ? (int)qcount[shard * WF_HS] : shard_size;
             if ((int64_t)c < cap) {
                 win_next = shard * shard_size + (int)c;
                 win_end = shard * shard_size + min((int)c + chunk, cap);
                 fill(state);
                 return true;
             }
-            const uint64_t open = open_shards(heads, qcount ? (int)qcount[lane_id()] : shard_size);
+            const uint64_t open = open_shards(heads, qcount ? (int)qcount[lane_id() * WF_HS] : shard_size);
             if (open == 0) {
                 exhausted = true;
                 return false;
             }
-            shard = next_open(open, shard);
+            // The waves of one home shard would all move to the same next open shard, and near a
+            // launch's end every wave to the last few, one memory-side atomic after another: each
+            // wave instead starts its search at its own pseudo-random shard
+            if (WF_SPREAD) {
+                spread = spread * 0x9e3779b1u + 0x7f4a7c15u;
+                shard = next_open(open, (int)(spread >> 26));
+            } else {
+                shard = next_open(open, shard);
+            }
         }
     }
     __device__ __forceinline__ void fill(const int32_t* __restrict__ state) {
@@ -205,8 +205,6 @@ struct Trav {
     int node, sp;
     int inst;   // two-level scenes: the instance whose template the lane is in (-1: the world)
     int inst_sp;  // and the stack depth at which it entered (entries below belong to the world)
-    int pleaf;  // MFX_SPECULATIVE: a postponed leaf's code (-1: none)
-    int pbase;  // and the slot base of its frame (two-level scenes)
 };
 
 __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV d, double tmax) {
@@ -218,17 +216,13 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.node = 0;
     T.inst = -1;
     T.inst_sp = 0;
-    T.pleaf = -1;
-    T.pbase = 0;
 }
 
-// one node step of the per-lane traversal: the BVH4 in two-level scenes, else the flat scene's
-// traversal image (MfxTNode)
-template <bool SHADOW, bool INST, typename ST>
+// one node step of the per-lane traversal (BVH4; shadow rays far-first)
+template <bool SHADOW, typename ST>
 __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, const RayF& rf, float tlim, const ST& stack,
                                               int& sp, TopNodes tn) {
-    if constexpr (INST) return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
-    else return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.tnodes, node, rf, tlim, stack, sp, tn);
+    return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
@@ -243,52 +237,15 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
     // the FP32 ray and the node-test limit are recomputed each round (the same values) rather than
     // held through the leaf tests: fewer live registers, fewer spills (+1 to +5 %)
-    rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf_t(S, T.o, T.d);
+    rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
     const float tlim = f_tlim(T.B.t);  // the query's tMax until the first hit, then the best t
-#if MFX_SPECULATIVE
-    // Speculative while-while (Aila & Laine 2009): a lane that reaches a leaf postpones it and keeps
-    // stepping nodes until it reaches a second one, so the node loop and the leaf tests run with
-    // more lanes busy. Results are unchanged: the leaf semantics are order-independent (beats()),
-    // the postponed leaf only culls later (closest hits: a few more node visits). Measured (r02ad):
-    // C2 -5 %, C4 -4 %, C3 +2.5 %; off.
-    while (true) {
-        if (T.node >= 0) {
-            if (STATS) st.nodes++;
-            if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;
-            T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
-            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
-        }
-        if (T.node < 0 && T.node != MFX_TRAV_EXIT && T.pleaf < 0) {  // postpone the leaf, pop the next entry
-            T.pleaf = ~T.node;
-            T.pbase = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
-            if (T.sp == 0) {
-                T.node = MFX_TRAV_EXIT;
-            } else {
-                T.node = stack.get(T.sp - 1, stack.deep(T.sp));
-                --T.sp;
-            }
-            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
-        }
-        if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
-    }
-    DIAG_MARK(dg, node, diag);
-    if (T.pleaf >= 0) {
-        const bool better = leaf_hit<SHADOW, STATS>(S, T.pleaf, T.o, T.d, 1e-6, T.tmax64, T.B, st, T.pbase);
-        T.pleaf = -1;
-        if (SHADOW && better) {
-            T.B.found = true;
-            return true;
-        }
-    }
-    return T.node == MFX_TRAV_EXIT;
-#else
     while (T.node >= 0) {
         if (STATS) st.nodes++;
 #ifdef MFX_DIAG_OCCLUSION
         if (STATS && !SHADOW && T.B.found) st.after_nodes++;
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = trav_node_step<SHADOW, INST>(S, T.node, rf, tlim, stack, T.sp, tn);
+        T.node = trav_node_step<SHADOW>(S, T.node, rf, tlim, stack, T.sp, tn);
         if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
@@ -312,7 +269,6 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     T.node = stack.get(T.sp - 1, stack.deep(T.sp));
     --T.sp;
     return false;
-#endif
 }
 
 // Path index of this generation -> (sample, 8x8 pixel tile, pixel), sample-major and
@@ -354,11 +310,9 @@ struct PendShd {
     }
 };
 
-#ifndef MFX_KEY_RECOMPUTE
 // k_shadow derives a camera ray's path key from its slot (as k_extend did) instead of reading it:
 // k_extend stores no keys, and only continuing paths get theirs stored, at their first vertex
-#define MFX_KEY_RECOMPUTE 1  // r02bs: C2 +0.9 to +2.5 %, C3 +2.5 to +4.3 %, C4 +0.5 to +0.8 %; 2 (every vertex) r03av: -0.3 to -1.2 %
-#endif
+// (r02bs: C2 +0.9 to +2.5 %, C3 +2.5 to +4.3 %; derived at every vertex, r03av: -0.3 to -1.2 %)
 #ifndef MFX_HEMI_WAVE
 #define MFX_HEMI_WAVE 1  // k_shadow: the rejection sampler's stragglers' trials spread over the whole wave
 #endif
@@ -447,7 +401,7 @@ template <bool STATS, bool SPILL, bool INST, bool Q>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
-    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_ext);
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
@@ -457,11 +411,12 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
     int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes, P.wx};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
+    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int s = 0;
@@ -494,33 +449,12 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                         take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
                     }
                     const uint64_t tm = __ballot(take);
-                    // entry: slot | direction octant << 28 (extension rays) | camera-ray flag << 31
-                    if (take)
-                        pend[n + __popcll(tm & lanes_below())] =
-                            sj == WF_FREE ? (j | (int)0x80000000) : (j | (((sj >> WF_OCT_SHIFT) & 7) << 28));
+                    // entry: slot | camera-ray flag << 31
+                    if (take) pend[n + __popcll(tm & lanes_below())] = sj == WF_FREE ? (j | (int)0x80000000) : j;
                     n += __popcll(tm);
                     sc.advance(P.state);
                 }
                 wave_lds_sync();
-#if MFX_OCTANT_SORT
-                // extension rays grouped by direction octant (a stable counting sort of the list):
-                // lanes that take entries together trace rays of one octant
-                if (!P.start) {
-                    const int e0 = lane < n ? pend[lane] : 0, e1 = lane + 64 < n ? pend[lane + 64] : 0;
-                    const int k0 = (e0 >> 28) & 7, k1 = (e1 >> 28) & 7;
-                    int d0 = 0, d1 = 0, off = 0;
-                    for (int k = 0; k < 8; ++k) {
-                        const uint64_t b0 = __ballot(lane < n && k0 == k), b1 = __ballot(lane + 64 < n && k1 == k);
-                        if (k0 == k) d0 = off + __popcll(b0 & lanes_below());
-                        if (k1 == k) d1 = off + __popcll(b0) + __popcll(b1 & lanes_below());
-                        off += __popcll(b0) + __popcll(b1);
-                    }
-                    wave_lds_sync();
-                    if (lane < n) pend[d0] = e0;
-                    if (lane + 64 < n) pend[d1] = e1;
-                    wave_lds_sync();
-                }
-#endif
                 pend_lo = 0;
                 pend_hi = n;
                 if (n == 0) break;  // every chunk scanned
@@ -529,7 +463,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
                 const int e = pend[pend_lo + rank];
-                s = e & 0x0fffffff;
+                s = e & 0x7fffffff;
                 fresh = e < 0;
                 DV o, d;
                 if (fresh) {
@@ -547,10 +481,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
                     o = ld3(CAM.position);
                     d = vnormalize(vsub(target, o));
-                    // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH)
-#if !MFX_KEY_RECOMPUTE
-                    P.key[s] = key;
-#endif
+                    // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH); the
+                    // key is derived again by k_shadow (stored only for a path that continues)
                     c_primary++;
                 } else {
                     o = dv(P.ox[s], P.oy[s], P.oz[s]);
@@ -626,10 +558,11 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     uint64_t* stm = (uint64_t*)lds_all + wave * P.stack_size;  // per wave: stack masks, then nodes
     int* stk = (int*)((uint64_t*)lds_all + 4 * P.stack_size) + wave * P.stack_size;
     uint32_t* red = (uint32_t*)((int*)((uint64_t*)lds_all + 4 * P.stack_size) + 4 * P.stack_size);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0, P.tnodes, P.wx};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
+    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
     while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr)) {
@@ -684,7 +617,7 @@ template <bool STATS, bool SPILL, int WAVES, bool INST, bool Q>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
-    load_top_nodes((float4*)lds_all, INST ? (const void*)P.nodes : (const void*)P.tnodes, P.ntop_shd);
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
@@ -695,12 +628,13 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.tri32, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, P.tnodes, P.wx};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
+    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     int nshade = 0;      // wave-uniform: hits listed for shading
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
@@ -732,7 +666,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const int sj = sc.word();
                     const int sv = sj & WF_STATE_MASK;
                     const bool hit = (sv & ~WF_FRESH) == WF_HIT;
-#if MFX_MISS_IN_PLACE
                     // a pool slot's miss stays as k_extend wrote it: k_resolve takes MISS as finished
                     // (its depth word holds the lit vertices) and a camera ray's MISS | FRESH as black
                     if (Q && P.qslot && sv == WF_MISS) {  // a queue entry: its slot finishes (no lit vertex: stays unfinished)
@@ -743,22 +676,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                             P.fstate[jr] = WF_DONE;
                         }
                     }
-#else
-                    if (sv == (WF_MISS | WF_FRESH)) {
-                        P.state[j] = WF_FREE;
-                    } else if (sv == WF_MISS) {
-                        if (Q && P.qslot) {  // a queue entry: its slot finishes (a path with no lit vertex stays unfinished)
-                            const int dw = P.depth[j];
-                            if (dw >> WF_LIT_SHIFT) {
-                                const int jr = P.qslot[j];
-                                P.fdepth[jr] = dw;
-                                P.fstate[jr] = WF_DONE;
-                            }
-                        } else {
-                            P.state[j] = WF_DONE;
-                        }
-                    }
-#endif
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
@@ -791,10 +708,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
                     else nm = ld3(sh.n);
                     mat = sh.material;
-#if MFX_KEY_RECOMPUTE
-                    // the key k_extend derived for the path's camera ray (same expressions): at the
-                    // first vertex (MFX_KEY_RECOMPUTE 1) or at every one (2: keys are never stored)
-                    if (first || MFX_KEY_RECOMPUTE == 2) {
+                    // the key k_extend derived for the path's camera ray (same expressions)
+                    if (first) {
                         int x, y;
                         int64_t smp;
                         path_pixel(P, P.path_base + jr, x, y, smp);
@@ -803,9 +718,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     } else {
                         key = P.key[j];
                     }
-#else
-                    key = P.key[j];
-#endif
                     rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
                 }
                 // the depth -1 query's result is discarded (Integrators.fs:109): never traced
@@ -820,7 +732,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                         const int gl = __shfl(g, __builtin_ctzll(rem));
                         const uint64_t gm = __ballot(cn && g == gl);
                         unsigned long long base = 0;
-                        if (lane == __builtin_ctzll(gm)) base = atomicAdd(P.ncount + gl, (unsigned long long)__popcll(gm));
+                        if (lane == __builtin_ctzll(gm)) base = atomicAdd(P.ncount + gl * WF_HS, (unsigned long long)__popcll(gm));
                         base = __shfl(base, __builtin_ctzll(gm));
                         if (cn && g == gl) qi = gl * shard_size + (int)base + __popcll(gm & lanes_below());
                         rem &= ~gm;
@@ -875,21 +787,17 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                                            // state are written after the shadow ray)
                         P.nox[qi] = hp.x; P.noy[qi] = hp.y; P.noz[qi] = hp.z;
                         P.ndx[qi] = wi.x; P.ndy[qi] = wi.y; P.ndz[qi] = wi.z;
-                        if (MFX_KEY_RECOMPUTE != 2) P.nkey[qi] = key;
+                        P.nkey[qi] = key;
                         P.nrn[qi] = rn;
                         P.nslot[qi] = jr;
                     } else if (cn) {  // what the next vertex reads, in place
-#if MFX_KEY_RECOMPUTE == 1
                         if (first) P.key[j] = key;
-#endif
                         P.rn[j] = rn;
                         P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
                     }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
                     pd.slot[lane] = (Q && cn && P.ncount) ? qi : j;
-                    // bits 24..26: the next ray's direction octant (MFX_OCTANT_SORT)
-                    const int oct = (wi.x < 0. ? 1 : 0) | (wi.y < 0. ? 2 : 0) | (wi.z < 0. ? 4 : 0);
-                    pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff) | (oct << 24);
+                    pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
                     pd.v[4 * 64 + lane] = cs; pd.v[5 * 64 + lane] = solid;
@@ -972,7 +880,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             // continue with the next vertex's remaining depth; or finished: k_resolve folds the
             // recorded vertices (none lit: nothing to add, FREE)
             const int dwn = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-            const int need = WF_NEED_EXT | (((vflag >> 24) & 7) << WF_OCT_SHIFT);
+            const int need = WF_NEED_EXT;
             if (nq) {
                 P.ndepth[s] = dwn;
                 P.nstate[s] = need;
@@ -1140,7 +1048,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         int mask[U];
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            mask[u] = ((sw[u] & WF_STATE_MASK) == WF_DONE || (MFX_MISS_IN_PLACE && (sw[u] & WF_STATE_MASK) == WF_MISS))
+            mask[u] = ((sw[u] & WF_STATE_MASK) == WF_DONE || (sw[u] & WF_STATE_MASK) == WF_MISS)
                           ? (P.depth[jv[u]] >> WF_LIT_SHIFT) & 0xffff : 0;
         PathRec R[U];
 #pragma unroll
@@ -1270,7 +1178,7 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     unsigned long long* z = P.ctl;
     size_t nz = WF_NCTL;
     if (P.ncount) {
-        nz += WF_SHARDS;
+        nz += WF_SHARDS * WF_HS;
         if (P.ncount < P.ctl) z = P.ncount;
     }
     hipError_t e = hipMemsetAsync(z, 0, nz * sizeof(unsigned long long), st);

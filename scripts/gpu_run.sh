@@ -11,7 +11,7 @@
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
 #   diag:CFG             one MFX_DIAG_ITER=1 frame (per-iteration ray counts and stage times)
-#   dispatch:CFG         per-dispatch duration and HBM bytes of one frame (kernel trace + FETCH_SIZE and
+#   dispatch:CFG[:SPP]   per-dispatch duration and HBM bytes of one frame (kernel trace + FETCH_SIZE and
 #                        WRITE_SIZE passes, scripts/per_dispatch.py) -> dispatch_CFG.txt
 #   diagab:SCENE:SPP     per-iteration stage times of every build_variants/*.so (with its .env), 2 rounds
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
@@ -59,13 +59,15 @@ for step in "$@"; do
       MFX_DIAG_ITER=1 timeout -k 10 300 python3 bench.py --config $a1 --steps 1 --warmup 1 --no-cpu-baseline \
         --no-render-api --no-stats > $O/diag_$a1.json 2> $O/diag_$a1.txt ;;
     dispatch)
-      D=$R/$O/dispatch_$a1; mkdir -p $D
+      D=$R/$O/dispatch_$a1
       B="$R/bench.py --config $a1 --steps 1 --warmup 1 --no-cpu-baseline --no-stats --no-render-api"
+      [ -n "$a2" ] && B="$B --spp $a2" && D=${D}_$a2
+      mkdir -p $D
       (cd /tmp && export TMPDIR=/tmp &&
        timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $D/trace -o run -- python3 $B > $D/trace.log 2>&1 &&
        timeout -k 10 200 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $D/fetch -o run -- python3 $B > $D/fetch.log 2>&1 &&
        timeout -k 10 200 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $D/write -o run -- python3 $B > $D/write.log 2>&1)
-      python3 scripts/per_dispatch.py $D | tee $O/dispatch_$a1.txt ;;
+      python3 scripts/per_dispatch.py $D | tee $O/$(basename $D).txt ;;
     diagab)
       for round in 0 1; do
         for l in build_variants/*.so; do

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-dispatch view of a scripts/profile_traffic.sh directory (or any rocprofv3 output with a
 kernel-trace pass under trace/ and FETCH_SIZE / WRITE_SIZE passes under fetch/ and write/): for
-each trace kernel launch of the last frame, in order, its duration and HBM bytes (FETCH_SIZE x2 by
+each trace kernel launch of the last frame, in order, its duration, HBM bytes, start offset and the idle gap
+before it (FETCH_SIZE x2 by
 the gfx950 correction, WRITE_SIZE as reported). The wavefront's launches of one frame run
 k_camera, then (k_shadow, k_extend) per bounce, so the order names the bounce.
 Usage: per_dispatch.py DIR"""
@@ -39,7 +40,8 @@ def main(d):
         for r in csv.DictReader(open(tr)):
             k = short(r["Kernel_Name"])
             if k in KERNELS:
-                durs.append((int(r["Dispatch_Id"]), k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6))
+                durs.append((int(r["Dispatch_Id"]), k, (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6,
+                             int(r["Start_Timestamp"]), int(r["End_Timestamp"])))
         durs.sort()
     fetch = pmc(one(os.path.join(d, "fetch", "**", "*counter_collection.csv")), "FETCH_SIZE")
     write = pmc(one(os.path.join(d, "write", "**", "*counter_collection.csv")), "WRITE_SIZE")
@@ -50,13 +52,20 @@ def main(d):
 
     durs, fetch, write = last_frame(durs), last_frame(fetch), last_frame(write)
     n = max(len(durs), len(fetch), len(write))
-    print(f"{'#':>3} {'kernel':10} {'ms':>8} {'fetch GB':>9} {'write GB':>9}")
+    print(f"{'#':>3} {'kernel':10} {'ms':>8} {'fetch GB':>9} {'write GB':>9} {'start ms':>9} {'gap ms':>7}")
+    t0 = durs[0][3] if durs else 0
     for i in range(n):
         k = (durs[i][1] if i < len(durs) else fetch[i][1] if i < len(fetch) else write[i][1])
         ms = f"{durs[i][2]:8.3f}" if i < len(durs) else " " * 8
         fb = f"{2.0 * fetch[i][2] * 1024 / 1e9:9.3f}" if i < len(fetch) else " " * 9
         wb = f"{write[i][2] * 1024 / 1e9:9.3f}" if i < len(write) else " " * 9
-        print(f"{i:3d} {k:10} {ms} {fb} {wb}")
+        st = f"{(durs[i][3] - t0) / 1e6:9.3f}" if i < len(durs) else " " * 9
+        gp = f"{(durs[i][3] - durs[i - 1][4]) / 1e6:7.3f}" if 0 < i < len(durs) else " " * 7
+        print(f"{i:3d} {k:10} {ms} {fb} {wb} {st} {gp}")
+    if durs:
+        busy = sum(d[2] for d in durs)
+        span = (durs[-1][4] - durs[0][3]) / 1e6
+        print(f"frame span {span:.3f} ms, kernels busy {busy:.3f} ms, gaps {span - busy:.3f} ms")
 
 
 if __name__ == "__main__":

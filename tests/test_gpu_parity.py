@@ -14,7 +14,9 @@ from conftest import SEED, scene
 
 pytestmark = pytest.mark.gpu
 
-SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced@2l"]
+# spot16_instanced: the library's default flags (flattened, it fits the budget); @2l: two-level forced
+SCENES = ["two_spheres_plane", "cornell", "spot", "cube_cornell", "renault", "spot16", "spot16_instanced",
+          "spot16_instanced@2l"]
 
 
 def random_rays(arrays, n, rng, camera_frac=0.5):
@@ -104,6 +106,7 @@ def test_fp64_device_math_bit_exact(gpu):
     ("cube_cornell", 64, 36, 8),
     ("renault", 64, 36, 4),
     ("spot16", 64, 36, 4),
+    ("spot16_instanced", 64, 36, 4),
     ("spot16_instanced@2l", 64, 36, 4),
 ])
 @pytest.mark.parametrize("mode", ["wavefront", "megakernel"])
@@ -126,6 +129,21 @@ def test_image_parity(gpu, oracle, name, w, h, spp, mode):
     else:  # FP64 atomics add a pixel's paths in arrival order
         assert diff.max() <= 1e-12 * max(1.0, np.abs(ref).max()), diff.max()
     assert np.all(img[:, 3] == 1.0)
+
+
+def test_default_flags_two_level_when_over_budget(gpu, oracle, monkeypatch):
+    """An instanced scene over the flatten budget takes the two-level traversal with the default
+    flags (no MFX_F_TWO_LEVEL): images and ray counts still equal the oracle's on the expansion."""
+    from mafrixraytracing_amd.native import NativeContext
+    monkeypatch.setenv("MFX_FLATTEN_MAX_BYTES", "1024")
+    a = scene("spot16_instanced", 48, 27)
+    ref, st = oracle.OracleScene(a).sample(2, SEED, with_stats=True)
+    with NativeContext(a, seed=SEED) as ctx:
+        assert ctx.instancing_info()["instances"] == 16  # two-level
+        img = ctx.sample(2)
+        counts = ctx.ray_counts()
+    assert counts[0] == st[0] and counts[1] == st[1] and counts[2] == st[2], (counts[:3], st[:3])
+    assert np.array_equal(img, ref)
 
 
 def test_successive_sample_calls_continue_the_stream(gpu, oracle):

@@ -151,3 +151,13 @@ def test_flatten_budget_selects_two_level(c5, monkeypatch):
     assert abi.build_instanced_info(inst)["instances"] == 0
     monkeypatch.setenv("MFX_FLATTEN_MAX_BYTES", str(93698 * 512 - 1))
     assert abi.build_instanced_info(inst)["instances"] == 16
+
+
+def test_flatten_and_two_level_flags_are_rejected(c5):
+    """MFX_F_FLATTEN and MFX_F_TWO_LEVEL contradict each other: the library refuses the pair
+    instead of quietly picking one."""
+    _, inst = c5
+    with pytest.raises(abi.MfxError, match="exclude each other"):
+        abi.build_instanced_info(inst, flags=abi.MFX_F_FLATTEN | abi.MFX_F_TWO_LEVEL)
+    assert abi.build_instanced_info(inst, flags=abi.MFX_F_TWO_LEVEL)["instances"] == 16
+    assert abi.build_instanced_info(inst, flags=abi.MFX_F_FLATTEN)["instances"] == 0
