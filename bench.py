@@ -46,6 +46,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+XGMI_LINK_GBS = 153.0  # one xGMI link of MI355X (7 per GPU); the reduce model assumes one ring over one link
 SPOT_SCENE = os.path.join(ROOT, "scenes", "spot.xml")
 # BASELINE.json configs: scene, spp per GPU per step at N = 1, label. C4 and C5 are
 # 8-GPU configs; at N = 1 a step is one GPU's share of them (256/8 and 512/8 spp).
@@ -225,13 +226,22 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
                         "to pageable host memory, synchronize"}
 
 
+def xgmi_reduce_ms(nbytes, n):
+    """Modeled N-rank sum-reduce of an nbytes buffer to one rank: a ring reduce-scatter then a gather
+    to the root over one xGMI link per hop, each moving (N - 1) / N of the buffer; RCCL's rings over
+    several of the 7 links only make it faster, so this bounds the transfer from above."""
+    return 2.0 * nbytes * (n - 1) / n / (XGMI_LINK_GBS * 1e9) * 1e3
+
+
 def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=3, flags=0):
     """One GPU's share of a strong-scaled job, measured on this GPU: the config's spp split over N
     GPUs is spp / N samples per GPU per step (C2: 32 / 16 / 8). Timed per N: the share's trace
     (clear + trace + sync, the step's fixed per-generation costs included), and the library's RCCL
     reduce of the FP64 accumulator on a devices=[0] context (a 1-rank communicator: its launch and
-    local cost; the xGMI transfer of an N-rank reduce is not in it). predicted_efficiency =
-    (t_1GPU / N) / (t_share + t_reduce): what the N-GPU strong run can reach at most."""
+    local cost). The N-rank reduce's xGMI transfer is modeled (xgmi_reduce_ms). predicted_efficiency
+    = (t_1GPU / N) / (t_share + t_reduce_modeled), the reduce not overlapped; with the bench's
+    pipelined frames (frame k's reduce under frame k + 1's trace) it is (t_1GPU / N) / max(t_share,
+    t_reduce_modeled): predicted_efficiency_pipelined."""
     from mafrixraytracing_amd.native import NativeContext
     out = {}
     with NativeContext(arrays, seed=seed, devices=[0], flags=flags) as rc:
@@ -244,6 +254,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=3, flags=0):
             rc.accum_reduce()
         rc.sync()
         t_red = (time.perf_counter() - t0) / n_red * 1e3
+    acc_bytes = 3 * 8 * arrays.width * arrays.height
     with NativeContext(arrays, seed=seed, flags=flags) as ctx:
         for n in (2, 4, 8):
             share = spp // n
@@ -260,13 +271,17 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=3, flags=0):
                 c = ctx.ray_counts()
                 rays += c[0] + c[1] + c[2]
             t = (time.perf_counter() - t0) / steps * 1e3
+            t_x = max(t_red, xgmi_reduce_ms(acc_bytes, n))
             out[str(n)] = {"spp_per_gpu": share, "ms_per_step": round(t, 3),
                            "mrays_per_s_per_gpu": round(rays / steps / (t / 1e3) / 1e6, 2),
                            "vs_full_step_rate": round(rays / steps / (t / 1e3) / 1e6 / value_1gpu, 4),
-                           "predicted_efficiency": round((ms_1gpu / n) / (t + t_red), 4)}
+                           "reduce_ms_modeled": round(t_x, 4),
+                           "predicted_efficiency": round((ms_1gpu / n) / (t + t_x), 4),
+                           "predicted_efficiency_pipelined": round((ms_1gpu / n) / max(t, t_x), 4)}
     return {"reduce_ms_1rank": round(t_red, 4), "shares": out,
             "note": "per-GPU share of --scaling strong at N GPUs, measured on one GPU; reduce_ms_1rank is the "
-                    "devices=[0] RCCL reduce (no xGMI transfer)"}
+                    "devices=[0] RCCL reduce (no xGMI transfer); reduce_ms_modeled = max(that, a one-link ring "
+                    f"reduce of the {acc_bytes / 1e6:.1f} MB FP64 accumulator at {XGMI_LINK_GBS:.0f} GB/s)"}
 
 
 def main():
@@ -383,18 +398,48 @@ def main():
     elapsed = time.perf_counter() - t0
     if args.api == "render":
         elapsed = call_s
-    if use_dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+
+    def job_max_sum(el, ry):  # the slowest rank's time, the job's rays
+        if not use_dist:
+            return el, ry
+        t = torch.tensor([el], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        r = torch.tensor([rays], dtype=torch.float64, device=f"cuda:{local}")
+        r = torch.tensor([ry], dtype=torch.float64, device=f"cuda:{local}")
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
-        rays_all = float(r.item())
-    else:
-        rays_all = rays
+        return float(t.item()), float(r.item())
+
+    elapsed, rays_all = job_max_sum(elapsed, rays)
+
+    strong = None
+    if ngpu > 1 and args.api == "batch" and args.scaling == "weak":
+        # the same job strong-scaled, in the same run: the config's spp per step split over the N GPUs
+        # (each traces about spp / N), timed like the weak steps (barriers, max over ranks)
+        def strong_step(k):
+            base = (args.warmup + args.steps) * spp_step + k * args.spp
+            if pr is not None:
+                pr.frame(args.spp, base, all_ranks=backend == "gloo")
+            else:
+                ctx.accum_clear()
+                ctx.trace_accumulate(args.spp, base)
+                ctx.accum_reduce()
+                ctx.sync()
+        strong_step(0)
+        barrier()
+        ts, srays = time.perf_counter(), 0.0
+        for k in range(args.steps):
+            strong_step(1 + k)
+            c = ctx.ray_counts()
+            srays += c[0] + c[1] + c[2]
+        barrier()
+        s_el, s_rays = job_max_sum(time.perf_counter() - ts, srays)
+        strong = {"scaling": "strong", "global_spp_per_step": args.spp, "spp_per_gpu": args.spp / ngpu,
+                  "value": round(s_rays / s_el / 1e6, 2), "unit": "Mrays/s", "steps": args.steps,
+                  "ms_per_step": round(s_el / args.steps * 1e3, 3), "rays_per_step": s_rays / args.steps,
+                  "note": "the config's spp per step split over the GPUs (whole-job Mrays/s); the line's value is "
+                          "the weak-scaled job"}
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
                 for k in ("total_ms", "camera_ms", "extend_ms", "camera_launches", "shadow_ms", "iterations", "launches",
-                          "generations")}
+                          "generations", "tail_ms", "tail_launches", "tail_ext_rays", "tail_shadow_rays")}
 
     result = None
     # launches per timed unit: a step, or (--api render) one 1-spp call
@@ -490,8 +535,10 @@ def main():
                         "peak_case": tdroof["peak"]["case"],
                         "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
 
-            def kernel_roofline(kname, kms, krays, launches, bray):
+            def kernel_roofline(kname, kms, krays, launches, bray, bytes_total=None):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
+                if bytes_total is not None:  # a kernel tracing both kinds of ray (k_tail)
+                    bray = bytes_total / krays if krays else 0.0
                 achieved = krays * bray / (kms / 1e3) / 1e9
                 traffic = None
                 if tdata:  # rocprof names the instance: k_shadow<false> or k_shadow<false, SPILL, ...>;
@@ -534,11 +581,18 @@ def main():
                                   "own BVH2 walk, while a packet fetches each node and slot once for its 64 rays "
                                   "(scalar loads), so the index can exceed 1; the TD object is the measured roof")
                     ks.append((stage_ms["camera_ms"], kc))
-                ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt
+                t_ext, t_shd = stage_ms["tail_ext_rays"], stage_ms["tail_shadow_rays"]  # k_tail's, per step
+                ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt - t_ext
                 ext_ms = stage_ms["extend_ms"] - stage_ms["camera_ms"]
                 ks.append((ext_ms, kernel_roofline("k_extend<false>", ext_ms, ext_rays, launches - cl, bc)))
                 ks.append((stage_ms["shadow_ms"], kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"],
-                                                                  (rays - closest_rays) / nt, launches, bs)))
+                                                                  (rays - closest_rays) / nt - t_shd, launches, bs)))
+                if stage_ms["tail_launches"] > 0:
+                    kt = kernel_roofline("k_tail<false>", stage_ms["tail_ms"], t_ext + t_shd, stage_ms["tail_launches"],
+                                         0.0, bytes_total=t_ext * bc + t_shd * bs)
+                    kt["note"] = ("the paths' bounces after the ray-queue start, extension and shadow rays of one lane "
+                                  "each; bytes priced at the closest / shadow B_ray of its rays")
+                    ks.append((stage_ms["tail_ms"], kt))
                 ks.sort(key=lambda x: -x[0])
                 roofline = dict(ks[0][1])
                 roofline["other_kernels"] = [k for _, k in ks[1:]]
@@ -595,6 +649,8 @@ def main():
                        "parallelism": par},
             "roofline": roofline, "render_api": rapi, "sample_api": sapi, "strong_share": share, "cpu_baseline": cpu,
         }
+        if strong is not None:
+            result["strong"] = strong
         print(json.dumps(result), file=json_out, flush=True)
     ctx.close()
     if use_dist:

@@ -137,6 +137,7 @@ struct mfx_ctx {
     WfQueue wq[2]{};
     int wf_queue_from = MFX_RAY_QUEUE ? -2 : -1;  // -2: automatic (wf_queue_auto)
     int wf_queue_auto = 1;  // from the last trace's live paths per iteration (note_live); 1 before any
+    bool wf_auto_read = false;  // the first wavefront trace's counters have been read for wf_queue_auto
     int32_t wf_qchunk = 256;  // entries per chunk fetch on a ray queue (MFX_QCHUNK)
     // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
     // slots, 15 GB) runs the frame as one generation: no kernel ends with a partly filled pool
@@ -146,6 +147,15 @@ struct mfx_ctx {
     unsigned long long* d_wfctl = nullptr;  // [WF_CTL_ALLOC] queue 0 counts, chunk heads, queue 1 counts
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
+    int it_per_gen = 0;                     // and per generation
+    // MFX_TAIL (default on): once a trace moves its paths to queue 0, one k_tail launch per generation
+    // runs them to their ends instead of the remaining bounce-synchronous iterations
+    bool wf_tail = true;
+    int wf_tail_grid = 0;
+    int32_t wf_tchunk = 256;                // queue entries per k_tail chunk fetch (MFX_TCHUNK)
+    std::vector<hipEvent_t> tail_ev;        // per generation: k_tail start, end
+    int tail_recorded = 0;                  // k_tail launches of the last trace with events
+    int tail_iter = -1;                     // the first iteration k_tail ran (-1: none)
     int generations = 0;
     bool mega_last = false;
     bool cam_last = false;  // the last wavefront trace ran its camera rays as packets (k_camera)
@@ -236,6 +246,8 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->tail_ev)
+        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -307,6 +319,8 @@ static int ctx_setup(mfx_ctx* c) {
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* qf = getenv("MFX_QUEUE_FROM")) c->wf_queue_from = MFX_RAY_QUEUE ? std::max(-2, atoi(qf)) : -1;
     if (const char* qc = getenv("MFX_QCHUNK")) c->wf_qchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(qc) / 64 * 64));
+    if (const char* tc = getenv("MFX_TCHUNK")) c->wf_tchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(tc) / 64 * 64));
+    if (const char* te = getenv("MFX_TAIL")) c->wf_tail = atoi(te) != 0;
     if (const char* rq = getenv("MFX_RAY_QUEUE")) {
         if (atoi(rq) == 0) c->wf_queue_from = -1;
     }
@@ -411,6 +425,12 @@ static int ctx_setup(mfx_ctx* c) {
         }
     }
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
+    {  // k_tail: the LDS of k_shadow's stack share and top nodes minus its lists, the register budget of its build
+        int tb = 0;
+        CK(mfx_tail_occupancy(c->wf_stack_lds_shd, c->wf_stack_lds_shd < c->stack_size, c->wf_ntop_shd, ninst,
+                              c->wf_shadow_waves, &tb));
+        c->wf_tail_grid = prop.multiProcessorCount * std::max(1, std::min(tb, 8));
+    }
     {  // deep traversal-stack entries of every lane of the larger grid
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
         const int deep = c->stack_size - std::min(c->wf_stack_lds_ext, c->wf_stack_lds_shd);
@@ -706,6 +726,8 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nmat = (int32_t)(c->host.albedo.size() / 3);
 }
 
+static void note_live(mfx_ctx* c, const unsigned long long* h);
+
 // The wavefront pipeline. The frame's path indices (sample-major, 8x8 tiles) are cut into
 // generations of at most wf_pool_max paths; slot j of a generation holds path path_base + j. A
 // generation is max_depth + 1 iterations of (k_extend, k_shadow) — the primary ray and the
@@ -755,12 +777,37 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.cam_grid = c->host.inst.empty() ? c->wf_cam_grid : 0;
     if (own_events) c->cam_last = P.cam_grid > 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
-    const int iters = (int)ngen * (P.max_depth + 1);
+    // MFX_TAIL: the iterations after the queue start run as one k_tail launch on queue 0
+    const int qf = c->wf_queue_from == -2 ? c->wf_queue_auto : c->wf_queue_from;
+    const bool tail = c->wf_tail && qf >= 0 && qf < P.max_depth;
+    const int per_gen = tail ? qf + 1 : P.max_depth + 1;  // bounce-synchronous iterations per generation
+    const int iters = (int)ngen * per_gen;
     while (own_events && (int)c->it_ev.size() < 3 * iters) {
         hipEvent_t e;
         HIPCHECK(hipEventCreate(&e));
         c->it_ev.push_back(e);
     }
+    while (own_events && tail && (int)c->tail_ev.size() < 2 * ngen) {
+        hipEvent_t e;
+        HIPCHECK(hipEventCreate(&e));
+        c->tail_ev.push_back(e);
+    }
+    // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
+    auto diag = [&](int64_t g, const char* what, int d, float fe, float fs) -> int {
+        HIPCHECK(hipStreamSynchronize(c->stream));
+        unsigned long long h[WF_NCTR * WF_SHARDS];
+        HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+        double r[WF_NCTR] = {0};
+        for (int k = 0; k < WF_SHARDS; ++k)
+            for (int q = 0; q < WF_NCTR; ++q) r[q] += (double)h[WF_NCTR * k + q];
+        for (int q = WF_CTR_ITER + 1; q < WF_CTR_ITER + WF_ITER_CTRS; ++q) r[1] += r[q];
+        fprintf(stderr, "gen %lld %s %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
+                " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g; cumulative traversal closest %.0f %.0f %.0f"
+                " shadow %.0f %.0f %.0f; scan %.4g shade %.4g\n", (long long)g, what, d,
+                r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9],
+                r[16], r[17]);
+        return MFX_OK;
+    };
     HIPCHECK(hipEventRecord(own_events ? c->ev0 : e0, c->stream));
     int it = 0;
     for (int64_t g = 0; g < ngen; ++g) {
@@ -770,7 +817,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
         P.total = std::min<int64_t>(gen_max, total - P.path_base);
         P.pool = (int32_t)((P.total + 4095) / 4096 * 4096);
         HIPCHECK(hipMemsetAsync(P.state, 0, sizeof(int32_t) * (size_t)P.pool, c->stream));
-        for (int d = 0; d <= P.max_depth; ++d, ++it) {
+        for (int d = 0; d < per_gen; ++d, ++it) {
             P.start = d == 0 ? 1 : 0;
             P.iter = d;
             wf_queue_views(c, P, d);
@@ -784,22 +831,29 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             HIPCHECK(hipEventRecord(ev[0], c->stream));
             HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, ev + 1));
             HIPCHECK(hipEventRecord(ev[2], c->stream));
-            if (c->diag_iter) {  // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
-                HIPCHECK(hipStreamSynchronize(c->stream));
-                unsigned long long h[WF_NCTR * WF_SHARDS];
-                HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-                double r[WF_NCTR] = {0};
-                for (int k = 0; k < WF_SHARDS; ++k)
-                    for (int q = 0; q < WF_NCTR; ++q) r[q] += (double)h[WF_NCTR * k + q];
-                for (int q = WF_CTR_ITER + 1; q < WF_CTR_ITER + WF_ITER_CTRS; ++q) r[1] += r[q];
+            if (c->diag_iter) {
                 float fe = 0.f, fs = 0.f;
                 HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
-                fprintf(stderr, "gen %lld iter %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
-                        " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g; cumulative traversal closest %.0f %.0f %.0f"
-                        " shadow %.0f %.0f %.0f; scan %.4g shade %.4g\n", (long long)g, d + 1,
-                        r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9],
-                        r[16], r[17]);
+                const int rc = diag(g, "iter", d + 1, fe, fs);
+                if (rc) return rc;
+            }
+        }
+        if (tail) {  // iterations qf + 1 .. max_depth: every path of queue 0 to its end
+            P.start = 0;
+            P.iter = qf + 1;
+            wf_queue_views(c, P, qf + 1);
+            P.ncount = nullptr;  // k_tail continues paths in their own entries: no next queue
+            P.chunk = c->wf_chunk_env ? chunk0 : c->wf_tchunk;
+            hipEvent_t* ev = own_events ? c->tail_ev.data() + 2 * g : nullptr;
+            if (ev) HIPCHECK(hipEventRecord(ev[0], c->stream));
+            HIPCHECK(mfx_wf_tail(P, c->wf_tail_grid, stats, c->stream));
+            if (ev) HIPCHECK(hipEventRecord(ev[1], c->stream));
+            if (ev && c->diag_iter) {
+                float ft = 0.f;
+                HIPCHECK(hipEventElapsedTime(&ft, ev[0], ev[1]));
+                const int rc = diag(g, "tail", qf + 2, ft, 0.f);
+                if (rc) return rc;
             }
         }
         wf_queue_views(c, P, -1);  // k_resolve reads the pool's final state and depth words
@@ -811,7 +865,20 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     }
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
+    if (c->wf_queue_from == -2 && !c->wf_auto_read) {
+        // The automatic queue start is taken from a trace's per-iteration counters. Read them once,
+        // after the context's first wavefront trace, so a caller that never polls the counters gets
+        // the same kernels as one that does (every later poll re-reads the same scene's shares).
+        unsigned long long h[WF_NCTR * WF_SHARDS];
+        HIPCHECK(hipMemcpyAsync(h, P.counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
+        HIPCHECK(hipStreamSynchronize(c->stream));
+        note_live(c, h);
+        c->wf_auto_read = true;
+    }
     c->it_recorded = iters;
+    c->it_per_gen = per_gen;
+    c->tail_recorded = tail ? (int)ngen : 0;
+    c->tail_iter = tail ? qf + 1 : -1;
     c->generations = (int)ngen;
     return MFX_OK;
 }
@@ -935,17 +1002,17 @@ int mfx_accum_reduce(mfx_ctx* c) {
     return MFX_OK;
 }
 
-int mfx_trace_timing(mfx_ctx* c, double out[8]) {
+int mfx_trace_timing(mfx_ctx* c, double out[12]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
     if (c->rep_valid) {  // a call served from held frames: its batch's device time, no stage split
-        for (int k = 0; k < 8; ++k) out[k] = 0.0;
+        for (int k = 0; k < 12; ++k) out[k] = 0.0;
         out[0] = c->rep_ms;
         return MFX_OK;
     }
     double total = 0;
     int rc = mfx_last_trace_ms(c, &total);
     if (rc) return rc;
-    for (int k = 0; k < 8; ++k) out[k] = 0.0;
+    for (int k = 0; k < 12; ++k) out[k] = 0.0;
     out[0] = total;
     if (c->mega_last) {
         out[2] = total;
@@ -955,7 +1022,7 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
         // [2] the closest-hit kernels (k_camera + k_extend), [4] k_shadow (+ memset), summed over
         // iterations; [1] of [2] the k_camera launches (each generation's first iteration when
         // camera rays run as packets), [3] their count; the resolve launches make up the rest of [0]
-        const int per_gen = c->host.max_depth + 1;
+        const int per_gen = std::max(1, c->it_per_gen);
         for (int it = 0; it < c->it_recorded; ++it) {
             const hipEvent_t* ev = c->it_ev.data() + 3 * it;
             float fe = 0.f, fs = 0.f;
@@ -971,6 +1038,23 @@ int mfx_trace_timing(mfx_ctx* c, double out[8]) {
         out[5] = c->it_recorded;
         out[6] = c->it_recorded;
         out[7] = c->generations;
+        // [8] the k_tail launches' time, [9] their count, [10] / [11] their extension / shadow rays
+        for (int g = 0; g < c->tail_recorded; ++g) {
+            float ft = 0.f;
+            HIPCHECK(hipEventElapsedTime(&ft, c->tail_ev[2 * g], c->tail_ev[2 * g + 1]));
+            out[8] += ft;
+        }
+        out[9] = c->tail_recorded;
+        if (c->tail_recorded > 0) {
+            unsigned long long h[WF_NCTR * WF_SHARDS];
+            HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
+            for (int g = 0; g < WF_SHARDS; ++g) {
+                const unsigned long long* x = h + WF_NCTR * g;
+                out[11] += (double)x[3];
+                for (int d = std::max(1, c->tail_iter); d < WF_ITER_CTRS; ++d) out[10] += (double)x[WF_CTR_ITER + d];
+                if (c->host.max_depth >= WF_ITER_CTRS) out[10] += (double)x[1];  // deeper vertices (counter 1)
+            }
+        }
     }
     return MFX_OK;
 }

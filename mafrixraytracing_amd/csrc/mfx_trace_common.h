@@ -290,9 +290,9 @@ __device__ __forceinline__ bool beats(const Best& B, double t, int first, int in
 // Returns whether the leaf's result is a hit, with its t, the hit slot's info and the leaf's
 // `first`. The two tests have no side effects, so the primitives run first and the box (six
 // FP64 divisions) only when the answer still depends on it.
-template <bool SHADOW>
+// shadow: an any-hit query (the first hit below tMax decides the leaf)
 __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV o, DV d, double tMin, double tMax,
-                             double& t_out, int& info_out, int& first_out) {
+                             double& t_out, int& info_out, int& first_out, bool shadow) {
     const MfxLeaf* __restrict__ lf = (const MfxLeaf*)(ref_blob + (size_t)off16 * 16);
     const MfxSlot* __restrict__ sl = (const MfxSlot*)(lf + 1);
     const int count = lf->count, kinds = lf->kinds;
@@ -328,7 +328,7 @@ __device__ bool ref_leaf_hit(const uint8_t* __restrict__ ref_blob, int off16, DV
             best_slot = hs;
         }
         // a hit below tMax has a key below every miss's: the minBy result is a hit
-        if (SHADOW && h && t < tMax) break;
+        if (shadow && h && t < tMax) break;
     }
     if (!best_hit) return false;
     if (!aabb_hit64(lf->lo, lf->hi, o, d, tMin, tMax)) return false;
@@ -487,9 +487,12 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
 // when B improved.
 // base: the slot index the code counts from (an instance's run of world slots; 0 otherwise).
 // UNI: the leaf is wave-uniform (packet traversal): its slots are read through scalar loads.
-template <bool SHADOW, bool STATS, bool UNI = false>
+// RT: the query kind is the per-lane runtime flag shd_rt instead of SHADOW (k_tail's lanes trace
+// closest-hit and shadow queries side by side).
+template <bool SHADOW, bool STATS, bool UNI = false, bool RT = false>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
-                                         Best& B, Stats& st, int base = 0) {
+                                         Best& B, Stats& st, int base = 0, bool shd_rt = false) {
+    const bool shd = RT ? shd_rt : SHADOW;
     const int s0 = base + (code >> 3), n = (code & 7) + 1;
     const MfxSlot* __restrict__ sl = S.slots + s0;
     if (STATS) st.clusters++;
@@ -553,8 +556,8 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         if (t >= tMax) {
             double t2;
             int info2, first2;
-            if (ref_leaf_hit<SHADOW>(S.ref_blob, S.slot_ref[s0 + hs], o, d, tMin, tMax, t2, info2, first2)) {
-                if (SHADOW) return true;
+            if (ref_leaf_hit(S.ref_blob, S.slot_ref[s0 + hs], o, d, tMin, tMax, t2, info2, first2, shd)) {
+                if (shd) return true;
                 if (beats(B, t2, first2, info2)) {
                     B = Best{t2, info2, first2, true};
                     improved = true;
@@ -562,8 +565,8 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
             }
             continue;
         }
-        if (!SHADOW && B.found && t > B.t) continue;  // cannot win: skip the box test
-        if (!SHADOW && !beats(B, t, first, info)) continue;
+        if (!shd && B.found && t > B.t) continue;  // cannot win: skip the box test
+        if (!shd && !beats(B, t, first, info)) continue;
 #if MFX_TRI_BOX_PROOF && MFX_LEAF_PRELOAD
         if (kind != MFX_KIND_SPHERE && tri_box_pass(r.a, r.b, r.c, o, d, tMin, tMax)) {
             // the reference leaf's box test passes (proved; its box is not read)
@@ -579,7 +582,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         } else {
             if (!aabb_hit(sl[hs].lo, sl[hs].hi, o, d, tMin, tMax)) continue;
         }
-        if (SHADOW) return true;
+        if (shd) return true;
         B = Best{t, info, first, true};
         improved = true;
     }
@@ -712,9 +715,11 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
     return node;
 }
 
+// far_rt: the child order as a per-lane runtime flag (k_tail); FAR calls leave it at its default
 template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
+                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0},
+                                         bool far_rt = FAR) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
@@ -748,7 +753,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = n <= f;
-        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
+        d[k] = h ? (far_rt ? -f : n) : __builtin_inff();
         nh += h ? 1 : 0;
     }
     cswap(d[0], c[0], d[1], c[1]);

@@ -190,4 +190,8 @@ def test_bench_two_ranks_rehearsal_under_torchrun(gpu):
     assert r1.returncode == 0, r1.stderr[-3000:]
     one = json.loads(r1.stdout.strip().splitlines()[-1])
     assert line["rays_per_step"] == one["rays_per_step"] > 0
+    # the strong split of the same job in the same run: the config's 2 spp per step over the 2 ranks
+    st = line["strong"]
+    assert st["scaling"] == "strong" and st["global_spp_per_step"] == 2 and st["spp_per_gpu"] == 1
+    assert 0 < st["rays_per_step"] < line["rays_per_step"] and st["value"] > 0
 
