@@ -691,7 +691,6 @@ static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
     P.ox = A.ox; P.oy = A.oy; P.oz = A.oz; P.dx = A.dx; P.dy = A.dy; P.dz = A.dz;
     P.key = A.key; P.rn = A.rn; P.depth = A.depth; P.state = A.state;
     P.fstate = A.state;
-    P.fdepth = A.depth;
     P.qslot = nullptr;
     P.qcount = nullptr;
     P.ncount = nullptr;

@@ -10,7 +10,7 @@
 // in its state, so no ray queue (and no hot queue-tail atomic) exists:
 //   FREE (iteration 1) | NEED_EXT -(k_extend: camera or extension ray, closest hit)-> HIT | MISS
 //   HIT -(k_shadow: shade + shadow ray)-> NEED_EXT, DONE (a lit vertex recorded) or FREE (none)
-//   MISS stays: a finished path (its depth word holds the lit vertices; k_resolve folds it), black
+//   MISS stays: a finished path (its state word holds the lit vertices; k_resolve folds it), black
 //   for a camera ray's MISS | FRESH
 // A path's radiance is not summed forward. Each vertex v records the operands of its BRDF factor
 // c_v = col (the cosine ei and the material) and, when its shadow ray reaches the light, those of
@@ -37,6 +37,8 @@
 #define WF_FRESH 4  // flag on WF_HIT / WF_MISS: the path's camera ray. Its throughput (1), radiance
                     // (0), draw count (2) and depth (max_depth) are implicit: never stored
 #define WF_DONE 8   // finished with a lit vertex: k_resolve folds its vertices and adds them to its pixel
+// A finished path's state word (WF_DONE, or WF_MISS left by k_extend) carries its lit-vertex mask
+// << WF_SHADE_SHIFT, so k_resolve reads no depth word
 #define WF_STATE_MASK 15
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
 // depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
@@ -106,12 +108,12 @@ struct WfParams {
     // Ray queues (MFX_RAY_QUEUE; null: every iteration works on the slot pool in place). From the
     // second iteration on, the arrays above are a queue's: entry i holds a continuing path's ray,
     // key, draw count, depth word and state, and qslot[i] names its slot, which keeps the path's
-    // vertex records (vei, vmat, vls) and its final state and depth word (fstate, fdepth: what
+    // vertex records (vei, vmat, vls) and its final state word (fstate, with the lit mask: what
     // k_resolve reads). k_shadow appends the paths that continue to the next queue (n*), so the
     // sparse later bounces read and write dense memory instead of scattered slots.
     const int32_t* qslot;             // entry -> slot (null: entry = slot, the pool itself)
     const unsigned long long* qcount; // [WF_SHARDS * WF_HS] entries of each shard range of this iteration's queue (null: the pool)
-    int32_t *fstate, *fdepth;         // the slot pool's state / depth words (== state / depth in place)
+    int32_t* fstate;                  // the slot pool's state words (== state in place)
     double *nox, *noy, *noz, *ndx, *ndy, *ndz;  // the next queue (null: continue in place)
     uint64_t* nkey;
     uint32_t* nrn;

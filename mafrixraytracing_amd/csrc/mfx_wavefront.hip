@@ -565,8 +565,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
                 P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
                 P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
-            } else {
-                P.state[s] = WF_MISS | fl;
+            } else {  // a later miss finishes the path: its lit mask goes into the state word
+                P.state[s] = WF_MISS | (fresh || Q ? 0 : ((P.depth[s] >> WF_LIT_SHIFT) & 0xffff) << WF_SHADE_SHIFT) | fl;
             }
             active = false;
         }
@@ -723,14 +723,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const int sv = sj & WF_STATE_MASK;
                     const bool hit = (sv & ~WF_FRESH) == WF_HIT;
                     // a pool slot's miss stays as k_extend wrote it: k_resolve takes MISS as finished
-                    // (its depth word holds the lit vertices) and a camera ray's MISS | FRESH as black
+                    // (its state word holds the lit vertices) and a camera ray's MISS | FRESH as black
                     if (Q && P.qslot && sv == WF_MISS) {  // a queue entry: its slot finishes (no lit vertex: stays unfinished)
                         const int dw = P.depth[j];
-                        if (dw >> WF_LIT_SHIFT) {
-                            const int jr = P.qslot[j];
-                            P.fdepth[jr] = dw;
-                            P.fstate[jr] = WF_DONE;
-                        }
+                        if (dw >> WF_LIT_SHIFT) P.fstate[P.qslot[j]] = WF_DONE | ((dw >> WF_LIT_SHIFT) << WF_SHADE_SHIFT);
                     }
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
@@ -906,14 +902,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 P.ndepth[s] = dwn;
                 P.nstate[s] = need;
             } else if (Q && (P.ncount || P.qslot)) {  // finished; the pool's slot keeps its final words
-                if (mask) {
-                    const int jr = P.qslot ? P.qslot[s] : s;
-                    P.fdepth[jr] = dwn;
-                    P.fstate[jr] = WF_DONE;
-                }
+                if (mask) P.fstate[P.qslot ? P.qslot[s] : s] = WF_DONE | (mask << WF_SHADE_SHIFT);
             } else {
-                if (cont || mask) P.depth[s] = dwn;
-                P.state[s] = cont ? need : (mask ? WF_DONE : WF_FREE);
+                if (cont) P.depth[s] = dwn;
+                P.state[s] = cont ? need : (mask ? WF_DONE | (mask << WF_SHADE_SHIFT) : WF_FREE);
             }
             active = false;
         }
@@ -1056,20 +1048,13 @@ __global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
                 fin = false;
                 count_ext(dw);
             } else {  // finished: k_resolve folds the recorded vertices (none lit: black, nothing to write)
-                if (mask) {
-                    P.fdepth[jr] = dwn;
-                    P.fstate[jr] = WF_DONE;
-                }
+                if (mask) P.fstate[jr] = WF_DONE | (mask << WF_SHADE_SHIFT);
                 active = false;
             }
         }
         // ---- a finished extension ray: a miss ends the path, a hit is shaded ----
         if (fin && !shd && !T.B.found) {
-            if (dw >> WF_LIT_SHIFT) {
-                const int jr = P.qslot[e];
-                P.fdepth[jr] = dw;
-                P.fstate[jr] = WF_DONE;
-            }
+            if (dw >> WF_LIT_SHIFT) P.fstate[P.qslot[e]] = WF_DONE | ((dw >> WF_LIT_SHIFT) << WF_SHADE_SHIFT);
             active = false;
         }
         const bool own = fin && !shd && T.B.found;
@@ -1137,7 +1122,7 @@ __global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
 
 // One path's vertex records as loaded by k_resolve: for the first WF_RES_VERTS vertices up to its
 // deepest lit one, ei and the material; cs and solid for the lit ones. Loaded in one round of
-// independent loads (the state and depth words came in the rounds before), so a path costs three
+// independent loads (the state word came in the round before), so a path costs two
 // dependent memory round trips instead of one per vertex and field.
 struct PathRec {
     int mask;  // lit-vertex mask (0: black path, or not a finished path of this generation)
@@ -1208,8 +1193,9 @@ __device__ __forceinline__ void fold_path(const WfParams& P, int64_t j, const Pa
 // exact), black below the last lit vertex, and l = 0 at an occluded or unlit one. One thread per
 // tile-ordered pixel position q; for a fixed sample, consecutive q are consecutive slots, so the
 // loads are coalesced. No atomics: one thread owns each pixel, generations are stream-ordered.
-// The records of WF_RES_SAMPLES samples are loaded together (state words, then depth words, then
-// vertex records: three rounds of independent loads), then folded and added in sample order.
+// The records of WF_RES_SAMPLES samples are loaded together (state words, which carry a finished
+// path's lit mask, then vertex records: two rounds of independent loads), then folded and added in
+// sample order.
 // Render-ahead (P.planes): each sample's 1-spp image goes to its own plane, 0.0 + its path (what a
 // one-sample call adds to its zeroed accumulator), 0.0 for a black one.
 // ------------------------------------------------------------------------------------------------
@@ -1252,7 +1238,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 #pragma unroll
         for (int u = 0; u < U; ++u)
             mask[u] = ((sw[u] & WF_STATE_MASK) == WF_DONE || (sw[u] & WF_STATE_MASK) == WF_MISS)
-                          ? (P.depth[jv[u]] >> WF_LIT_SHIFT) & 0xffff : 0;
+                          ? ((unsigned)sw[u] >> WF_SHADE_SHIFT) & 0xffff : 0;
         PathRec R[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) load_path(P, jv[u], mask[u], R[u]);
