@@ -195,11 +195,14 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * of K x 28 B per pixel). Every frame's bytes and the film equal the one-sample path's (a sample's
  * image depends only on the seed and its global index); mfx_reset, an spp != 1 call or mfx_sample
  * in between make the held frames recompute from the film as it then is. mfx_stats: the first call
- * served from a batch reports the K samples' rays and device time, the others 0 rays in 0 s. K is
- * cut to what fits in a quarter of the free HBM, or in MFX_RENDER_AHEAD_MAX_BYTES (environment)
- * if smaller (one buffer, no background batch, if two do not fit); when not even two samples fit,
- * the context frees the buffers and renders one sample per call from then on. The accumulator
- * (mfx_accum_read_mean) does not hold the samples of calls served from batches.                */
+ * served from a batch reports the K samples' rays and device time, the others 0 rays in 0 s. The
+ * two buffers take at most MFX_RENDER_AHEAD_MAX_BYTES (environment; default 2 GiB) and a quarter of
+ * the free HBM: K is cut to fit two buffers while at least 8 samples fit in each (1080p: 2 x 16),
+ * else one buffer of as many samples as fit (no background batch); when not even two samples fit,
+ * the context frees the buffers and renders one sample per call from then on. A background batch
+ * is traced once a batch starts being served, so an application that stops early has traced at
+ * most one batch ahead. The accumulator (mfx_accum_read_mean) does not hold the samples of calls
+ * served from batches.                                                                        */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
 /* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */

@@ -1247,11 +1247,15 @@ static int ahead_alloc(mfx_ctx* c) {
     const size_t per_sample = plane + frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
     size_t fr = 0, tot = 0;
     HIPCHECK(hipMemGetInfo(&fr, &tot));
-    size_t budget = fr / 4;  // both buffers within a quarter of the free HBM
+    // Both buffers within MFX_RENDER_AHEAD_MAX_BYTES (default 2 GiB) and a quarter of the free HBM:
+    // a context never takes more than that for render-ahead, whatever K it asked for. K shrinks to
+    // fit two buffers (the background batch) while at least 8 samples fit in each; below that one
+    // buffer of as many samples as fit. At 1080p (58 MB per sample) the default cap gives 2 x 16.
+    size_t budget = std::min<size_t>(fr / 4, (size_t)2 << 30);
     if (const char* e = getenv("MFX_RENDER_AHEAD_MAX_BYTES")) budget = std::min(budget, (size_t)atoll(e));
     int nbuf = 2;
-    int64_t k = c->render_ahead;
-    if ((size_t)k * per_sample + fixed > budget / 2) {
+    int64_t k = std::min<int64_t>(c->render_ahead, budget / 2 > fixed ? (int64_t)((budget / 2 - fixed) / per_sample) : 0);
+    if (k < std::min(8, c->render_ahead)) {
         nbuf = 1;  // no background batch: one buffer of as many samples as fit
         k = budget > fixed ? (int64_t)((budget - fixed) / per_sample) : 0;
         k = std::min<int64_t>(k, c->render_ahead);

@@ -841,7 +841,11 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 vflag = pd.flag[e];
                 scs = pd.v[4 * 64 + e]; ssolid = pd.v[5 * 64 + e];
                 // origin = the hit point k_extend stored (a cache hit: the shading just read it), or
-                // its copy in the next queue
+                // its copy in the next queue. That copy (nox..noz, and nslot below) was stored in this
+                // kernel by the lane that shaded the hit, which may be another lane of this wave: the
+                // read is ordered after that store by the wave_lds_sync() calls that end the shading
+                // batch (release / acquire fences at wavefront scope cover global memory as well as
+                // LDS), and one wave's vector memory operations reach its L1 in order.
                 const bool nq = Q && (vflag & 1) && P.ncount;
                 const double* hx = nq ? P.nox : P.ox;
                 const double* hy = nq ? P.noy : P.oy;
