@@ -459,6 +459,14 @@ def main():
                 del os.environ["MFX_CAMERA_PACKETS"]
             else:
                 os.environ["MFX_CAMERA_PACKETS"] = old
+            # the camera-ray packets' own fetches (k_camera's bytes: each node and slot once per wave)
+            pk = None
+            if not args.megakernel and stage_ms["camera_launches"] > 0:
+                with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS | mode) as sc:
+                    sc.trace_accumulate(1, 10 ** 6)
+                    sp = sc.ray_counts()
+                if sp[10] > 0:
+                    pk = {"node_fetches_per_ray": sp[10] / sp[0], "slot_fetches_per_ray": sp[11] / sp[0]}
             rc, rs = s[0] + s[1], s[2]
             # closest-hit traversal counters in s[4..6], shadow in s[7..9]
             stats = {"closest": {"node_visits_per_ray": s[4] / rc, "cluster_visits_per_ray": s[5] / rc,
@@ -469,6 +477,8 @@ def main():
                              "cluster_visits_per_ray": (s[5] + s[8]) / (rc + rs),
                              "prim_tests_per_ray": (s[6] + s[9]) / (rc + rs)},
                      "rays_per_path": (rc + rs) / s[0]}
+            if pk:
+                stats["camera_packets"] = pk
 
         def bytes_per_ray(c):
             # SURVEY.md §8d / DESIGN.md §7: 32 B per BVH2 node visit (internal or leaf), 36 B per
@@ -535,6 +545,25 @@ def main():
                         "peak_case": tdroof["peak"]["case"],
                         "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
 
+            def smem_roofline(kname, kms, launches):
+                """k_camera's roof: scalar-memory instructions (SQ_INSTS_SMEM, the PMC pass of
+                scripts/pmc_td_roof.sh) per launch over this run's HIP-event launch time, against
+                scripts/ubench/sload's peak rate at the clock the pass ran at."""
+                if not tdroof or "smem_peak" not in tdroof:
+                    return None
+                ks = [kv for kk, kv in tdroof["kernels"].items() if kk.split("<")[0] == kname and "smem_per_launch" in kv]
+                if not ks:
+                    return None
+                kv = ks[0]
+                mhz = kv["smem_gpu_clocks_per_launch"] / kv["smem_ms_per_launch"] / 1e3
+                ach = kv["smem_per_launch"] / (kms / launches / 1e3) / 1e9
+                peak = tdroof["smem_peak"]["smem_per_clock"] * mhz * 1e6 / 1e9
+                return {"bound": "smem", "achieved": round(ach, 3), "peak": round(peak, 3),
+                        "unit": "G scalar-load instructions/s", "frac": round(ach / peak, 4),
+                        "frac_pmc_pass": round(kv["smem_frac_of_peak"], 4),
+                        "smem_per_launch": kv["smem_per_launch"], "peak_case": tdroof["smem_peak"]["case"],
+                        "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
+
             def kernel_roofline(kname, kms, krays, launches, bray, bytes_total=None):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
                 if bytes_total is not None:  # a kernel tracing both kinds of ray (k_tail)
@@ -550,6 +579,9 @@ def main():
                         traffic = sum(kv.get("hbm_bytes_per_launch", 0.0) * kv.get("launches_profiled", 1) for kv in ks) / nl
                 return {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                         "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                        "traffic_note": "PMC HBM bytes per launch, an upper bound: FETCH_SIZE x2 (the gfx950 "
+                                        "correction measured for wide streaming reads) is applied to these gathers "
+                                        "too, and MALL hits count as fabric traffic" if traffic else None,
                         "td": td_roofline(kname, kms, launches),
                         "kernel": kname, "launches_per_step": launches,
                         "avg_launch_ms": round(kms / launches, 4),
@@ -576,10 +608,18 @@ def main():
                 bs = fixture["shadow"]["B_ray"] if fixture else bytes_per_ray(stats["shadow"])
                 ks = []
                 if cl > 0:
-                    kc = kernel_roofline("k_camera<false>", stage_ms["camera_ms"], primary_rays / nt, cl, bc)
-                    kc["note"] = ("speed index, not a bandwidth fraction: the bytes model prices each camera ray's "
-                                  "own BVH2 walk, while a packet fetches each node and slot once for its 64 rays "
-                                  "(scalar loads), so the index can exceed 1; the TD object is the measured roof")
+                    # k_camera's bytes are its packets' own fetches: per camera ray its
+                    # share of the wave-uniform 128-B node steps and 80-B slot prefixes (scalar loads,
+                    # once per wave), plus its state word read and hit point + state word written (32 B)
+                    pkc = stats.get("camera_packets")
+                    b_cam = (128.0 * pkc["node_fetches_per_ray"] + 80.0 * pkc["slot_fetches_per_ray"] + 32.0) if pkc else bc
+                    kc = kernel_roofline("k_camera<false>", stage_ms["camera_ms"], primary_rays / nt, cl, b_cam)
+                    kc["bytes_per_ray_source"] = ("packet fetch counters (mfx_ray_counts out[10], out[11], "
+                                                  "MFX_F_COUNT_STATS pass)" if pkc else kc["bytes_per_ray_source"])
+                    kc["td"] = None  # its nodes and slots do not pass the TD: the scalar-load roof is kc["smem"]
+                    kc["smem"] = smem_roofline("k_camera", stage_ms["camera_ms"], cl)
+                    kc["note"] = ("HBM index priced at the bytes the packets fetch (each node and slot once per wave, "
+                                  "through the scalar cache); its binding roof is the scalar-load rate (smem)")
                     ks.append((stage_ms["camera_ms"], kc))
                 t_ext, t_shd = stage_ms["tail_ext_rays"], stage_ms["tail_shadow_rays"]  # k_tail's, per step
                 ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt - t_ext

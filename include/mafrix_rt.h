@@ -261,7 +261,9 @@ int mfx_trace_timing(mfx_ctx* ctx, double out[12]);
  * out[0] = primary, out[1] = extension (closest-hit queries actually traced, excluding the
  * reference's discarded depth -1 query), out[2] = shadow, out[3] = paths; with
  * MFX_F_COUNT_STATS: out[4..6] = internal-node visits, cluster (reference leaf) visits and
- * primitive tests of the closest-hit queries, out[7..9] the same for the shadow queries.     */
+ * primitive tests of the closest-hit queries, out[7..9] the same for the shadow queries, and
+ * out[10] / out[11] = the camera-ray packets' own fetches (k_camera: wave-uniform 128-B node
+ * steps and leaf slots, once per wave; the per-ray visits of packet lanes are in out[4..6]).    */
 int mfx_ray_counts(mfx_ctx* ctx, double out[16]);
 
 /* SURVEY.md §8(b)'s stats call, for the Mrays/s metric (§8(d)): rays = primary + extension +

@@ -152,6 +152,7 @@ struct mfx_ctx {
     // runs them to their ends instead of the remaining bounce-synchronous iterations
     bool wf_tail = true;
     int wf_tail_grid = 0;
+    int wf_tail_waves = 4;                  // k_tail's register budget: 3 or 4 waves per SIMD
     int32_t wf_tchunk = 256;                // queue entries per k_tail chunk fetch (MFX_TCHUNK)
     std::vector<hipEvent_t> tail_ev;        // per generation: k_tail start, end
     int tail_recorded = 0;                  // k_tail launches of the last trace with events
@@ -167,6 +168,7 @@ struct mfx_ctx {
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
     int wf_ntop_ext = 0, wf_ntop_shd = 0;  // top BVH nodes each trace kernel copies into LDS
+    int wf_nslot_ext = 0, wf_nslot_shd = 0;  // and slots (a small scene's whole slot array, or none)
     int wf_shadow_waves = 4;               // k_shadow's register budget: 3 or 4 waves per SIMD
     int32_t* d_spill = nullptr;      // deep traversal-stack entries
     double* d_vscratch = nullptr;    // megakernel: per-lane vertex records [max_depth + 1][6][grid * 256]
@@ -397,6 +399,16 @@ static int ctx_setup(mfx_ctx* c) {
                 else hi = mid - 1;
             }
             (shd ? c->wf_ntop_shd : c->wf_ntop_ext) = lo;
+            // A small scene's whole slot array (80-B test prefixes) in LDS too, when it fits beside the
+            // top nodes without costing a resident block: every leaf test then reads LDS (C3: 26 slots)
+            int ns = (int)c->host.slots.size();
+            if (ns > WF_SLOT_LDS_MAX || (getenv("MFX_SLOT_LDS") && atoi(getenv("MFX_SLOT_LDS")) == 0)) ns = 0;
+            if (ns > 0) {
+                int b = 0;
+                CK(mfx_wf_kernel_occupancy(shd, nlds, nlds < c->stack_size, lo, ninst, &b, ns));
+                if (b < want) ns = 0;
+            }
+            (shd ? c->wf_nslot_shd : c->wf_nslot_ext) = ns;
         }
         // k_shadow with at most 3 resident blocks per CU (its LDS) runs the instance compiled for 3
         // waves per SIMD: more registers, no spills (C2 / C5 +2 %); with 4 it keeps the 4-wave one
@@ -406,9 +418,9 @@ static int ctx_setup(mfx_ctx* c) {
         if (c->diag_iter)
             fprintf(stderr,
                     "wavefront: stack %d/%d (extend) %d/%d (shadow) in LDS, blocks/CU extend %d shadow %d (%d-wave "
-                    "build), top nodes in LDS %d / %d\n",
+                    "build), top nodes in LDS %d / %d, slots in LDS %d / %d\n",
                     c->wf_stack_lds_ext, c->stack_size, c->wf_stack_lds_shd, c->stack_size, ebpc, sbpc,
-                    c->wf_shadow_waves, c->wf_ntop_ext, c->wf_ntop_shd);
+                    c->wf_shadow_waves, c->wf_ntop_ext, c->wf_ntop_shd, c->wf_nslot_ext, c->wf_nslot_shd);
     }
     if (const char* b = getenv("MFX_BLOCKS_PER_CU")) {  // tuning knob: resident blocks per CU (<= occupancy)
         ebpc = std::min(ebpc, std::max(1, atoi(b)));
@@ -426,9 +438,11 @@ static int ctx_setup(mfx_ctx* c) {
     }
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
     {  // k_tail: the LDS of k_shadow's stack share and top nodes minus its lists, the register budget of its build
+        c->wf_tail_waves = c->wf_shadow_waves;
+        if (const char* e = getenv("MFX_TAIL_WAVES")) c->wf_tail_waves = atoi(e) == 3 ? 3 : 4;
         int tb = 0;
         CK(mfx_tail_occupancy(c->wf_stack_lds_shd, c->wf_stack_lds_shd < c->stack_size, c->wf_ntop_shd, ninst,
-                              c->wf_shadow_waves, &tb));
+                              c->wf_tail_waves, &tb, c->wf_nslot_shd));
         c->wf_tail_grid = prop.multiProcessorCount * std::max(1, std::min(tb, 8));
     }
     {  // deep traversal-stack entries of every lane of the larger grid
@@ -763,6 +777,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.stack_lds_shd = c->wf_stack_lds_shd;
     P.ntop_ext = c->wf_ntop_ext;
     P.ntop_shd = c->wf_ntop_shd;
+    P.nslot_ext = c->wf_nslot_ext;
+    P.nslot_shd = c->wf_nslot_shd;
     P.shadow_waves = c->wf_shadow_waves;
     P.ninst_lds = std::min<int>((int)c->host.inst.size(), WF_INST_LDS);
     P.spill = c->d_spill;
@@ -846,7 +862,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             P.chunk = c->wf_chunk_env ? chunk0 : c->wf_tchunk;
             hipEvent_t* ev = own_events ? c->tail_ev.data() + 2 * g : nullptr;
             if (ev) HIPCHECK(hipEventRecord(ev[0], c->stream));
+            P.shadow_waves = c->wf_tail_waves;  // (k_tail's own build)
             HIPCHECK(mfx_wf_tail(P, c->wf_tail_grid, stats, c->stream));
+            P.shadow_waves = c->wf_shadow_waves;
             if (ev) HIPCHECK(hipEventRecord(ev[1], c->stream));
             if (ev && c->diag_iter) {
                 float ft = 0.f;

@@ -236,6 +236,10 @@ struct SceneView {
     const MfxInstance* __restrict__ inst;  // two-level scenes: the instances (else null)
     const MfxInstance* inst_lds;           // LDS copy of instances [0, ninst_lds) (wavefront kernels)
     int ninst_lds;
+    // LDS copy of every slot's 80-B test prefix (a small scene's whole slot array, five 16-B columns
+    // per slot; wavefront kernels), or none: nslot_lds is the slot count or 0
+    const int4* slots_lds;
+    int nslot_lds;
 };
 
 // An instance's record: from the kernel's LDS copy when it holds it, else from global memory
@@ -399,6 +403,24 @@ __device__ __forceinline__ void load_box_u(const MfxSlot* __restrict__ p, double
     hi[0] = i2d(r6.z, r6.w); hi[1] = i2d(r7.x, r7.y); hi[2] = i2d(r7.z, r7.w);
 }
 
+// The same prefix from the kernel's LDS copy of the slots (SceneView::slots_lds)
+__device__ __forceinline__ SlotR load_slot_lds(const int4* t, int slot) {
+    const int4* q = t + 5 * slot;
+    const int4 r0 = q[0], r1 = q[1], r2 = q[2], r3 = q[3], r4 = q[4];
+    SlotR s;
+    s.a = dv(i2d(r0.x, r0.y), i2d(r0.z, r0.w), i2d(r1.x, r1.y));
+    s.b = dv(i2d(r1.z, r1.w), i2d(r2.x, r2.y), i2d(r2.z, r2.w));
+    s.c = dv(i2d(r3.x, r3.y), i2d(r3.z, r3.w), i2d(r4.x, r4.y));
+    s.first = r4.z;
+    s.info = r4.w;
+    return s;
+}
+// block-wide copy of n slots' test prefixes into LDS at kernel start (ends with a barrier)
+__device__ __forceinline__ void load_slots_lds(int4* lds, const MfxSlot* __restrict__ g, int n) {
+    for (int i = threadIdx.x; i < 5 * n; i += blockDim.x) lds[i] = ((const int4*)(g + i / 5))[i % 5];
+    __syncthreads();
+}
+
 // Triangle.PreCalcu + Hit — Trangle.fs:120-155 (tMax deliberately not checked, :148)
 __device__ __forceinline__ bool tri_hit64(const SlotR& s, DV o, DV d, double tMin, double& t) {
     DV s1 = vcross(d, s.c);
@@ -498,9 +520,10 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     if (STATS) st.clusters++;
     bool improved = false;
     constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
+    const bool in_lds = !UNI && S.nslot_lds > 0;  // the LDS copy holds every slot (wave-uniform)
     for (int k = 0; k < n; ++k) {
 #if MFX_LEAF_PRELOAD
-        SlotR r = UNI ? load_slot_u(sl + k) : load_slot(sl + k);
+        SlotR r = UNI ? load_slot_u(sl + k) : (in_lds ? load_slot_lds(S.slots_lds, s0 + k) : load_slot(sl + k));
         // the reference leaf's box (bytes 80..127; both slots of a rect carry the same one)
         double2 bx0 = make_double2(0, 0), bx1 = bx0, bx2 = bx0;
         if (PRE == 2) {
@@ -523,7 +546,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
                 ++k;  // Rect.Hit: trig1, else trig2 (Rect.fs:26-31); the second slot follows
                 if (!hit) {
                     hs = k;
-                    r = UNI ? load_slot_u(sl + k) : load_slot(sl + k);
+                    r = UNI ? load_slot_u(sl + k) : (in_lds ? load_slot_lds(S.slots_lds, s0 + k) : load_slot(sl + k));
                     hit = tri_hit64(r, o, d, tMin, t);
                     info = r.info;
                     first = r.first;
@@ -860,9 +883,12 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
 }
 
 // Closest hits of the wave's active lanes (act) by packet traversal; B per lane as traverse() gives.
+// STATS: besides the per-lane visits (st), the wave's own fetches: wave-uniform node steps (one
+// 128-B node each) and leaf slots (an 80-B test prefix each), counted on every lane alike.
 template <bool STATS>
 __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
-                                               int* stk, uint64_t* stm, Stats& st) {
+                                               int* stk, uint64_t* stm, Stats& st, uint32_t& pk_nodes,
+                                               uint32_t& pk_slots) {
     B = Best{tMax, -1, -1, false};
     const RayF rf = make_rayf(o, d);
     float tlim = f_tlim(tMax);
@@ -872,9 +898,11 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
     while (true) {
         while (node >= 0) {
             if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
+            if (STATS) pk_nodes++;
             node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep);
         }
         if (node == MFX_TRAV_EXIT) return;
+        if (STATS) pk_slots += (~node & 7) + 1;
         if ((mask >> __lane_id()) & 1) {  // the lanes whose ray hits the leaf's box
             leaf_hit<false, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st);
             tlim = f_tlim(B.t);

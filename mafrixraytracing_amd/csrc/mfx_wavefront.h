@@ -137,6 +137,7 @@ struct WfParams {
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q
     int32_t ntop_ext, ntop_shd;           // top BVH nodes each trace kernel keeps in LDS (<= nodes)
+    int32_t nslot_ext, nslot_shd;         // slots each trace kernel keeps in LDS (all of a small scene's, or 0)
     int32_t shadow_waves;                 // k_shadow instance: 3 or 4 waves per SIMD (register budget)
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
     int32_t cam_grid;                     // > 0: a generation's camera rays run k_camera (packets) on this grid
@@ -160,14 +161,20 @@ struct WfParams {
 #ifndef WF_INST_LDS
 #define WF_INST_LDS 64  // instance records (48 B) a trace kernel keeps in LDS, at most; more stay in global memory
 #endif
+#ifndef WF_SLOT_LDS_MAX
+#define WF_SLOT_LDS_MAX 256  // slots a trace kernel may keep in LDS (80 B each; the whole array or none)
+#endif
 #ifndef WF_NTOP_MAX
 #define WF_NTOP_MAX MFX_TOP_NODES  // top BVH nodes a trace kernel may keep in LDS (mfx_scene.cpp numbers them first)
 #endif
 // resident blocks per CU of k_extend / k_shadow with `stack_lds` stack entries per lane (spill: the
 // SpillStack instance), ntop top BVH nodes and min(ninst, WF_INST_LDS) instance records in LDS
-hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu);
-// resident blocks per CU of k_tail (the same stack share and top nodes as k_shadow, its wave build)
-hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu);
+// (and nslot slots' test prefixes)
+hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu,
+                                   int nslot = 0);
+// resident blocks per CU of k_tail (the same stack share, top nodes and slots as k_shadow, its wave build)
+hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu,
+                              int nslot = 0);
 // resident blocks per CU of k_camera (camera-ray packets)
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu);
 // a ray queue's arrays (MFX_RAY_QUEUE): entries in the pool's shard ranges, counts per shard

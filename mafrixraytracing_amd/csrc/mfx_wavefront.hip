@@ -460,14 +460,16 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
-    int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
+    int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
+    if (P.nslot_ext) load_slots_lds(slot_lds, P.slots, P.nslot_ext);
+    int* lds = (int*)(slot_lds + 5 * P.nslot_ext);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
     int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_ext};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -621,6 +623,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
+    uint32_t pk_nodes = 0, pk_slots = 0;  // STATS: the wave's own node and slot fetches (every lane counts them)
     while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr)) {
         const int j = sc.win_next + lane;
         const int sj = sc.word();
@@ -645,7 +648,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
             c_primary++;
         }
         Best B;
-        packet_closest<STATS>(S, act, o, d, 99999999., B, stk, stm, st);  // Integrators.fs:108
+        packet_closest<STATS>(S, act, o, d, 99999999., B, stk, stm, st, pk_nodes, pk_slots);  // Integrators.fs:108
         if (act) {
             if (B.found) {
                 const DV hp = vadd(o, vmul(d, B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
@@ -662,6 +665,9 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
         block_add<4>(cnt + 4, st.nodes, red);
         block_add<4>(cnt + 5, st.clusters, red);
         block_add<4>(cnt + 6, st.prims, red);
+        // packet fetches, once per wave (lane 0's count): mfx_ray_counts out[10], out[11]
+        block_add<4>(cnt + 10, lane == 0 ? pk_nodes : 0u, red);
+        block_add<4>(cnt + 11, lane == 0 ? pk_slots : 0u, red);
     }
 }
 
@@ -676,7 +682,9 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
-    int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
+    int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
+    if (P.nslot_shd) load_slots_lds(slot_lds, P.slots, P.nslot_shd);
+    int* lds = (int*)(slot_lds + 5 * P.nslot_shd);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -684,7 +692,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_shd};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -960,7 +968,9 @@ __global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
-    int* lds = (int*)(inst_lds + (INST ? P.ninst_lds : 0));
+    int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
+    if (P.nslot_shd) load_slots_lds(slot_lds, P.slots, P.nslot_shd);
+    int* lds = (int*)(slot_lds + 5 * P.nslot_shd);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -971,7 +981,7 @@ __global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
     uint32_t* vctr = red + 16;  // [WF_ITER_CTRS] the block's extension rays by vertex index ([0]: deeper)
     if (threadIdx.x < WF_ITER_CTRS) vctr[threadIdx.x] = 0;
     __syncthreads();
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_shd};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -1272,9 +1282,10 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 // ------------------------------------------------------------------------------------------------
 // launchers
 // ------------------------------------------------------------------------------------------------
-// top nodes, stacks, pending-ray lists, block reduction scratch (64 B) and, for k_shadow, the shade lists
-static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst) {
-    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) +
+// top nodes, instances, slots, stacks, pending-ray lists, block reduction scratch (64 B) and, for
+// k_shadow, the shade lists
+static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst, int nslot = 0) {
+    const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
                           (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
@@ -1289,9 +1300,10 @@ static int wf_lds_blocks(size_t bytes) {
     return (int)(per_cu / ((bytes + g - 1) / g * g));
 }
 
-hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu) {
+hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu,
+                                   int nslot) {
     const bool inst = ninst > 0;
-    const size_t lds = wf_lds_bytes(stack_lds, shadow, ntop, std::min(ninst, WF_INST_LDS));
+    const size_t lds = wf_lds_bytes(stack_lds, shadow, ntop, std::min(ninst, WF_INST_LDS), nslot);
     const void* k;
     if (shadow)
         k = inst ? (spill ? (const void*)k_shadow<false, true, 4, true, false> : (const void*)k_shadow<false, false, 4, true, false>)
@@ -1365,8 +1377,8 @@ static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev) {
     const int ni = P.inst ? P.ninst_lds : 0;
-    const size_t lds_e = wf_lds_bytes(P.stack_lds_ext, false, P.ntop_ext, ni);
-    const size_t lds_s = wf_lds_bytes(P.stack_lds_shd, true, P.ntop_shd, ni);
+    const size_t lds_e = wf_lds_bytes(P.stack_lds_ext, false, P.ntop_ext, ni, P.nslot_ext);
+    const size_t lds_s = wf_lds_bytes(P.stack_lds_shd, true, P.ntop_shd, ni, P.nslot_shd);
     // the chunk heads and, beside them (WF_CTL_Q0 / WF_CTL_Q1), the next queue's shard counts
     unsigned long long* z = P.ctl;
     size_t nz = WF_NCTL;
@@ -1382,8 +1394,9 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     return hipGetLastError();
 }
 
-static size_t tail_lds_bytes(int stack_size, int ntop, int ninst) {
-    return (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)4 * stack_size * 64 * sizeof(int) +
+static size_t tail_lds_bytes(int stack_size, int ntop, int ninst, int nslot) {
+    return (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
+           (size_t)4 * stack_size * 64 * sizeof(int) +
            (size_t)4 * (WF_TAIL_PEND + 64) * sizeof(int) + 64 + 4 * WF_ITER_CTRS;
 }
 
@@ -1393,9 +1406,9 @@ static void launch_tail(const WfParams& P, int grid, bool stats, hipStream_t st,
     else hipLaunchKernelGGL((k_tail<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
 }
 
-hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu) {
+hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu, int nslot) {
     const bool inst = ninst > 0;
-    const size_t lds = tail_lds_bytes(stack_lds, ntop, std::min(ninst, WF_INST_LDS));
+    const size_t lds = tail_lds_bytes(stack_lds, ntop, std::min(ninst, WF_INST_LDS), nslot);
     const void* k;
     if (waves == 3)
         k = inst ? (spill ? (const void*)k_tail<false, true, 3, true> : (const void*)k_tail<false, false, 3, true>)
@@ -1410,7 +1423,7 @@ hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, in
 
 hipError_t mfx_wf_tail(const WfParams& P, int grid, bool stats, hipStream_t st) {
     const int ni = P.inst ? P.ninst_lds : 0;
-    const size_t lds = tail_lds_bytes(P.stack_lds_shd, P.ntop_shd, ni);
+    const size_t lds = tail_lds_bytes(P.stack_lds_shd, P.ntop_shd, ni, P.nslot_shd);
     hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
     const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;

@@ -44,7 +44,7 @@ for step in "$@"; do
     prof)
       bash scripts/profile_traffic.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/prof_$a1.log 2>&1 ;;
     td)
-      make -s -C scripts/ubench td_gather > /dev/null 2>&1 || true
+      make -s -C scripts/ubench td_gather sload > /dev/null 2>&1 || true
       bash scripts/pmc_td_roof.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/td_$a1.log 2>&1 ;;
     pmc)
       bash scripts/pmc_td.sh ${TAG}_$(echo $a1 | tr A-Z a-z) --config $a1 > $O/pmc_$a1.log 2>&1 ;;

@@ -37,9 +37,11 @@ def child(scene, spps):
             c = ctx.ray_counts()
             out[spp] = {"frame_ms": min(ms[1:]), "rays": c[0] + c[1] + c[2]}
     os.environ["MFX_DIAG_ITER"] = "1"
-    r, w = os.pipe()
+    import tempfile
+    tf = tempfile.TemporaryFile()
     saved = os.dup(2)
-    os.dup2(w, 2)
+    sys.stderr.flush()
+    os.dup2(tf.fileno(), 2)
     with NativeContext(a, seed=DEFAULT_SEED) as ctx:
         for spp in spps:
             for k in range(2):
@@ -48,9 +50,10 @@ def child(scene, spps):
                 ctx.accum_clear()
                 ctx.trace_accumulate(spp, k * spp)
                 ctx.sync()
+    sys.stderr.flush()
     os.dup2(saved, 2)
-    os.close(w)
-    text = os.read(r, 1 << 24).decode()
+    tf.seek(0)
+    text = tf.read().decode()
     cur = None
     for line in text.splitlines():
         m = re.match(r"@@ spp (\d+) rep (\d+)", line)
@@ -87,8 +90,8 @@ def main():
         p = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", scene, spps], env=env,
                            capture_output=True, text=True, timeout=600)
         if p.returncode:
-            print(p.stderr[-3000:])
-            raise SystemExit(f"variant {name} failed")
+            print(p.stdout[-2000:], p.stderr[-3000:])
+            raise SystemExit(f"variant {name} failed: exit status {p.returncode}")
         d = {int(k): x for k, x in json.loads(p.stdout.strip().splitlines()[-1]).items()}
         xs = sorted(d)
         print(f"=== {name} ({envs or 'defaults'})")

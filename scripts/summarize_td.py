@@ -81,6 +81,32 @@ def main():
             "frac_of_peak": v["TCP_TOTAL_CACHE_ACCESSES_sum"] / cyc / peak_lpc,
             "td_busy_frac": v["TD_TD_BUSY_sum"] / (cyc * N_TD),
         }
+    # the scalar-memory pass (k_camera's roof): SQ_INSTS_SMEM per GPU clock against scripts/ubench/sload's
+    # peak case (wave-uniform 128-B nodes from a 256 KB table, two 64-B loads each, 4 waves per SIMD)
+    sub = per_dispatch(os.path.join(out, "ubench_smem"))
+    sp = [v for (i, k), v in sub.items() if "sgather" in k and v.get("GRBM_GUI_ACTIVE", 0) > 0]
+    if sp:
+        for v in sp:
+            v["cyc"] = v["GRBM_GUI_ACTIVE"] / N_XCD
+        pv = max(sp, key=lambda v: v["SQ_INSTS_SMEM"] / v["cyc"])
+        speak = pv["SQ_INSTS_SMEM"] / pv["cyc"]
+        res["smem_peak"] = {"case": "scripts/ubench/sload peak: wave-uniform 128-B nodes (two s_load_dwordx16) at "
+                                    "hashed indices of a 256 KB table, 4 independent per round, 16 waves per CU",
+                            "smem_per_clock": speak, "clock_mhz": pv["cyc"] / pv["ns"] * 1e3}
+        sk = collections.defaultdict(lambda: collections.defaultdict(float))
+        for (i, k), v in per_dispatch(os.path.join(out, "bench_smem")).items():
+            name = k.replace("void ", "")
+            if name in res["kernels"]:
+                for c, x in v.items():
+                    sk[name][c] += x
+                sk[name]["launches"] += 1
+        for name, v in sk.items():
+            cyc = v["GRBM_GUI_ACTIVE"] / N_XCD
+            res["kernels"][name].update({"smem_per_launch": v["SQ_INSTS_SMEM"] / v["launches"],
+                                         "smem_per_clock": v["SQ_INSTS_SMEM"] / cyc,
+                                         "smem_frac_of_peak": v["SQ_INSTS_SMEM"] / cyc / speak,
+                                         "smem_gpu_clocks_per_launch": cyc / v["launches"],
+                                         "smem_ms_per_launch": v["ns"] / v["launches"] / 1e6})
     dst = os.path.join(ROOT, "profiles", f"td_{scene}.json")
     with open(os.path.join(out, "td.json"), "w") as f:
         json.dump(res, f, indent=1)

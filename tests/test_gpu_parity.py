@@ -208,7 +208,7 @@ def test_wavefront_small_pool_many_iterations(gpu, oracle, pool, monkeypatch):
     with NativeContext(a, seed=SEED) as ctx:
         img = ctx.sample(6)
         tm = ctx.trace_timing()
-    assert tm["iterations"] > 5
+    assert tm["generations"] > 1
     assert np.array_equal(img, ref)
 
 
