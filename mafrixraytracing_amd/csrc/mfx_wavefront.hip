@@ -226,6 +226,9 @@ __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, cons
                                                             shd && MFX_SHADOW_ORDER == 1);
 }
 
+#ifndef MFX_INLOOP_REFILL
+#define MFX_INLOOP_REFILL 0  // experiment (A/B variant): k_extend refills lanes whose walk ended inside the node loop
+#endif
 #ifndef MFX_NODE_LANES_MIN_TAIL
 #define MFX_NODE_LANES_MIN_TAIL 14  // k_tail's node-loop exit (its lanes mix closest-hit and shadow rays)
 #endif
@@ -485,6 +488,49 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     constexpr bool DG = MFX_DIAG_STAMPS == 1;
     DiagAcc dg{};
     if (DG) dg.last = stamp();
+    // the lane takes listed entry e: its camera ray (FREE slot) or the slot's extension ray
+    auto start_ray = [&](int e) {
+        s = e & 0x7fffffff;
+        fresh = e < 0;
+        DV o, d;
+        if (fresh) {
+            // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
+            int x, y;
+            int64_t smp;
+            path_pixel(P, P.path_base + s, x, y, smp);
+            const int64_t pixel = (int64_t)x * P.height + y;  // Color[w,h] x-major
+            const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
+            const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
+            uint32_t rn = 0;
+            const double u = ((double)x + rng_next(key, rn)) / (double)P.width;
+            const double v = ((double)y + rng_next(key, rn)) / (double)P.height;
+            const MfxCamera& CAM = P.cam;
+            const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
+            o = ld3(CAM.position);
+            d = vnormalize(vsub(target, o));
+            // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH); the
+            // key is derived again by k_shadow (stored only for a path that continues)
+            c_primary++;
+        } else {
+            o = dv(P.ox[s], P.oy[s], P.oz[s]);
+            d = dv(P.dx[s], P.dy[s], P.dz[s]);
+            c_ext++;
+        }
+        trav_begin(T, S, o, d, 99999999.);  // Integrators.fs:108
+        active = true;
+    };
+    // the lane's ray is finished: its closest hit (hit point, shade index) or its miss
+    auto finish_ray = [&]() {
+        const int fl = fresh ? WF_FRESH : 0;
+        if (T.B.found) {
+            const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
+            P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
+            P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
+        } else {  // a later miss finishes the path: its lit mask goes into the state word
+            P.state[s] = WF_MISS | (fresh || Q ? 0 : ((P.depth[s] >> WF_LIT_SHIFT) & 0xffff) << WF_SHADE_SHIFT) | fl;
+        }
+        active = false;
+    };
 
     while (true) {
         // ---- dynamic fetch: idle lanes take pending rays by rank ----
@@ -520,36 +566,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             const int avail = pend_hi - pend_lo;
             const int rank = __popcll(m & lanes_below());
             if (idle && rank < avail) {
-                const int e = pend[pend_lo + rank];
-                s = e & 0x7fffffff;
-                fresh = e < 0;
-                DV o, d;
-                if (fresh) {
-                    // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
-                    int x, y;
-                    int64_t smp;
-                    path_pixel(P, P.path_base + s, x, y, smp);
-                    const int64_t pixel = (int64_t)x * P.height + y;  // Color[w,h] x-major
-                    const int64_t gsample = P.sample_base + P.part_index + smp * P.part_count;
-                    const uint64_t key = path_key(P.seed, (uint64_t)pixel, (uint64_t)gsample);
-                    uint32_t rn = 0;
-                    const double u = ((double)x + rng_next(key, rn)) / (double)P.width;
-                    const double v = ((double)y + rng_next(key, rn)) / (double)P.height;
-                    const MfxCamera& CAM = P.cam;
-                    const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
-                    o = ld3(CAM.position);
-                    d = vnormalize(vsub(target, o));
-                    // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH); the
-                    // key is derived again by k_shadow (stored only for a path that continues)
-                    c_primary++;
-                } else {
-                    o = dv(P.ox[s], P.oy[s], P.oz[s]);
-                    d = dv(P.dx[s], P.dy[s], P.dz[s]);
-                    c_ext++;
-                }
-                trav_begin(T, S, o, d, 99999999.);  // Integrators.fs:108
+                start_ray(pend[pend_lo + rank]);
                 idle = false;
-                active = true;
             }
             const int pm = __popcll(m);
             pend_lo += pm < avail ? pm : avail;
@@ -559,19 +577,55 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
-        if (active) fin = trav_step<false, STATS, INST>(T, S, stack, tn, st, dg, DG);
-        DIAG_MARK(dg, leaf, DG);
-        if (fin) {
-            const int fl = fresh ? WF_FRESH : 0;
-            if (T.B.found) {
-                const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
-                P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
-                P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
-            } else {  // a later miss finishes the path: its lit mask goes into the state word
-                P.state[s] = WF_MISS | (fresh || Q ? 0 : ((P.depth[s] >> WF_LIT_SHIFT) & 0xffff) << WF_SHADE_SHIFT) | fl;
+#if MFX_INLOOP_REFILL
+        // Experiment: a lane whose walk ends inside the node loop (stack empty, no child hit) writes
+        // its result and takes the next listed ray there, instead of idling until the loop exits
+        if (active) {
+            RayF rf{};
+            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
+            rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
+            float tlim = f_tlim(T.B.t);
+            while (true) {
+                if (active && T.node >= 0) {
+                    if (STATS) st.nodes++;
+                    T.node = trav_node_step<false>(S, T.node, rf, tlim, stack, T.sp, tn, false);
+                    if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
+                }
+                const bool ended = active && T.node == MFX_TRAV_EXIT;
+                const uint64_t em = __ballot(ended);
+                if (em && pend_lo < pend_hi) {
+                    if (ended) {
+                        finish_ray();
+                        const int rank = __popcll(em & lanes_below());
+                        if (rank < pend_hi - pend_lo) {
+                            start_ray(pend[pend_lo + rank]);
+                            rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
+                            tlim = f_tlim(T.B.t);
+                        }
+                    }
+                    const int ne = __popcll(em), avail = pend_hi - pend_lo;
+                    pend_lo += ne < avail ? ne : avail;
+                }
+                if (__popcll(__ballot(active && T.node >= 0)) < MFX_NODE_LANES_MIN) break;
             }
-            active = false;
+            if (active && T.node == MFX_TRAV_EXIT) {
+                fin = true;
+            } else if (active && T.node < 0) {
+                const int base = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
+                leaf_hit<false, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
+                if (T.sp == 0) {
+                    fin = true;
+                } else {
+                    T.node = stack.get(T.sp - 1, stack.deep(T.sp));
+                    --T.sp;
+                }
+            }
         }
+#else
+        if (active) fin = trav_step<false, STATS, INST>(T, S, stack, tn, st, dg, DG);
+#endif
+        DIAG_MARK(dg, leaf, DG);
+        if (fin) finish_ray();
         DIAG_MARK(dg, fin, DG);
     }
     unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
