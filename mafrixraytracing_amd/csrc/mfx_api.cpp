@@ -847,6 +847,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, ev + 1));
             HIPCHECK(hipEventRecord(ev[2], c->stream));
             if (c->diag_iter) {
+                HIPCHECK(hipStreamSynchronize(c->stream));
                 float fe = 0.f, fs = 0.f;
                 HIPCHECK(hipEventElapsedTime(&fe, ev[0], ev[1]));
                 HIPCHECK(hipEventElapsedTime(&fs, ev[1], ev[2]));
@@ -867,6 +868,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             P.shadow_waves = c->wf_shadow_waves;
             if (ev) HIPCHECK(hipEventRecord(ev[1], c->stream));
             if (ev && c->diag_iter) {
+                HIPCHECK(hipStreamSynchronize(c->stream));
                 float ft = 0.f;
                 HIPCHECK(hipEventElapsedTime(&ft, ev[0], ev[1]));
                 const int rc = diag(g, "tail", qf + 2, ft, 0.f);

@@ -67,7 +67,9 @@
 #endif
 #define WF_CTL_EXT 0                       // [WF_SHARDS * WF_HS] k_extend slot-chunk heads
 #define WF_CTL_SHD (WF_SHARDS * WF_HS)     // [WF_SHARDS * WF_HS] k_shadow slot-chunk heads
-#define WF_NCTL (2 * WF_SHARDS * WF_HS)
+#define WF_CTL_CLOSED_EXT (2 * WF_SHARDS * WF_HS)       // k_extend's closed-shard mask (a line of its own)
+#define WF_CTL_CLOSED_SHD (2 * WF_SHARDS * WF_HS + 16)  // k_shadow's
+#define WF_NCTL (2 * WF_SHARDS * WF_HS + 32)
 // the ray queues' shard counts sit on either side of the heads, so one memset per iteration clears
 // the heads and the next queue's counts: [WF_CTL_Q0 | heads | WF_CTL_Q1], P.ctl = the heads
 #define WF_CTL_Q0 (-WF_SHARDS * WF_HS)

@@ -119,10 +119,14 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
 #ifndef WF_SPREAD
 #define WF_SPREAD 1  // a wave whose shard closed picks the next open shard from a per-wave pseudo-random start
 #endif
+#ifndef WF_CLOSED_MASK
+#define WF_CLOSED_MASK 1  // closed shards are found from one mask word, not from a load of all 64 heads
+#endif
 struct Scanner {
     int win_next, win_end, shard;
     bool exhausted;
     uint32_t spread;  // WF_SPREAD: the wave's pseudo-random walk over the shards
+    uint64_t closed_seen;  // WF_CLOSED_MASK: shards this wave found closed itself
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
     // work are skipped with no further memory round trip. Slots of a taken chunk change only
@@ -133,8 +137,12 @@ struct Scanner {
     // chunks from its block's home shard while it lasts, then from the next open shard.
     // qcount: a ray queue's per-shard entry counts (MFX_RAY_QUEUE: a queue fills shard g's range from
     // its start); null: whole shards
+    // closed: the launch's closed-shard mask (WF_CLOSED_MASK): bit g set by the one fetch that
+    // crosses shard g's end (the fetch whose start lands in [cap, cap + chunk)); a wave also skips the
+    // shards its own fetches found closed, so an unset bit never makes it retry one
     __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
-                                           const int32_t* __restrict__ state, const unsigned long long* qcount) {
+                                           const int32_t* __restrict__ state, const unsigned long long* qcount,
+                                           unsigned long long* closed) {
         if (win_next < win_end) return true;
         if (exhausted) return false;
         while (true) {
@@ -148,7 +156,16 @@ struct Scanner {
                 fill(state);
                 return true;
             }
+#if WF_CLOSED_MASK
+            if (lane_id() == 0 && (int64_t)c < (int64_t)cap + chunk) atomicOr(closed, 1ull << shard);
+            closed_seen |= 1ull << shard;
+            unsigned long long cm = 0;
+            if (lane_id() == 0) cm = __hip_atomic_load(closed, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            cm = __shfl(cm, 0);
+            const uint64_t open = ~(cm | closed_seen);
+#else
             const uint64_t open = open_shards(heads, qcount ? (int)qcount[lane_id() * WF_HS] : shard_size);
+#endif
             if (open == 0) {
                 exhausted = true;
                 return false;
@@ -541,7 +558,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 // list at least 64 slots to trace (or all that are left) from as many windows as it
                 // takes; only state words are read here, WF_LOOKAHEAD windows per round trip
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr, P.ctl + WF_CTL_CLOSED_EXT)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -678,7 +695,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
     uint32_t pk_nodes = 0, pk_slots = 0;  // STATS: the wave's own node and slot fetches (every lane counts them)
-    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr)) {
+    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr, P.ctl + WF_CTL_CLOSED_EXT)) {
         const int j = sc.win_next + lane;
         const int sj = sc.word();
         sc.advance(P.state);
@@ -778,7 +795,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr)) {
+                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr, P.ctl + WF_CTL_CLOSED_SHD)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -1064,7 +1081,7 @@ __global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
         while (m != 0) {
             if (pend_lo == pend_hi) {
                 int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, P.qcount)) {
+                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, P.qcount, P.ctl + WF_CTL_CLOSED_EXT)) {
                     const int j = sc.win_next + lane;
                     const bool take = (sc.word() & WF_STATE_MASK) == WF_NEED_EXT;
                     const uint64_t tm = __ballot(take);

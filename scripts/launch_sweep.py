@@ -42,18 +42,25 @@ def child(scene, spps):
     saved = os.dup(2)
     sys.stderr.flush()
     os.dup2(tf.fileno(), 2)
-    with NativeContext(a, seed=DEFAULT_SEED) as ctx:
-        for spp in spps:
-            for k in range(2):
-                sys.stderr.write(f"@@ spp {spp} rep {k}\n")
-                sys.stderr.flush()
-                ctx.accum_clear()
-                ctx.trace_accumulate(spp, k * spp)
-                ctx.sync()
+    err = None
+    try:
+        with NativeContext(a, seed=DEFAULT_SEED) as ctx:
+            for spp in spps:
+                for k in range(2):
+                    sys.stderr.write(f"@@ spp {spp} rep {k}\n")
+                    sys.stderr.flush()
+                    ctx.accum_clear()
+                    ctx.trace_accumulate(spp, k * spp)
+                    ctx.sync()
+    except Exception as e:  # noqa: BLE001 (reported with the captured library output below)
+        err = e
     sys.stderr.flush()
     os.dup2(saved, 2)
     tf.seek(0)
     text = tf.read().decode()
+    if err is not None:
+        print(text[-3000:], file=sys.stderr)
+        raise err
     cur = None
     for line in text.splitlines():
         m = re.match(r"@@ spp (\d+) rep (\d+)", line)
