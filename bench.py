@@ -318,7 +318,7 @@ def main():
     use_dist = world > 1 or os.environ.get("MFX_BENCH_FORCE_DIST") == "1"
 
     import numpy as np
-    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE
+    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE, MFX_F_WAVEFRONT
     from mafrixraytracing_amd.distributed import PipelinedNativeRender, step_spp
     from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
@@ -462,7 +462,9 @@ def main():
             # the camera-ray packets' own fetches (k_camera's bytes: each node and slot once per wave)
             pk = None
             if not args.megakernel and stage_ms["camera_launches"] > 0:
-                with NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=MFX_F_COUNT_STATS | mode) as sc:
+                # (a 1-spp call runs the megakernel unless the wavefront is pinned: k_camera must run)
+                with NativeContext(arrays, seed=DEFAULT_SEED, device=local,
+                                   flags=MFX_F_COUNT_STATS | MFX_F_WAVEFRONT | mode) as sc:
                     sc.trace_accumulate(1, 10 ** 6)
                     sp = sc.ray_counts()
                 if sp[10] > 0:

@@ -132,6 +132,7 @@ struct mfx_ctx {
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
+    bool wf_pool_q = false;  // the pool holds the ray queues' arrays too (allocated only for a trace that uses them)
     // MFX_RAY_QUEUE: the ray queues, and the first iteration (0-based) whose k_shadow moves the
     // continuing paths to one (-1: every iteration in place; MFX_RAY_QUEUE=0 / MFX_QUEUE_FROM=d)
     WfQueue wq[2]{};
@@ -317,7 +318,8 @@ static int ctx_setup(mfx_ctx* c) {
             c->wf_pool_max = std::max<int64_t>(1 << 20, std::min<int64_t>(c->wf_pool_max, fit));
         }
     }
-    if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, atoll(pm));
+    // (at most 2^28 slots: k_extend's pending entries keep a slot index in 28 bits)
+    if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, std::min<int64_t>(1 << 28, atoll(pm)));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* qf = getenv("MFX_QUEUE_FROM")) c->wf_queue_from = MFX_RAY_QUEUE ? std::max(-2, atoi(qf)) : -1;
     if (const char* qc = getenv("MFX_QCHUNK")) c->wf_qchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(qc) / 64 * 64));
@@ -648,15 +650,17 @@ int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* in
 
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
-// Allocate (or grow) the wavefront path-slot pool (SoA).
-static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
-    if (pool <= c->wf_pool) return MFX_OK;
+// Allocate (or grow) the wavefront path-slot pool (SoA). queues: the trace runs ray queues
+// (MFX_RAY_QUEUE), whose arrays (7 doubles and 7 words per slot) are allocated only then.
+static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
+    if (pool <= c->wf_pool && (!queues || c->wf_pool_q)) return MFX_OK;
     if (c->wf_mem) (void)hipFree(c->wf_mem);
     c->wf_mem = nullptr;
     c->wf_pool = 0;
     const size_t P = (size_t)pool;
     const int nv = c->host.max_depth + 1;  // vertices per path
-    const size_t bytes = P * (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4) + 64 * 256;
+    const size_t per_slot = WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4 - (queues ? 0 : WF_QUEUE_BYTES_PER_SLOT);
+    const size_t bytes = P * per_slot + 64 * 256;
     hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
@@ -673,6 +677,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     c->wf.depth = (int32_t*)take(P * 4);
     c->wf.state = (int32_t*)take(P * 4);
 #if MFX_RAY_QUEUE
+    if (queues) {
     // queue 0: its own arrays; queue 1: the pool's ray arrays (o, d, key, rn: dead once the
     // iterations run on queues) and its own depth, state and slot words
     WfQueue& q0 = c->wq[0];
@@ -692,8 +697,10 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool) {
     }
     q0.count = c->d_wfctl;                                  // WF_CTL_Q0
     q1.count = c->d_wfctl - WF_CTL_Q0 + WF_CTL_Q1;
+    }
 #endif
     c->wf_pool = pool;
+    c->wf_pool_q = queues;
     return MFX_OK;
 }
 
@@ -758,7 +765,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     // generations of whole 64-path windows (one 8x8 tile of one sample each: the camera-ray packets)
     const int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
     const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
-    int rc = wf_ensure_pool(c, pool);
+    const int qf = c->wf_queue_from == -2 ? c->wf_queue_auto : c->wf_queue_from;  // the ray-queue start
+    int rc = wf_ensure_pool(c, pool, qf >= 0);
     if (rc) return rc;
     WfParams P = c->wf;
     fill_scene_params(c, P);
@@ -793,7 +801,6 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     if (own_events) c->cam_last = P.cam_grid > 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     // MFX_TAIL: the iterations after the queue start run as one k_tail launch on queue 0
-    const int qf = c->wf_queue_from == -2 ? c->wf_queue_auto : c->wf_queue_from;
     const bool tail = c->wf_tail && qf >= 0 && qf < P.max_depth;
     const int per_gen = tail ? qf + 1 : P.max_depth + 1;  // bounce-synchronous iterations per generation
     const int iters = (int)ngen * per_gen;

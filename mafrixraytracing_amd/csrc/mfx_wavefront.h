@@ -40,6 +40,9 @@
 // A finished path's state word (WF_DONE, or WF_MISS left by k_extend) carries its lit-vertex mask
 // << WF_SHADE_SHIFT, so k_resolve reads no depth word
 #define WF_STATE_MASK 15
+// A NEED_EXT state word written in place carries the path's lit mask << WF_SHADE_SHIFT too; k_extend's
+// pending entries hold a slot index in 28 bits (pools of at most 2^28 slots), the mask above it
+#define WF_ENTRY_SLOT 0x0fffffff
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
 // depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
 // shadow ray reached the light); so at most WF_MAX_VERTS vertices (max_depth < WF_MAX_VERTS)
@@ -156,6 +159,8 @@ struct WfParams {
 // dead after the pool's last iteration, plus its own depth, state and slot)
 #define WF_DOUBLES_PER_SLOT(nvert) (7 + 3 * (nvert) + (MFX_RAY_QUEUE ? 7 : 0))
 #define WF_WORDS_PER_SLOT(nvert) (3 + (nvert) + (MFX_RAY_QUEUE ? 7 : 0))  // rn, depth, state + the vertices' materials
+// the two ray queues' share of that (queue 0's ray, key and draw count; both queues' depth, state and slot)
+#define WF_QUEUE_BYTES_PER_SLOT (MFX_RAY_QUEUE ? 7 * 8 + 7 * 4 : 0)
 
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)

@@ -505,9 +505,16 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     constexpr bool DG = MFX_DIAG_STAMPS == 1;
     DiagAcc dg{};
     if (DG) dg.last = stamp();
+    // An in-place extension ray's entry carries the path's lit-vertex mask (k_shadow wrote it into
+    // the NEED_EXT state word) in bits 28..30 when it fits (iterations 1..3: vertices 0..2), so a
+    // miss writes its finished state word without loading the depth word (a dependent round trip
+    // in the finishing round: bounce-1 k_extend 8.0 -> 9.1 ms on C2 when it did, r04a)
+    const bool lit_in_entry = !Q && P.iter <= 3;
+    int litm = 0;  // the lane's path's lit mask (lit_in_entry)
     // the lane takes listed entry e: its camera ray (FREE slot) or the slot's extension ray
     auto start_ray = [&](int e) {
-        s = e & 0x7fffffff;
+        s = e & WF_ENTRY_SLOT;
+        litm = (e >> 28) & 7;
         fresh = e < 0;
         DV o, d;
         if (fresh) {
@@ -544,7 +551,8 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
             P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
         } else {  // a later miss finishes the path: its lit mask goes into the state word
-            P.state[s] = WF_MISS | (fresh || Q ? 0 : ((P.depth[s] >> WF_LIT_SHIFT) & 0xffff) << WF_SHADE_SHIFT) | fl;
+            const int lm = fresh || Q ? 0 : (lit_in_entry ? litm : (P.depth[s] >> WF_LIT_SHIFT) & 0xffff);
+            P.state[s] = WF_MISS | (lm << WF_SHADE_SHIFT) | fl;
         }
         active = false;
     };
@@ -570,8 +578,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                         take = !P.tile_padding || path_pixel(P, P.path_base + j, x, y, smp);
                     }
                     const uint64_t tm = __ballot(take);
-                    // entry: slot | camera-ray flag << 31
-                    if (take) pend[n + __popcll(tm & lanes_below())] = sj == WF_FREE ? (j | (int)0x80000000) : j;
+                    // entry: slot | camera-ray flag << 31, or slot | lit mask << 28 (lit_in_entry)
+                    if (take)
+                        pend[n + __popcll(tm & lanes_below())] =
+                            sj == WF_FREE ? (j | (int)0x80000000)
+                                          : (lit_in_entry ? j | (((unsigned)sj >> WF_SHADE_SHIFT) & 7) << 28 : j);
                     n += __popcll(tm);
                     sc.advance(P.state);
                 }
@@ -980,7 +991,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             // continue with the next vertex's remaining depth; or finished: k_resolve folds the
             // recorded vertices (none lit: nothing to add, FREE)
             const int dwn = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-            const int need = WF_NEED_EXT;
+            // in place, NEED_EXT carries the lit mask for k_extend's pending entries (lit_in_entry)
+            const int need = WF_NEED_EXT | (nq ? 0 : mask << WF_SHADE_SHIFT);
             if (nq) {
                 P.ndepth[s] = dwn;
                 P.nstate[s] = need;
