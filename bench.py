@@ -439,7 +439,7 @@ def main():
                           "the weak-scaled job"}
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
                 for k in ("total_ms", "camera_ms", "extend_ms", "camera_launches", "shadow_ms", "iterations", "launches",
-                          "generations", "tail_ms", "tail_launches", "tail_ext_rays", "tail_shadow_rays")}
+                          "generations")}
 
     result = None
     # launches per timed unit: a step, or (--api render) one 1-spp call
@@ -566,10 +566,8 @@ def main():
                         "smem_per_launch": kv["smem_per_launch"], "peak_case": tdroof["smem_peak"]["case"],
                         "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
 
-            def kernel_roofline(kname, kms, krays, launches, bray, bytes_total=None):
+            def kernel_roofline(kname, kms, krays, launches, bray):
                 # per launch: (rays/launch * B/ray) / (ms/launch) == per-step totals
-                if bytes_total is not None:  # a kernel tracing both kinds of ray (k_tail)
-                    bray = bytes_total / krays if krays else 0.0
                 achieved = krays * bray / (kms / 1e3) / 1e9
                 traffic = None
                 if tdata:  # rocprof names the instance: k_shadow<false> or k_shadow<false, SPILL, ...>;
@@ -623,18 +621,11 @@ def main():
                     kc["note"] = ("HBM index priced at the bytes the packets fetch (each node and slot once per wave, "
                                   "through the scalar cache); its binding roof is the scalar-load rate (smem)")
                     ks.append((stage_ms["camera_ms"], kc))
-                t_ext, t_shd = stage_ms["tail_ext_rays"], stage_ms["tail_shadow_rays"]  # k_tail's, per step
-                ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt - t_ext
+                ext_rays = (closest_rays - (primary_rays if cl > 0 else 0.0)) / nt
                 ext_ms = stage_ms["extend_ms"] - stage_ms["camera_ms"]
                 ks.append((ext_ms, kernel_roofline("k_extend<false>", ext_ms, ext_rays, launches - cl, bc)))
                 ks.append((stage_ms["shadow_ms"], kernel_roofline("k_shadow<false>", stage_ms["shadow_ms"],
-                                                                  (rays - closest_rays) / nt - t_shd, launches, bs)))
-                if stage_ms["tail_launches"] > 0:
-                    kt = kernel_roofline("k_tail<false>", stage_ms["tail_ms"], t_ext + t_shd, stage_ms["tail_launches"],
-                                         0.0, bytes_total=t_ext * bc + t_shd * bs)
-                    kt["note"] = ("the paths' bounces after the ray-queue start, extension and shadow rays of one lane "
-                                  "each; bytes priced at the closest / shadow B_ray of its rays")
-                    ks.append((stage_ms["tail_ms"], kt))
+                                                                  (rays - closest_rays) / nt, launches, bs)))
                 ks.sort(key=lambda x: -x[0])
                 roofline = dict(ks[0][1])
                 roofline["other_kernels"] = [k for _, k in ks[1:]]

@@ -249,13 +249,10 @@ int mfx_last_trace_ms(mfx_ctx* ctx, double* ms);
  * kernels (path start + closest hit: k_camera and k_extend), out[4] = k_shadow (shading + shadow
  * ray + path finish); out[1] = the part of out[2] spent in k_camera (each generation's camera
  * rays traced as packets, flat scenes) and out[3] = its launches (0 when k_extend traced them);
- * the per-generation k_resolve launches make up the rest of out[0]; out[5] = bounce-synchronous
- * iterations (max_depth + 1 per generation, or up to the ray-queue start when k_tail runs the
- * rest), out[6] = launches of each stage (= out[5]), out[7] = generations; out[8] = the k_tail
- * launches' time (the paths' remaining bounces after the queue start, one launch per generation),
- * out[9] = their count, out[10] / out[11] = the extension / shadow rays they traced.
- * Megakernel: out[0] = out[2] = its single launch.                                            */
-int mfx_trace_timing(mfx_ctx* ctx, double out[12]);
+ * the per-generation k_resolve launches make up the rest of out[0]; out[5] = iterations
+ * (max_depth + 1 per generation), out[6] = launches of each stage (= out[5]), out[7] =
+ * generations. Megakernel: out[0] = out[2] = its single launch.                               */
+int mfx_trace_timing(mfx_ctx* ctx, double out[8]);
 
 /* Ray counters of the last mfx_trace_accumulate / mfx_sample call:
  * out[0] = primary, out[1] = extension (closest-hit queries actually traced, excluding the

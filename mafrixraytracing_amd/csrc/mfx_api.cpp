@@ -149,15 +149,6 @@ struct mfx_ctx {
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
     int it_per_gen = 0;                     // and per generation
-    // MFX_TAIL (default on): once a trace moves its paths to queue 0, one k_tail launch per generation
-    // runs them to their ends instead of the remaining bounce-synchronous iterations
-    bool wf_tail = true;
-    int wf_tail_grid = 0;
-    int wf_tail_waves = 4;                  // k_tail's register budget: 3 or 4 waves per SIMD
-    int32_t wf_tchunk = 256;                // queue entries per k_tail chunk fetch (MFX_TCHUNK)
-    std::vector<hipEvent_t> tail_ev;        // per generation: k_tail start, end
-    int tail_recorded = 0;                  // k_tail launches of the last trace with events
-    int tail_iter = -1;                     // the first iteration k_tail ran (-1: none)
     int generations = 0;
     bool mega_last = false;
     bool cam_last = false;  // the last wavefront trace ran its camera rays as packets (k_camera)
@@ -249,8 +240,6 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
-    for (hipEvent_t e : c->tail_ev)
-        if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -323,8 +312,6 @@ static int ctx_setup(mfx_ctx* c) {
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* qf = getenv("MFX_QUEUE_FROM")) c->wf_queue_from = MFX_RAY_QUEUE ? std::max(-2, atoi(qf)) : -1;
     if (const char* qc = getenv("MFX_QCHUNK")) c->wf_qchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(qc) / 64 * 64));
-    if (const char* tc = getenv("MFX_TCHUNK")) c->wf_tchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(tc) / 64 * 64));
-    if (const char* te = getenv("MFX_TAIL")) c->wf_tail = atoi(te) != 0;
     if (const char* rq = getenv("MFX_RAY_QUEUE")) {
         if (atoi(rq) == 0) c->wf_queue_from = -1;
     }
@@ -439,14 +426,6 @@ static int ctx_setup(mfx_ctx* c) {
         }
     }
     c->wf_shd_grid = prop.multiProcessorCount * std::max(1, std::min(sbpc, 8));
-    {  // k_tail: the LDS of k_shadow's stack share and top nodes minus its lists, the register budget of its build
-        c->wf_tail_waves = c->wf_shadow_waves;
-        if (const char* e = getenv("MFX_TAIL_WAVES")) c->wf_tail_waves = atoi(e) == 3 ? 3 : 4;
-        int tb = 0;
-        CK(mfx_tail_occupancy(c->wf_stack_lds_shd, c->wf_stack_lds_shd < c->stack_size, c->wf_ntop_shd, ninst,
-                              c->wf_tail_waves, &tb, c->wf_nslot_shd));
-        c->wf_tail_grid = prop.multiProcessorCount * std::max(1, std::min(tb, 8));
-    }
     {  // deep traversal-stack entries of every lane of the larger grid
         const size_t lanes = (size_t)std::max(c->wf_ext_grid, c->wf_shd_grid) * 256;
         const int deep = c->stack_size - std::min(c->wf_stack_lds_ext, c->wf_stack_lds_shd);
@@ -800,19 +779,12 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.cam_grid = c->host.inst.empty() ? c->wf_cam_grid : 0;
     if (own_events) c->cam_last = P.cam_grid > 0;
     const int64_t ngen = (total + gen_max - 1) / gen_max;
-    // MFX_TAIL: the iterations after the queue start run as one k_tail launch on queue 0
-    const bool tail = c->wf_tail && qf >= 0 && qf < P.max_depth;
-    const int per_gen = tail ? qf + 1 : P.max_depth + 1;  // bounce-synchronous iterations per generation
+    const int per_gen = P.max_depth + 1;  // bounce-synchronous iterations per generation
     const int iters = (int)ngen * per_gen;
     while (own_events && (int)c->it_ev.size() < 3 * iters) {
         hipEvent_t e;
         HIPCHECK(hipEventCreate(&e));
         c->it_ev.push_back(e);
-    }
-    while (own_events && tail && (int)c->tail_ev.size() < 2 * ngen) {
-        hipEvent_t e;
-        HIPCHECK(hipEventCreate(&e));
-        c->tail_ev.push_back(e);
     }
     // MFX_DIAG_ITER=1: per-iteration ray counts and stage times on stderr
     auto diag = [&](int64_t g, const char* what, int d, float fe, float fs) -> int {
@@ -862,26 +834,6 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
                 if (rc) return rc;
             }
         }
-        if (tail) {  // iterations qf + 1 .. max_depth: every path of queue 0 to its end
-            P.start = 0;
-            P.iter = qf + 1;
-            wf_queue_views(c, P, qf + 1);
-            P.ncount = nullptr;  // k_tail continues paths in their own entries: no next queue
-            P.chunk = c->wf_chunk_env ? chunk0 : c->wf_tchunk;
-            hipEvent_t* ev = own_events ? c->tail_ev.data() + 2 * g : nullptr;
-            if (ev) HIPCHECK(hipEventRecord(ev[0], c->stream));
-            P.shadow_waves = c->wf_tail_waves;  // (k_tail's own build)
-            HIPCHECK(mfx_wf_tail(P, c->wf_tail_grid, stats, c->stream));
-            P.shadow_waves = c->wf_shadow_waves;
-            if (ev) HIPCHECK(hipEventRecord(ev[1], c->stream));
-            if (ev && c->diag_iter) {
-                HIPCHECK(hipStreamSynchronize(c->stream));
-                float ft = 0.f;
-                HIPCHECK(hipEventElapsedTime(&ft, ev[0], ev[1]));
-                const int rc = diag(g, "tail", qf + 2, ft, 0.f);
-                if (rc) return rc;
-            }
-        }
         wf_queue_views(c, P, -1);  // k_resolve reads the pool's final state and depth words
         HIPCHECK(mfx_wf_resolve(P, c->stream));
     }
@@ -903,8 +855,6 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     }
     c->it_recorded = iters;
     c->it_per_gen = per_gen;
-    c->tail_recorded = tail ? (int)ngen : 0;
-    c->tail_iter = tail ? qf + 1 : -1;
     c->generations = (int)ngen;
     return MFX_OK;
 }
@@ -1028,7 +978,7 @@ int mfx_accum_reduce(mfx_ctx* c) {
     return MFX_OK;
 }
 
-int mfx_trace_timing(mfx_ctx* c, double out[12]) {
+int mfx_trace_timing(mfx_ctx* c, double out[8]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
     if (c->rep_valid) {  // a call served from held frames: its batch's device time, no stage split
         for (int k = 0; k < 12; ++k) out[k] = 0.0;
@@ -1038,7 +988,7 @@ int mfx_trace_timing(mfx_ctx* c, double out[12]) {
     double total = 0;
     int rc = mfx_last_trace_ms(c, &total);
     if (rc) return rc;
-    for (int k = 0; k < 12; ++k) out[k] = 0.0;
+    for (int k = 0; k < 8; ++k) out[k] = 0.0;
     out[0] = total;
     if (c->mega_last) {
         out[2] = total;
@@ -1064,23 +1014,6 @@ int mfx_trace_timing(mfx_ctx* c, double out[12]) {
         out[5] = c->it_recorded;
         out[6] = c->it_recorded;
         out[7] = c->generations;
-        // [8] the k_tail launches' time, [9] their count, [10] / [11] their extension / shadow rays
-        for (int g = 0; g < c->tail_recorded; ++g) {
-            float ft = 0.f;
-            HIPCHECK(hipEventElapsedTime(&ft, c->tail_ev[2 * g], c->tail_ev[2 * g + 1]));
-            out[8] += ft;
-        }
-        out[9] = c->tail_recorded;
-        if (c->tail_recorded > 0) {
-            unsigned long long h[WF_NCTR * WF_SHARDS];
-            HIPCHECK(hipMemcpy(h, c->d_counters, sizeof(h), hipMemcpyDeviceToHost));
-            for (int g = 0; g < WF_SHARDS; ++g) {
-                const unsigned long long* x = h + WF_NCTR * g;
-                out[11] += (double)x[3];
-                for (int d = std::max(1, c->tail_iter); d < WF_ITER_CTRS; ++d) out[10] += (double)x[WF_CTR_ITER + d];
-                if (c->host.max_depth >= WF_ITER_CTRS) out[10] += (double)x[1];  // deeper vertices (counter 1)
-            }
-        }
     }
     return MFX_OK;
 }

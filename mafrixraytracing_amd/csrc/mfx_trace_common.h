@@ -509,18 +509,19 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
 // when B improved.
 // base: the slot index the code counts from (an instance's run of world slots; 0 otherwise).
 // UNI: the leaf is wave-uniform (packet traversal): its slots are read through scalar loads.
-// RT: the query kind is the per-lane runtime flag shd_rt instead of SHADOW (k_tail's lanes trace
-// closest-hit and shadow queries side by side).
-template <bool SHADOW, bool STATS, bool UNI = false, bool RT = false>
+#ifndef MFX_SLOT_LDS
+#define MFX_SLOT_LDS 1  // small scenes' slots read from the kernels' LDS copy (SceneView::slots_lds)
+#endif
+template <bool SHADOW, bool STATS, bool UNI = false>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
-                                         Best& B, Stats& st, int base = 0, bool shd_rt = false) {
-    const bool shd = RT ? shd_rt : SHADOW;
+                                         Best& B, Stats& st, int base = 0) {
+    constexpr bool shd = SHADOW;
     const int s0 = base + (code >> 3), n = (code & 7) + 1;
     const MfxSlot* __restrict__ sl = S.slots + s0;
     if (STATS) st.clusters++;
     bool improved = false;
     constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
-    const bool in_lds = !UNI && S.nslot_lds > 0;  // the LDS copy holds every slot (wave-uniform)
+    const bool in_lds = MFX_SLOT_LDS && !UNI && S.nslot_lds > 0;  // the LDS copy holds every slot (wave-uniform)
     for (int k = 0; k < n; ++k) {
 #if MFX_LEAF_PRELOAD
         SlotR r = UNI ? load_slot_u(sl + k) : (in_lds ? load_slot_lds(S.slots_lds, s0 + k) : load_slot(sl + k));
@@ -738,11 +739,9 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
     return node;
 }
 
-// far_rt: the child order as a per-lane runtime flag (k_tail); FAR calls leave it at its default
 template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0},
-                                         bool far_rt = FAR) {
+                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
@@ -776,7 +775,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = n <= f;
-        d[k] = h ? (far_rt ? -f : n) : __builtin_inff();
+        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
         nh += h ? 1 : 0;
     }
     cswap(d[0], c[0], d[1], c[1]);

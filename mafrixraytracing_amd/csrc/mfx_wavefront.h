@@ -56,7 +56,7 @@
 #ifndef WF_LOOKAHEAD
 #define WF_LOOKAHEAD 4  // windows whose state words a scan loads in one round
 #endif
-#define WF_NCTR 24  // counters per shard: [0..2] rays, [3] k_tail's shadow rays, [4..9] traversal statistics, [10..17] diagnostics,
+#define WF_NCTR 24  // counters per shard: [0..2] rays, [3] unused, [4..9] traversal statistics, [10..17] diagnostics,
                     // [WF_CTR_ITER + d] extension rays of iteration d (1 <= d < WF_ITER_CTRS; [1]
                     // holds the others, and the host's sums add these into it)
 #define WF_CTR_ITER 18
@@ -179,9 +179,6 @@ struct WfParams {
 // (and nslot slots' test prefixes)
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu,
                                    int nslot = 0);
-// resident blocks per CU of k_tail (the same stack share, top nodes and slots as k_shadow, its wave build)
-hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu,
-                              int nslot = 0);
 // resident blocks per CU of k_camera (camera-ray packets)
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu);
 // a ray queue's arrays (MFX_RAY_QUEUE): entries in the pool's shard ranges, counts per shard
@@ -195,9 +192,6 @@ struct WfQueue {
 // one iteration (extend, shadow); ev[0] is recorded between the two kernels (ev may be null)
 hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                             hipEvent_t* ev);
-// the rest of every path in the queue P reads (P.qcount) in one launch (k_tail): iterations
-// q + 1 .. max_depth of the paths the queue-start iteration q moved to queue 0
-hipError_t mfx_wf_tail(const WfParams& P, int grid, bool stats, hipStream_t st);
 // after a generation's last iteration: add its finished paths' radiance to their pixels
 hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st);
 

@@ -235,30 +235,20 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
     T.inst_sp = 0;
 }
 
-// one node step of the per-lane traversal (BVH4; shadow rays far-first); shd: the query kind
+// one node step of the per-lane traversal (BVH4; shadow rays far-first)
 template <bool SHADOW, typename ST>
 __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, const RayF& rf, float tlim, const ST& stack,
-                                              int& sp, TopNodes tn, bool shd) {
-    return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn,
-                                                            shd && MFX_SHADOW_ORDER == 1);
+                                              int& sp, TopNodes tn) {
+    return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
 }
-
-#ifndef MFX_INLOOP_REFILL
-#define MFX_INLOOP_REFILL 0  // experiment (A/B variant): k_extend refills lanes whose walk ended inside the node loop
-#endif
-#ifndef MFX_NODE_LANES_MIN_TAIL
-#define MFX_NODE_LANES_MIN_TAIL 14  // k_tail's node-loop exit (its lanes mix closest-hit and shadow rays)
-#endif
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
 // INST: a two-level scene; a lane enters and leaves instances inside the node loop (inst_frame).
-// RT: the query kind is the lane's runtime flag shd_rt (k_tail) instead of SHADOW.
-template <bool SHADOW, bool STATS, bool INST, typename ST, bool RT = false>
+template <bool SHADOW, bool STATS, bool INST, typename ST>
 __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
-                                          DiagAcc& dg, bool diag, bool shd_rt = false) {
-    const bool shd = RT ? shd_rt : SHADOW;
+                                          DiagAcc& dg, bool diag) {
     // the frame of the entry popped at the end of the last round (an instance left or entered)
     RayF rf{};  // (the frame switch's own ray update is superseded below)
     if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
@@ -272,13 +262,11 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (STATS && !SHADOW && T.B.found) st.after_nodes++;
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = trav_node_step<SHADOW>(S, T.node, rf, tlim, stack, T.sp, tn, shd);
+        T.node = trav_node_step<SHADOW>(S, T.node, rf, tlim, stack, T.sp, tn);
         if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
-        if (__popcll(__ballot(T.node >= 0)) <
-            (RT ? MFX_NODE_LANES_MIN_TAIL : (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)))
-            break;
+        if (__popcll(__ballot(T.node >= 0)) < (SHADOW ? MFX_NODE_LANES_MIN_SHD : MFX_NODE_LANES_MIN)) break;
     }
     DIAG_MARK(dg, node, diag);
     if (T.node >= 0) return false;
@@ -287,9 +275,9 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     if (STATS && !SHADOW && T.B.found) st.after_leaves++;
 #endif
     const int base = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
-    const bool better = leaf_hit<SHADOW, STATS, false, RT>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base, shd);
+    const bool better = leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
     if (better) {
-        if (shd) {
+        if (SHADOW) {
             T.B.found = true;
             return true;
         }
@@ -605,53 +593,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
-#if MFX_INLOOP_REFILL
-        // Experiment: a lane whose walk ends inside the node loop (stack empty, no child hit) writes
-        // its result and takes the next listed ray there, instead of idling until the loop exits
-        if (active) {
-            RayF rf{};
-            if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
-            rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
-            float tlim = f_tlim(T.B.t);
-            while (true) {
-                if (active && T.node >= 0) {
-                    if (STATS) st.nodes++;
-                    T.node = trav_node_step<false>(S, T.node, rf, tlim, stack, T.sp, tn, false);
-                    if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
-                }
-                const bool ended = active && T.node == MFX_TRAV_EXIT;
-                const uint64_t em = __ballot(ended);
-                if (em && pend_lo < pend_hi) {
-                    if (ended) {
-                        finish_ray();
-                        const int rank = __popcll(em & lanes_below());
-                        if (rank < pend_hi - pend_lo) {
-                            start_ray(pend[pend_lo + rank]);
-                            rf = INST ? frame_ray(S, T.inst, T.o, T.d) : make_rayf(T.o, T.d);
-                            tlim = f_tlim(T.B.t);
-                        }
-                    }
-                    const int ne = __popcll(em), avail = pend_hi - pend_lo;
-                    pend_lo += ne < avail ? ne : avail;
-                }
-                if (__popcll(__ballot(active && T.node >= 0)) < MFX_NODE_LANES_MIN) break;
-            }
-            if (active && T.node == MFX_TRAV_EXIT) {
-                fin = true;
-            } else if (active && T.node < 0) {
-                const int base = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
-                leaf_hit<false, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
-                if (T.sp == 0) {
-                    fin = true;
-                } else {
-                    T.node = stack.get(T.sp - 1, stack.deep(T.sp));
-                    --T.sp;
-                }
-            }
-        }
-#else
         if (active) fin = trav_step<false, STATS, INST>(T, S, stack, tn, st, dg, DG);
-#endif
         DIAG_MARK(dg, leaf, DG);
         if (fin) finish_ray();
         DIAG_MARK(dg, fin, DG);
@@ -1030,183 +972,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     }
 }
 
-// ------------------------------------------------------------------------------------------------
-// k_tail: the rest of every path in a ray queue, in one launch (MFX_TAIL). From the iteration whose
-// k_shadow moved the continuing paths to queue 0, each lane takes one queued path and runs it to its
-// end: its extension ray (closest hit), the vertex's shading, its shadow ray, and so on — the work
-// of iterations q + 1 .. max_depth, which otherwise cost 2 (max_depth - q) sparse bounce-synchronous
-// launches, each with a fixed ~0.2-0.4 ms of ramp and tail (scripts/launch_sweep.py). The lanes of a
-// wave trace closest-hit and shadow rays side by side (trav_step's runtime query kind) and a lane
-// whose ray finishes is refilled from the queue at once (persistent while-while). Every vertex is
-// the same FP64 arithmetic as k_shadow's (sample_vertex) on the same draws, and its records go to the
-// path's slot (qslot), so k_resolve and the images are unchanged.
-// A lane's path state between phases stays in its queue entry e: the next direction wi (dx..dz) and
-// the draw count (rn) are written back there at shading and read when the shadow ray finishes.
-// ------------------------------------------------------------------------------------------------
-#define WF_TAIL_PEND 128  // k_tail per-wave list of queue entries
-template <bool STATS, bool SPILL, int WAVES, bool INST>
-__global__ void __launch_bounds__(256, WAVES) k_tail(WfParams P) {
-    extern __shared__ int lds_all[];
-    const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
-    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
-    MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
-    if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
-    int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
-    if (P.nslot_shd) load_slots_lds(slot_lds, P.slots, P.nslot_shd);
-    int* lds = (int*)(slot_lds + 5 * P.nslot_shd);
-    const int lane = lane_id();
-    const int wave = threadIdx.x >> 6;
-    using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
-    const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_shd * 64 + lane, P, P.stack_lds_shd);
-    int* pend = lds + 4 * P.stack_lds_shd * 64 + wave * WF_TAIL_PEND;
-    int* scratch = lds + 4 * P.stack_lds_shd * 64 + 4 * WF_TAIL_PEND + wave * 64;  // the sampler's
-    uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_shd * 64 + 4 * WF_TAIL_PEND + 4 * 64);
-    uint32_t* vctr = red + 16;  // [WF_ITER_CTRS] the block's extension rays by vertex index ([0]: deeper)
-    if (threadIdx.x < WF_ITER_CTRS) vctr[threadIdx.x] = 0;
-    __syncthreads();
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_shd};
-    const int shard_size = P.pool / WF_SHARDS;
-
-    Scanner sc{};
-    sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
-    int pend_lo = 0, pend_hi = 0;
-    bool active = false;
-    bool shd = false;  // the lane's ray: false the path's extension ray, true its vertex's shadow ray
-    int e = 0;         // the lane's queue entry
-    int dw = 0;        // extension ray: the path's depth word; shadow ray: k_shadow's vflag (cn, lightable, v, lit mask)
-    double scs = 0.0, ssolid = 0.0;  // the operands of this vertex's direct term a_v (cs, solid)
-    Trav T{};
-    uint32_t c_shadow = 0;
-    Stats st{0, 0, 0}, st2{0, 0, 0};
-    DiagAcc dg{};
-    // an extension ray leaving with depth word w finds vertex max_depth - (w & 0xff): counted per vertex
-    auto count_ext = [&](int w) {
-        const int vi = P.max_depth - (w & 0xff);
-        atomicAdd(vctr + (vi < WF_ITER_CTRS ? vi : 0), 1u);
-    };
-
-    while (true) {
-        // ---- idle lanes take queued paths (their extension rays) ----
-        bool idle = !active;
-        uint64_t m = __ballot(idle);
-        while (m != 0) {
-            if (pend_lo == pend_hi) {
-                int n = 0;
-                while (n < 64 && sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, P.qcount, P.ctl + WF_CTL_CLOSED_EXT)) {
-                    const int j = sc.win_next + lane;
-                    const bool take = (sc.word() & WF_STATE_MASK) == WF_NEED_EXT;
-                    const uint64_t tm = __ballot(take);
-                    if (take) pend[n + __popcll(tm & lanes_below())] = j;
-                    n += __popcll(tm);
-                    sc.advance(P.state);
-                }
-                wave_lds_sync();
-                pend_lo = 0;
-                pend_hi = n;
-                if (n == 0) break;  // every queue range taken
-            }
-            const int avail = pend_hi - pend_lo;
-            const int rank = __popcll(m & lanes_below());
-            if (idle && rank < avail) {
-                e = pend[pend_lo + rank];
-                dw = P.depth[e];
-                trav_begin(T, S, dv(P.ox[e], P.oy[e], P.oz[e]), dv(P.dx[e], P.dy[e], P.dz[e]), 99999999.);  // Integrators.fs:108
-                shd = false;
-                count_ext(dw);
-                idle = false;
-                active = true;
-            }
-            const int pm = __popcll(m);
-            pend_lo += pm < avail ? pm : avail;
-            m = __ballot(idle);
-        }
-        if (!__any(active)) break;  // every queued path finished
-        bool fin = false;
-        if (active) fin = trav_step<false, STATS, INST, Stack, true>(T, S, stack, tn, shd ? st2 : st, dg, false, shd);
-
-        // ---- a finished shadow ray: its vertex's direct term, then the next extension ray or the end ----
-        if (fin && shd) {
-            const int v = (dw >> 2) & 15;
-            int mask = (dw >> WF_LIT_SHIFT) & 0xffff;
-            const int jr = P.qslot[e];
-            if (!T.B.found && (dw & 2)) {  // unoccluded: record the operands of its direct term a_v
-                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + jr;
-                vl[0] = scs;
-                vl[P.vstride] = ssolid;
-                mask |= 1 << v;
-            }
-            const int dwn = ((P.max_depth - v - 1) & 0xff) | (mask << WF_LIT_SHIFT);
-            if (dw & 1) {  // the path continues from the hit point (the shadow ray's origin) along wi
-                const DV o = T.o;
-                trav_begin(T, S, o, dv(P.dx[e], P.dy[e], P.dz[e]), 99999999.);
-                dw = dwn;
-                shd = false;
-                fin = false;
-                count_ext(dw);
-            } else {  // finished: k_resolve folds the recorded vertices (none lit: black, nothing to write)
-                if (mask) P.fstate[jr] = WF_DONE | (mask << WF_SHADE_SHIFT);
-                active = false;
-            }
-        }
-        // ---- a finished extension ray: a miss ends the path, a hit is shaded ----
-        if (fin && !shd && !T.B.found) {
-            if (dw >> WF_LIT_SHIFT) P.fstate[P.qslot[e]] = WF_DONE | ((dw >> WF_LIT_SHIFT) << WF_SHADE_SHIFT);
-            active = false;
-        }
-        const bool own = fin && !shd && T.B.found;
-        if (__any(own)) {
-            // one vertex of PathIntegrator.TraceRay (Integrators.fs:109-136) for the lanes at a hit
-            DV hp = dv(0, 0, 0), nm = dv(0, 0, 0);
-            uint64_t key = 0;
-            uint32_t rn = 0;
-            int mat = 0, jr = 0;
-            if (own) {
-                hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
-                const MfxShade sh = P.shade[T.B.info & MFX_INFO_SHADE_MASK];
-                if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
-                else nm = ld3(sh.n);
-                mat = sh.material;
-                key = P.key[e];
-                rn = P.rn[e];
-                jr = P.qslot[e];
-            }
-            const VertexSample V = sample_vertex(P, own, hp, nm, key, rn, scratch);
-            if (own) {
-                const int v = P.max_depth - (dw & 0xff);  // this vertex's index
-                P.vei[v * P.vstride + jr] = V.ei;
-                P.vmat[v * P.vstride + jr] = (WfMat)mat;
-                // the depth -1 query's result is discarded (Integrators.fs:109): never traced
-                const bool cn = (dw & 0xff) - 1 >= 0;
-                if (cn) {  // what the next vertex reads, in the path's queue entry
-                    P.dx[e] = V.wi.x; P.dy[e] = V.wi.y; P.dz[e] = V.wi.z;
-                    P.rn[e] = rn;
-                }
-                dw = (cn ? 1 : 0) | (V.lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
-                scs = V.cs;
-                ssolid = V.solid;
-                // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
-                trav_begin(T, S, hp, V.unit, V.dist - 1e-6);
-                shd = true;
-                c_shadow++;
-            }
-        }
-    }
-    unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
-    block_add<4>(cnt + 2, c_shadow, red);
-    block_add<4>(cnt + 3, c_shadow, red);  // the tail's own shadow rays (mfx_trace_timing)
-    if (threadIdx.x < WF_ITER_CTRS && vctr[threadIdx.x])
-        atomicAdd(cnt + (threadIdx.x ? WF_CTR_ITER + threadIdx.x : 1), (unsigned long long)vctr[threadIdx.x]);
-    if (STATS) {
-        block_add<4>(cnt + 4, st.nodes, red);
-        block_add<4>(cnt + 5, st.clusters, red);
-        block_add<4>(cnt + 6, st.prims, red);
-        block_add<4>(cnt + 7, st2.nodes, red);
-        block_add<4>(cnt + 8, st2.clusters, red);
-        block_add<4>(cnt + 9, st2.prims, red);
-    }
-}
-
 #ifndef WF_RES_VERTS
 #define WF_RES_VERTS 4  // vertices k_resolve loads in one round (max_depth 3 paths); deeper ones in a loop
 #endif
@@ -1474,53 +1239,6 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     e = P.inst ? launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s)
                : launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s);
     if (e != hipSuccess) return e;
-    return hipGetLastError();
-}
-
-static size_t tail_lds_bytes(int stack_size, int ntop, int ninst, int nslot) {
-    return (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
-           (size_t)4 * stack_size * 64 * sizeof(int) +
-           (size_t)4 * (WF_TAIL_PEND + 64) * sizeof(int) + 64 + 4 * WF_ITER_CTRS;
-}
-
-template <bool SPILL, int WAVES, bool INST>
-static void launch_tail(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
-    if (stats) hipLaunchKernelGGL((k_tail<true, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
-    else hipLaunchKernelGGL((k_tail<false, SPILL, WAVES, INST>), dim3(grid), dim3(256), lds, st, P);
-}
-
-hipError_t mfx_tail_occupancy(int stack_lds, bool spill, int ntop, int ninst, int waves, int* blocks_per_cu, int nslot) {
-    const bool inst = ninst > 0;
-    const size_t lds = tail_lds_bytes(stack_lds, ntop, std::min(ninst, WF_INST_LDS), nslot);
-    const void* k;
-    if (waves == 3)
-        k = inst ? (spill ? (const void*)k_tail<false, true, 3, true> : (const void*)k_tail<false, false, 3, true>)
-                 : (spill ? (const void*)k_tail<false, true, 3, false> : (const void*)k_tail<false, false, 3, false>);
-    else
-        k = inst ? (spill ? (const void*)k_tail<false, true, 4, true> : (const void*)k_tail<false, false, 4, true>)
-                 : (spill ? (const void*)k_tail<false, true, 4, false> : (const void*)k_tail<false, false, 4, false>);
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds);
-    *blocks_per_cu = std::min(*blocks_per_cu, wf_lds_blocks(lds));
-    return e;
-}
-
-hipError_t mfx_wf_tail(const WfParams& P, int grid, bool stats, hipStream_t st) {
-    const int ni = P.inst ? P.ninst_lds : 0;
-    const size_t lds = tail_lds_bytes(P.stack_lds_shd, P.ntop_shd, ni, P.nslot_shd);
-    hipError_t e = hipMemsetAsync(P.ctl, 0, WF_NCTL * sizeof(unsigned long long), st);
-    if (e != hipSuccess) return e;
-    const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
-    if (P.inst) {
-        if (spill && w3) launch_tail<true, 3, true>(P, grid, stats, st, lds);
-        else if (spill) launch_tail<true, 4, true>(P, grid, stats, st, lds);
-        else if (w3) launch_tail<false, 3, true>(P, grid, stats, st, lds);
-        else launch_tail<false, 4, true>(P, grid, stats, st, lds);
-    } else {
-        if (spill && w3) launch_tail<true, 3, false>(P, grid, stats, st, lds);
-        else if (spill) launch_tail<true, 4, false>(P, grid, stats, st, lds);
-        else if (w3) launch_tail<false, 3, false>(P, grid, stats, st, lds);
-        else launch_tail<false, 4, false>(P, grid, stats, st, lds);
-    }
     return hipGetLastError();
 }
 

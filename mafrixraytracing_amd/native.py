@@ -146,11 +146,10 @@ class NativeContext:
         return ms.value
 
     def trace_timing(self) -> dict:
-        out = np.zeros(12)
+        out = np.zeros(8)
         check(self.lib.mfx_trace_timing(self._h, dptr(out)), "mfx_trace_timing")
         return {"total_ms": out[0], "camera_ms": out[1], "extend_ms": out[2], "camera_launches": int(out[3]),
-                "shadow_ms": out[4], "iterations": int(out[5]), "launches": int(out[6]), "generations": int(out[7]),
-                "tail_ms": out[8], "tail_launches": int(out[9]), "tail_ext_rays": out[10], "tail_shadow_rays": out[11]}
+                "shadow_ms": out[4], "iterations": int(out[5]), "launches": int(out[6]), "generations": int(out[7])}
 
     def closest_hit(self, rays: np.ndarray, tmin: float = 1e-6, tmax: float = 99999999.0):
         rays = np.ascontiguousarray(rays, dtype=np.float64).reshape(-1, 6)

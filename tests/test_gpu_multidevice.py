@@ -136,9 +136,9 @@ def test_one_sample_calls_megakernel_equals_wavefront(gpu):
         for _ in range(3):
             assert np.array_equal(auto.render_rgba8(1), wf.render_rgba8(1))
             assert np.array_equal(auto.ray_counts()[:4], wf.ray_counts()[:4])
-            tw = wf.trace_timing()  # 4 bounce-synchronous iterations, or those up to the queue start + k_tail
+            tw = wf.trace_timing()  # 4 bounce-synchronous iterations
             assert auto.trace_timing()["launches"] == 1
-            assert tw["launches"] == 4 or (tw["tail_launches"] == 1 and 1 <= tw["launches"] < 4), tw
+            assert tw["launches"] == 4, tw
         assert np.array_equal(auto.film_mean(), wf.film_mean())
         assert np.array_equal(auto.sample(1), wf.sample(1))
     # two devices of one sample each: every device takes the megakernel

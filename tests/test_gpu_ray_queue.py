@@ -4,9 +4,8 @@ the scattered slots. The choice only moves data, so every mode must give the ora
 bit with the same ray counts: in place (-1), queues from the first vertex (0) or the second (1, 2),
 automatic (-2: the live share per iteration of the previous trace decides), small chunks, odd
 films, max_depth 5 (three queue hand-overs, both queues reused), two-level instancing, several
-generations (a small pool), and the render-ahead planes. Each mode runs twice: the remaining
-bounces after the queue start as bounce-synchronous queue iterations (MFX_TAIL=0) and as one k_tail
-launch (MFX_TAIL=1, the default), with small and large chunks of each."""
+generations (a small pool), and the render-ahead planes. Each mode runs with small and large
+chunks of queue entries."""
 import os
 
 import numpy as np
@@ -17,9 +16,8 @@ from conftest import SEED, scene
 pytestmark = pytest.mark.gpu
 
 MODES = ["-1", "0", "1", "2", "-2"]
-# (the remaining bounces after the queue start: queue iterations or k_tail) x chunk sizes
-TAILS = [{"MFX_TAIL": "0", "MFX_QCHUNK": "256"}, {"MFX_TAIL": "0", "MFX_QCHUNK": "64"},
-         {"MFX_TAIL": "1", "MFX_TCHUNK": "256"}, {"MFX_TAIL": "1", "MFX_TCHUNK": "64"}]
+# queue entries per chunk fetch of the queue iterations
+QCHUNKS = [{"MFX_QCHUNK": "256"}, {"MFX_QCHUNK": "64"}]
 
 
 def _ctx(a, env, **kw):
@@ -51,7 +49,7 @@ def test_queue_modes_match_oracle(gpu, oracle, name, w, h, spp, depth):
     # Sample(n) keeps the sample stream running: the second call renders samples n .. 2n - 1
     refs = [o.sample(spp, SEED, sample_base=k * spp, with_stats=True) for k in range(2)]
     for mode in MODES:
-        for env in TAILS:
+        for env in QCHUNKS:
             with _ctx(a, dict(env, MFX_QUEUE_FROM=mode)) as ctx:
                 for k, (ref, st) in enumerate(refs):  # the second call: the automatic mode has the first one's counts
                     img = ctx.sample(spp)
@@ -81,20 +79,21 @@ def test_auto_queue_start_settles_after_first_trace(gpu, oracle):
     """The automatic queue start (-2) is cross-call state: the first trace runs with the initial
     start (queues from the second vertex) and the library reads that trace's per-iteration counters
     once, so the next trace takes the scene's own choice without the caller polling any counter.
-    The Cornell box keeps most paths live, so its choice is in place: the first trace runs k_tail,
-    the second does not, and both equal the oracle at their sample bases."""
+    The Cornell box keeps most paths live, so its choice is in place: the first trace runs queues,
+    the second does not (the choice is not visible through the ABI), and both equal the oracle at
+    their sample bases with its ray counts."""
     a = scene("cube_cornell", 40, 32)
     o = oracle.OracleScene(a)
-    with _ctx(a, {"MFX_QUEUE_FROM": "-2", "MFX_TAIL": "1"}) as ctx:
-        tails = []
+    with _ctx(a, {"MFX_QUEUE_FROM": "-2"}) as ctx:
         for k in range(2):
             ctx.accum_clear()
             ctx.trace_accumulate(4, 4 * k)  # no counter poll in between
             ctx.sync()
-            tails.append(ctx.trace_timing()["tail_launches"])
             acc = ctx.accum_read_mean(4.0)
-            assert np.array_equal(acc, o.sample(4, SEED, sample_base=4 * k)), k
-    assert tails == [1, 0], tails
+            ref, st = o.sample(4, SEED, sample_base=4 * k, with_stats=True)
+            assert np.array_equal(acc, ref), k
+        c = ctx.ray_counts()
+    assert (c[0], c[1], c[2]) == (st[0], st[1], st[2])
 
 
 def test_queue_modes_over_generations(gpu, oracle):
