@@ -509,10 +509,8 @@ __device__ __forceinline__ bool tri_box_pass(DV a, DV e1, DV e2, DV o, DV d, dou
 // when B improved.
 // base: the slot index the code counts from (an instance's run of world slots; 0 otherwise).
 // UNI: the leaf is wave-uniform (packet traversal): its slots are read through scalar loads.
-#ifndef MFX_SLOT_LDS
-#define MFX_SLOT_LDS 1  // small scenes' slots read from the kernels' LDS copy (SceneView::slots_lds)
-#endif
-template <bool SHADOW, bool STATS, bool UNI = false>
+// SLDS: the slots are read from the kernel's LDS copy (S.slots_lds holds every slot of a small scene).
+template <bool SHADOW, bool STATS, bool UNI = false, bool SLDS = false>
 __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV d, double tMin, double tMax,
                                          Best& B, Stats& st, int base = 0) {
     constexpr bool shd = SHADOW;
@@ -521,7 +519,7 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
     if (STATS) st.clusters++;
     bool improved = false;
     constexpr int PRE = SHADOW ? MFX_SHADOW_PRELOAD : MFX_LEAF_PRELOAD;
-    const bool in_lds = MFX_SLOT_LDS && !UNI && S.nslot_lds > 0;  // the LDS copy holds every slot (wave-uniform)
+    constexpr bool in_lds = SLDS && !UNI;
     for (int k = 0; k < n; ++k) {
 #if MFX_LEAF_PRELOAD
         SlotR r = UNI ? load_slot_u(sl + k) : (in_lds ? load_slot_lds(S.slots_lds, s0 + k) : load_slot(sl + k));

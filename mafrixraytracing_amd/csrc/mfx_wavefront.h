@@ -43,6 +43,10 @@
 // A NEED_EXT state word written in place carries the path's lit mask << WF_SHADE_SHIFT too; k_extend's
 // pending entries hold a slot index in 28 bits (pools of at most 2^28 slots), the mask above it
 #define WF_ENTRY_SLOT 0x0fffffff
+// scene kinds of the trace kernels' instances (k_extend / k_shadow SK)
+#define WF_SK_FLAT 0
+#define WF_SK_INST 1  // two-level (instanced) scene
+#define WF_SK_SLDS 2  // small flat scene: every slot's test prefix in the kernel's LDS
 #define WF_SHADE_SHIFT 4  // WF_HIT state word: shade[] index << WF_SHADE_SHIFT | flags
 // depth word of a slot: remaining depth (low 8 bits) | lit-vertex mask << 8 (bit v: vertex v's
 // shadow ray reached the light); so at most WF_MAX_VERTS vertices (max_depth < WF_MAX_VERTS)

@@ -117,7 +117,7 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
 }
 
 #ifndef WF_SPREAD
-#define WF_SPREAD 1  // a wave whose shard closed picks the next open shard from a per-wave pseudo-random start
+#define WF_SPREAD 0  // 1: a wave whose shard closed picks the next open shard from a per-wave pseudo-random start (r04c: C2 -0.4 %, C4 -1.9 %)
 #endif
 #ifndef WF_CLOSED_MASK
 #define WF_CLOSED_MASK 1  // closed shards are found from one mask word, not from a load of all 64 heads
@@ -246,7 +246,8 @@ __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, cons
 // exact FP64. Returns true when the ray is finished (closest: stack empty; shadow: occluded or
 // stack empty).
 // INST: a two-level scene; a lane enters and leaves instances inside the node loop (inst_frame).
-template <bool SHADOW, bool STATS, bool INST, typename ST>
+// SLDS: the scene's slots are read from the kernel's LDS copy (a small flat scene, SceneView::slots_lds).
+template <bool SHADOW, bool STATS, bool INST, bool SLDS, typename ST>
 __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST& stack, TopNodes tn, Stats& st,
                                           DiagAcc& dg, bool diag) {
     // the frame of the entry popped at the end of the last round (an instance left or entered)
@@ -275,7 +276,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
     if (STATS && !SHADOW && T.B.found) st.after_leaves++;
 #endif
     const int base = (INST && T.inst >= 0) ? load_inst(S, T.inst).slot_base : 0;
-    const bool better = leaf_hit<SHADOW, STATS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
+    const bool better = leaf_hit<SHADOW, STATS, false, SLDS>(S, ~T.node, T.o, T.d, 1e-6, T.tmax64, T.B, st, base);
     if (better) {
         if (SHADOW) {
             T.B.found = true;
@@ -461,23 +462,28 @@ __device__ __forceinline__ VertexSample sample_vertex(const WfParams& P, bool ow
 // ------------------------------------------------------------------------------------------------
 // Q: the instance for the iterations on ray queues (MFX_RAY_QUEUE; P.qcount); the in-place one
 // has none of their code
-template <bool STATS, bool SPILL, bool INST, bool Q>
+// SK: the scene kind (WF_SK_FLAT, WF_SK_INST: two-level, WF_SK_SLDS: a small flat scene whose whole
+// slot array sits in LDS); only a small scene's instances carry the LDS slot reads (r04c: the runtime
+// branch in every leaf test cost C2 1.8 % and C4 4 %)
+template <bool STATS, bool SPILL, int SK, bool Q>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
+    constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
-    if (P.nslot_ext) load_slots_lds(slot_lds, P.slots, P.nslot_ext);
-    int* lds = (int*)(slot_lds + 5 * P.nslot_ext);
+    const int nslot = SLDS ? P.nslot_ext : 0;
+    if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
+    int* lds = (int*)(slot_lds + 5 * nslot);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_ext * 64 + lane, P, P.stack_lds_ext);
     int* pend = lds + 4 * P.stack_lds_ext * 64 + wave * WF_EXT_PEND;
     uint32_t* red = (uint32_t*)(lds + 4 * P.stack_lds_ext * 64 + 4 * WF_EXT_PEND);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_ext};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, nslot};
     const int shard_size = P.pool / WF_SHARDS;
 
     Scanner sc{};
@@ -593,7 +599,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fetch, DG);
         if (DG) dg.outer++;
         bool fin = false;
-        if (active) fin = trav_step<false, STATS, INST>(T, S, stack, tn, st, dg, DG);
+        if (active) fin = trav_step<false, STATS, INST, SLDS>(T, S, stack, tn, st, dg, DG);
         DIAG_MARK(dg, leaf, DG);
         if (fin) finish_ray();
         DIAG_MARK(dg, fin, DG);
@@ -699,16 +705,18 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
 // Q: the instance that reads a ray queue (P.qslot) or writes the next one (P.ncount), MFX_RAY_QUEUE
-template <bool STATS, bool SPILL, int WAVES, bool INST, bool Q>
+template <bool STATS, bool SPILL, int WAVES, int SK, bool Q>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
+    constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
-    if (P.nslot_shd) load_slots_lds(slot_lds, P.slots, P.nslot_shd);
-    int* lds = (int*)(slot_lds + 5 * P.nslot_shd);
+    const int nslot = SLDS ? P.nslot_shd : 0;
+    if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
+    int* lds = (int*)(slot_lds + 5 * nslot);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -716,7 +724,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
     uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, P.nslot_shd};
+    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, nslot};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -906,7 +914,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             fin = true;
         }
 #else
-        if (active) fin = trav_step<true, STATS, INST>(T, S, stack, tn, st, dg, DG);
+        if (active) fin = trav_step<true, STATS, INST, SLDS>(T, S, stack, tn, st, dg, DG);
 #endif
         DIAG_MARK(dg, leaf, DG);
         if (fin) {
@@ -1148,45 +1156,65 @@ static int wf_lds_blocks(size_t bytes) {
     return (int)(per_cu / ((bytes + g - 1) / g * g));
 }
 
+// the scene kind a kernel instance is built for (k_extend / k_shadow SK)
+static int scene_kind(bool inst, int nslot) { return inst ? WF_SK_INST : (nslot > 0 ? WF_SK_SLDS : WF_SK_FLAT); }
+
+template <int SK>
+static const void* occ_kernel(bool shadow, bool spill) {
+    if (shadow)
+        return spill ? (const void*)k_shadow<false, true, 4, SK, false> : (const void*)k_shadow<false, false, 4, SK, false>;
+    return spill ? (const void*)k_extend<false, true, SK, false> : (const void*)k_extend<false, false, SK, false>;
+}
+
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu,
                                    int nslot) {
-    const bool inst = ninst > 0;
     const size_t lds = wf_lds_bytes(stack_lds, shadow, ntop, std::min(ninst, WF_INST_LDS), nslot);
-    const void* k;
-    if (shadow)
-        k = inst ? (spill ? (const void*)k_shadow<false, true, 4, true, false> : (const void*)k_shadow<false, false, 4, true, false>)
-                 : (spill ? (const void*)k_shadow<false, true, 4, false, false> : (const void*)k_shadow<false, false, 4, false, false>);
-    else
-        k = inst ? (spill ? (const void*)k_extend<false, true, true, false> : (const void*)k_extend<false, false, true, false>)
-                 : (spill ? (const void*)k_extend<false, true, false, false> : (const void*)k_extend<false, false, false, false>);
+    const int sk = scene_kind(ninst > 0, nslot);
+    const void* k = sk == WF_SK_INST ? occ_kernel<WF_SK_INST>(shadow, spill)
+                                     : (sk == WF_SK_SLDS ? occ_kernel<WF_SK_SLDS>(shadow, spill) : occ_kernel<WF_SK_FLAT>(shadow, spill));
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, k, 256, lds);
     *blocks_per_cu = std::min(*blocks_per_cu, wf_lds_blocks(lds));
     return e;
 }
 
-template <bool SPILL, bool INST, bool Q>
+template <bool SPILL, int SK, bool Q>
 static void launch_extend_q(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (stats)
-        hipLaunchKernelGGL((k_extend<true, SPILL, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_extend<true, SPILL, SK, Q>), dim3(grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_extend<false, SPILL, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_extend<false, SPILL, SK, Q>), dim3(grid), dim3(256), lds, st, P);
 }
-template <bool SPILL, bool INST>
+template <bool SPILL, int SK>
 static void launch_extend(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
-    if (P.qcount) launch_extend_q<SPILL, INST, true>(P, grid, stats, st, lds);
-    else launch_extend_q<SPILL, INST, false>(P, grid, stats, st, lds);
+    if (P.qcount) launch_extend_q<SPILL, SK, true>(P, grid, stats, st, lds);
+    else launch_extend_q<SPILL, SK, false>(P, grid, stats, st, lds);
 }
-template <bool SPILL, int WAVES, bool INST, bool Q>
+template <bool SPILL, int WAVES, int SK, bool Q>
 static void launch_shadow_q(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (stats)
-        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_shadow<true, SPILL, WAVES, SK, Q>), dim3(grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, INST, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, SK, Q>), dim3(grid), dim3(256), lds, st, P);
 }
-template <bool SPILL, int WAVES, bool INST>
+template <bool SPILL, int WAVES, int SK>
 static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
-    if (P.qslot || P.ncount) launch_shadow_q<SPILL, WAVES, INST, true>(P, grid, stats, st, lds);
-    else launch_shadow_q<SPILL, WAVES, INST, false>(P, grid, stats, st, lds);
+    if (P.qslot || P.ncount) launch_shadow_q<SPILL, WAVES, SK, true>(P, grid, stats, st, lds);
+    else launch_shadow_q<SPILL, WAVES, SK, false>(P, grid, stats, st, lds);
+}
+template <int SK>
+static void launch_shadow_sk(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
+    // k_shadow is compiled for 3 waves per SIMD (up to 168 VGPRs) when its LDS allows no more blocks anyway
+    const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
+    if (spill && w3) launch_shadow<true, 3, SK>(P, grid, stats, st, lds);
+    else if (spill) launch_shadow<true, 4, SK>(P, grid, stats, st, lds);
+    else if (w3) launch_shadow<false, 3, SK>(P, grid, stats, st, lds);
+    else launch_shadow<false, 4, SK>(P, grid, stats, st, lds);
+}
+template <int SK>
+static void launch_extend_sk(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
+    // each kernel keeps its own share of the traversal stack in LDS (the rest spills)
+    if (P.stack_lds_ext < P.stack_size) launch_extend<true, SK>(P, grid, stats, st, lds);
+    else launch_extend<false, SK>(P, grid, stats, st, lds);
 }
 
 static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64; }
@@ -1197,28 +1225,28 @@ hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
     return e;
 }
 
-template <bool INST>
 static hipError_t launch_iteration(const WfParams& P, int ext_grid, int shd_grid, bool stats, hipStream_t st,
                                    hipEvent_t* ev, size_t lds_e, size_t lds_s) {
-    // each kernel keeps its own share of the traversal stack in LDS (the rest spills); k_shadow is
-    // compiled for 3 waves per SIMD (up to 168 VGPRs) when its LDS allows no more blocks anyway
-    if (!INST && P.start && P.cam_grid > 0) {  // camera rays as packets
+    const bool inst = P.inst != nullptr;
+    if (!inst && P.start && P.cam_grid > 0) {  // camera rays as packets
         if (stats) hipLaunchKernelGGL(k_camera<true>, dim3(P.cam_grid), dim3(256), cam_lds_bytes(P.stack_size), st, P);
         else hipLaunchKernelGGL(k_camera<false>, dim3(P.cam_grid), dim3(256), cam_lds_bytes(P.stack_size), st, P);
-    } else if (P.stack_lds_ext < P.stack_size) {
-        launch_extend<true, INST>(P, ext_grid, stats, st, lds_e);
     } else {
-        launch_extend<false, INST>(P, ext_grid, stats, st, lds_e);
+        switch (scene_kind(inst, P.nslot_ext)) {
+            case WF_SK_INST: launch_extend_sk<WF_SK_INST>(P, ext_grid, stats, st, lds_e); break;
+            case WF_SK_SLDS: launch_extend_sk<WF_SK_SLDS>(P, ext_grid, stats, st, lds_e); break;
+            default: launch_extend_sk<WF_SK_FLAT>(P, ext_grid, stats, st, lds_e);
+        }
     }
     if (ev) {  // between the two kernels (per-stage timing); null: not recorded
         const hipError_t e = hipEventRecord(ev[0], st);
         if (e != hipSuccess) return e;
     }
-    const bool spill = P.stack_lds_shd < P.stack_size, w3 = P.shadow_waves == 3;
-    if (spill && w3) launch_shadow<true, 3, INST>(P, shd_grid, stats, st, lds_s);
-    else if (spill) launch_shadow<true, 4, INST>(P, shd_grid, stats, st, lds_s);
-    else if (w3) launch_shadow<false, 3, INST>(P, shd_grid, stats, st, lds_s);
-    else launch_shadow<false, 4, INST>(P, shd_grid, stats, st, lds_s);
+    switch (scene_kind(inst, P.nslot_shd)) {
+        case WF_SK_INST: launch_shadow_sk<WF_SK_INST>(P, shd_grid, stats, st, lds_s); break;
+        case WF_SK_SLDS: launch_shadow_sk<WF_SK_SLDS>(P, shd_grid, stats, st, lds_s); break;
+        default: launch_shadow_sk<WF_SK_FLAT>(P, shd_grid, stats, st, lds_s);
+    }
     return hipSuccess;
 }
 
@@ -1236,8 +1264,7 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
     }
     hipError_t e = hipMemsetAsync(z, 0, nz * sizeof(unsigned long long), st);
     if (e != hipSuccess) return e;
-    e = P.inst ? launch_iteration<true>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s)
-               : launch_iteration<false>(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s);
+    e = launch_iteration(P, ext_grid, shd_grid, stats, st, ev, lds_e, lds_s);
     if (e != hipSuccess) return e;
     return hipGetLastError();
 }
