@@ -491,8 +491,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
-    int s = 0;
-    bool fresh = false;  // the lane's ray is its path's camera ray
+    int se = 0;  // the lane's listed entry: slot (WF_ENTRY_SLOT), lit mask << 28, camera-ray flag (sign)
     Trav T{};
     uint32_t c_primary = 0, c_ext = 0;
     Stats st{0, 0, 0};
@@ -501,15 +500,15 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     if (DG) dg.last = stamp();
     // An in-place extension ray's entry carries the path's lit-vertex mask (k_shadow wrote it into
     // the NEED_EXT state word) in bits 28..30 when it fits (iterations 1..3: vertices 0..2), so a
-    // miss writes its finished state word without loading the depth word (a dependent round trip
-    // in the finishing round: bounce-1 k_extend 8.0 -> 9.1 ms on C2 when it did, r04a)
+    // miss writes its finished state word, mask included, without loading the depth word (r04b:
+    // +0.5 % over that load; k_resolve reading the depth words of misses instead, r04g: -0.3 %).
+    // The lane keeps the entry itself: no register for the mask or the camera-ray flag.
     const bool lit_in_entry = !Q && P.iter <= 3;
-    int litm = 0;  // the lane's path's lit mask (lit_in_entry)
     // the lane takes listed entry e: its camera ray (FREE slot) or the slot's extension ray
     auto start_ray = [&](int e) {
-        s = e & WF_ENTRY_SLOT;
-        litm = (e >> 28) & 7;
-        fresh = e < 0;
+        se = e;
+        const int s = e & WF_ENTRY_SLOT;
+        const bool fresh = e < 0;
         DV o, d;
         if (fresh) {
             // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
@@ -539,13 +538,15 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     };
     // the lane's ray is finished: its closest hit (hit point, shade index) or its miss
     auto finish_ray = [&]() {
+        const int s = se & WF_ENTRY_SLOT;
+        const bool fresh = se < 0;
         const int fl = fresh ? WF_FRESH : 0;
         if (T.B.found) {
             const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
             P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
             P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
         } else {  // a later miss finishes the path: its lit mask goes into the state word
-            const int lm = fresh || Q ? 0 : (lit_in_entry ? litm : (P.depth[s] >> WF_LIT_SHIFT) & 0xffff);
+            const int lm = fresh || Q ? 0 : (lit_in_entry ? (se >> 28) & 7 : (P.depth[s] >> WF_LIT_SHIFT) & 0xffff);
             P.state[s] = WF_MISS | (lm << WF_SHADE_SHIFT) | fl;
         }
         active = false;
@@ -1106,9 +1107,10 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
         }
         int mask[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
+        for (int u = 0; u < U; ++u) {
             mask[u] = ((sw[u] & WF_STATE_MASK) == WF_DONE || (sw[u] & WF_STATE_MASK) == WF_MISS)
                           ? ((unsigned)sw[u] >> WF_SHADE_SHIFT) & 0xffff : 0;
+        }
         PathRec R[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) load_path(P, jv[u], mask[u], R[u]);
