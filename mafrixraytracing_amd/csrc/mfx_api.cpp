@@ -139,7 +139,7 @@ struct mfx_ctx {
     int wf_queue_from = MFX_RAY_QUEUE ? -2 : -1;  // -2: automatic (wf_queue_auto)
     int wf_queue_auto = 1;  // from the last trace's live paths per iteration (note_live); 1 before any
     bool wf_auto_read = false;  // the first wavefront trace's counters have been read for wf_queue_auto
-    int32_t wf_qchunk = 256;  // entries per chunk fetch on a ray queue (MFX_QCHUNK)
+    int32_t wf_qchunk = 128;  // entries per chunk fetch on a ray queue (MFX_QCHUNK; r04j: 128 against 256, C2 8 spp +2 %)
     // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
     // slots, 15 GB) runs the frame as one generation: no kernel ends with a partly filled pool
     // (+11 % on C2 over 32 M slots). Capped at 2^28 slots (31 GB of the 288 GB) and at a quarter
@@ -154,8 +154,7 @@ struct mfx_ctx {
     bool cam_last = false;  // the last wavefront trace ran its camera rays as packets (k_camera)
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
-    int wf_chunk = 1024;  // slots per chunk fetch (a multiple of 64)
-    bool wf_chunk_env = false;  // MFX_CHUNK given: that size for every frame
+    int wf_chunk = 256;  // slots per chunk fetch (a multiple of 64; r04j: 256 against 1024, C2 64 spp +1 %, 8 spp +6 %)
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
@@ -318,7 +317,6 @@ static int ctx_setup(mfx_ctx* c) {
     if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
     if (const char* ck = getenv("MFX_CHUNK")) {
         c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
-        c->wf_chunk_env = true;
     }
     CK(hipMemset(c->d_accum, 0, 3 * plane));
     CK(hipMemset(c->d_film, 0, 3 * plane));
@@ -769,9 +767,11 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.shadow_waves = c->wf_shadow_waves;
     P.ninst_lds = std::min<int>((int)c->host.inst.size(), WF_INST_LDS);
     P.spill = c->d_spill;
-    // slots per chunk fetch: 1024, or 512 for a frame of at most 2^25 paths (16 spp at 1080p), where
-    // the last big chunks of a launch are a larger share of it (r03e/r03f: 8 spp +6 %, 64 spp -1 %)
-    P.chunk = c->wf_chunk_env ? c->wf_chunk : (total <= ((int64_t)1 << 25) ? 512 : c->wf_chunk);
+    // slots per chunk fetch: 256 at every frame size. Round 3 used 1024 (512 for frames of at most
+    // 2^25 paths); with the shard counters on lines of their own and the closed-shard mask the chunk
+    // fetches no longer convoy, so small chunks cut the launches' tails (r04j: C2 fixed cost per
+    // frame 1.67 -> 1.24 ms, 8 spp +8 %, 64 spp +1 %)
+    P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const int32_t chunk0 = P.chunk;
     P.planes = planes;
@@ -816,7 +816,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
             P.iter = d;
             wf_queue_views(c, P, d);
             // a queue's entries are all live rays: smaller chunks keep the launch's tail short
-            P.chunk = P.qcount && !c->wf_chunk_env ? c->wf_qchunk : chunk0;
+            P.chunk = P.qcount ? c->wf_qchunk : chunk0;
             if (!own_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;

@@ -16,8 +16,8 @@ from conftest import SEED, scene
 pytestmark = pytest.mark.gpu
 
 MODES = ["-1", "0", "1", "2", "-2"]
-# queue entries per chunk fetch of the queue iterations
-QCHUNKS = [{"MFX_QCHUNK": "256"}, {"MFX_QCHUNK": "64"}]
+# queue entries / pool slots per chunk fetch
+QCHUNKS = [{}, {"MFX_QCHUNK": "64", "MFX_CHUNK": "1024"}]  # the default (128 / 256), and small queue / large pool chunks
 
 
 def _ctx(a, env, **kw):
