@@ -116,16 +116,12 @@ __device__ __forceinline__ int next_open(uint64_t open, int home) {
     return (home + __builtin_ctzll(r)) & (WF_SHARDS - 1);
 }
 
-#ifndef WF_SPREAD
-#define WF_SPREAD 0  // 1: a wave whose shard closed picks the next open shard from a per-wave pseudo-random start (r04c: C2 -0.4 %, C4 -1.9 %)
-#endif
 #ifndef WF_CLOSED_MASK
 #define WF_CLOSED_MASK 1  // closed shards are found from one mask word, not from a load of all 64 heads
 #endif
 struct Scanner {
     int win_next, win_end, shard;
     bool exhausted;
-    uint32_t spread;  // WF_SPREAD: the wave's pseudo-random walk over the shards
     uint64_t closed_seen;  // WF_CLOSED_MASK: shards this wave found closed itself
     // state words of the next WF_LOOKAHEAD windows of the chunk, loaded in one round of
     // independent loads (b[0] = the current window; -1 past the chunk's end): windows without
@@ -170,15 +166,9 @@ struct Scanner {
                 exhausted = true;
                 return false;
             }
-            // The waves of one home shard would all move to the same next open shard, and near a
-            // launch's end every wave to the last few, one memory-side atomic after another: each
-            // wave instead starts its search at its own pseudo-random shard
-            if (WF_SPREAD) {
-                spread = spread * 0x9e3779b1u + 0x7f4a7c15u;
-                shard = next_open(open, (int)(spread >> 26));
-            } else {
-                shard = next_open(open, shard);
-            }
+            // the next open shard after this one (a per-wave pseudo-random start instead, WF_SPREAD,
+            // measured C2 -0.4 %, C4 -1.9 %, r04c)
+            shard = next_open(open, shard);
         }
     }
     __device__ __forceinline__ void fill(const int32_t* __restrict__ state) {
@@ -488,7 +478,6 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
     int se = 0;  // the lane's listed entry: slot (WF_ENTRY_SLOT), lit mask << 28, camera-ray flag (sign)
@@ -651,7 +640,6 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
     uint32_t pk_nodes = 0, pk_slots = 0;  // STATS: the wave's own node and slot fetches (every lane counts them)
@@ -731,7 +719,6 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
-    sc.spread = (blockIdx.x * 4u + (threadIdx.x >> 6)) * 0x85ebca6bu + 0x2545f491u;
     int nshade = 0;      // wave-uniform: hits listed for shading
     int pend_lo = 0, pend_hi = 0;
     bool active = false;
