@@ -189,15 +189,15 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * rgba may be NULL (accumulate only).
  * Render-ahead (mfx_options.render_ahead = K > 1, one device, part_count 1): one-sample calls are
  * served from batches of K samples. A call whose global sample is not held traces the next K
- * samples in one batched pass (each sample's 1-spp image in its own FP64 plane) and runs the film
- * add and post of all K calls ahead, in call order; each call of the batch then only copies its
- * RGBA8 frame, and while a batch is served the next one is traced in the background (two buffers
- * of K x 28 B per pixel). Every frame's bytes and the film equal the one-sample path's (a sample's
- * image depends only on the seed and its global index); mfx_reset, an spp != 1 call or mfx_sample
- * in between make the held frames recompute from the film as it then is. mfx_stats: the first call
+ * samples in one batched pass that runs the film add and post of all K calls ahead, in call
+ * order; each call of the batch then only copies its RGBA8 frame, and while a batch is served the
+ * next one is traced in the background (two buffers of K x 4 B + 48 B per pixel). Every frame's
+ * bytes and the film equal the one-sample path's (a sample's image depends only on the seed and
+ * its global index); after mfx_reset, an spp != 1 call or mfx_sample the next one-sample call
+ * traces a batch again from the film as it then is. mfx_stats: the first call
  * served from a batch reports the K samples' rays and device time, the others 0 rays in 0 s. The
  * two buffers take at most MFX_RENDER_AHEAD_MAX_BYTES (environment; default 2 GiB) and a quarter of
- * the free HBM: K is cut to fit two buffers while at least 8 samples fit in each (1080p: 2 x 16),
+ * the free HBM: K is cut to fit two buffers while at least 8 samples fit in each (1080p: 2 x 64 in 1.26 GB),
  * else one buffer of as many samples as fit (no background batch); when not even two samples fit,
  * the context frees the buffers and renders one sample per call from then on. A background batch
  * is traced once a batch starts being served, so an application that stops early has traced at

@@ -80,22 +80,27 @@ hipError_t upload(T** dptr, const std::vector<T>& v) {
 }  // namespace
 
 
-// One render-ahead buffer: the 1-spp images (FP64 planes) of global samples [base, base + n), the
-// RGBA8 frame each of those one-sample render calls returns, and the film the frames start from.
+// One render-ahead buffer: the RGBA8 frames that the one-sample render calls of global samples
+// [base, base + n) return, the film before the first of them and the film after the last.
 struct AheadBuf {
-    double* planes = nullptr;           // [cap][3][npix]
     uint8_t* frames = nullptr;          // [cap][npix][4] (y-major RGBA8)
-    double* film_in = nullptr;          // [3][npix] the film before plane k0 (as the frames assume)
-    double* film_out = nullptr;         // [3][npix] the film after plane n - 1
+    double* film_in = nullptr;          // [3][npix] the film before sample base (as the frames assume)
+    double* film_out = nullptr;         // [3][npix] the film after sample base + n - 1
     unsigned long long* counters = nullptr;  // the batch's ray counters [WF_SHARDS][WF_NCTR]
     hipEvent_t t0 = nullptr, t1 = nullptr;   // around the batch's trace
     hipEvent_t ready = nullptr;         // frames computed
     int64_t base = 0, n = 0;            // samples held (n == 0: empty)
-    int64_t k0 = 0;                     // frames computed from index k0 on
     int64_t expect = 0;                 // the index whose frame a call may take next
     uint64_t epoch = 0;                 // film epoch the frames were computed in
-    double count0 = 0.0;                // Film frameCount before plane k0
+    double count0 = 0.0;                // Film frameCount before sample base
     bool reported = false;              // a call has reported the batch's rays and time
+};
+
+// k_resolve's frames mode for a wavefront trace (WfParams film / frames / count0)
+struct FrameMode {
+    double* film;     // the film state: read before the first sample, written after the last
+    uint8_t* frames;  // null: the film only
+    double count0;    // frameCount before the first sample
 };
 
 constexpr int kStageChunks = 4;  // host_readback's pipelined pieces
@@ -175,7 +180,9 @@ struct mfx_ctx {
     int ab_cur = -1;                 // the buffer the last render call was served from (-1: none)
     int64_t ab_last_k = -1;          // and its index in that buffer
     uint64_t film_epoch = 1;         // bumped when the film leaves the held frames' sequence
-    bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its planes)
+    bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its samples up to ab_last_k)
+    unsigned long long* d_counters_aux = nullptr;  // ray counters of a film-only re-trace (not reported)
+    hipEvent_t aux_ev0 = nullptr, aux_ev1 = nullptr;
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
     unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
     uint8_t* h_stage = nullptr;         // page-locked staging of large readbacks (host_readback)
@@ -204,12 +211,17 @@ static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
 
 static void ahead_free(mfx_ctx* c) {
     for (AheadBuf& B : c->ab) {
-        for (void* b : {(void*)B.planes, (void*)B.frames, (void*)B.film_in, (void*)B.film_out, (void*)B.counters})
+        for (void* b : {(void*)B.frames, (void*)B.film_in, (void*)B.film_out, (void*)B.counters})
             if (b) (void)hipFree(b);
         for (hipEvent_t e : {B.t0, B.t1, B.ready})
             if (e) (void)hipEventDestroy(e);
         B = AheadBuf{};
     }
+    if (c->d_counters_aux) (void)hipFree(c->d_counters_aux);
+    for (hipEvent_t e : {c->aux_ev0, c->aux_ev1})
+        if (e) (void)hipEventDestroy(e);
+    c->d_counters_aux = nullptr;
+    c->aux_ev0 = c->aux_ev1 = nullptr;
     c->ab_nbuf = 0;
     c->ab_cap = 0;
     c->ab_cur = -1;
@@ -731,10 +743,11 @@ static void note_live(mfx_ctx* c, const unsigned long long* h);
 // max_depth extension rays of PathIntegrator.TraceRay (Integrators.fs:107-137), one bounce of
 // every live path per iteration — then k_resolve adds its finished paths to their pixels. Every
 // launch count is known up front, so the whole call is enqueued without a host round trip.
-// planes != null (render-ahead): each sample's 1-spp image to its own plane, the ray counters to
-// `counters` and the trace bracketed by the events e0 / e1 instead of the context's (no per-iteration
-// events), so a batch traced in the background leaves the last call's timing records alone.
-static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes = nullptr,
+// fm != null (render-ahead): the samples are one-sample render calls added to fm->film in order
+// (k_resolve's frames mode), the ray counters go to `counters` and the trace is bracketed by the
+// events e0 / e1 instead of the context's (no per-iteration events), so a batch traced in the
+// background leaves the last call's timing records alone.
+static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode* fm = nullptr,
                     unsigned long long* counters = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     const int W = c->host.width, H = c->host.height;
     const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
@@ -774,7 +787,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, double* planes 
     P.chunk = c->wf_chunk;
     P.tile_padding = (W % 8 != 0 || H % 8 != 0) ? 1 : 0;
     const int32_t chunk0 = P.chunk;
-    P.planes = planes;
+    P.film = fm ? fm->film : nullptr;
+    P.frames = fm ? fm->frames : nullptr;
+    P.count0 = fm ? fm->count0 : 0.0;
     const bool stats = (c->flags & MFX_F_COUNT_STATS) != 0;
     P.cam_grid = c->host.inst.empty() ? c->wf_cam_grid : 0;
     if (own_events) c->cam_last = P.cam_grid > 0;
@@ -1191,26 +1206,30 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
 // (Scene.fs:331-333) asks for one sample per call: alone, a 1080p sample is ~21 rays per lane of a
 // persistent grid plus the film/post launch and the readback per call. A sample's 1-spp image
 // depends only on (seed, global sample index), so a call whose sample is not held traces the next K
-// samples in one batched wavefront pass (k_resolve writes each sample's image to its own FP64
-// plane) and film_frames_kernel then runs, in call order, the film add and post of all K calls
-// (the FP64 operations film_post_kernel runs per call, in the same order): each call of the batch
-// only copies its RGBA8 frame to the host. While a batch is served, the next one is traced and
-// post-processed in the background into the second buffer (the frame copies run on their own
-// stream, so they overlap that trace). Every frame and the film are the bytes the one-sample path
-// gives (tests/test_gpu_render_ahead.py).
+// samples in one batched wavefront pass whose k_resolve runs, per pixel and in call order, each
+// call's film add and post (the FP64 operations film_post_kernel runs per call, in the same order:
+// k_resolve's frames mode) into K RGBA8 frames and the film after the last call: each call of the
+// batch only copies its frame to the host. While a batch is served, the next one is traced in the
+// background into the second buffer (the frame copies run on their own stream, so they overlap that
+// trace). Every frame and the film are the bytes the one-sample path gives
+// (tests/test_gpu_render_ahead.py). A buffer holds K frames (4 B per pixel each) and two films: no
+// per-sample FP64 image is kept (round 3 kept one, 24 B per pixel per sample).
 // The frames assume the calls follow each other with nothing else touching the film. A reset, a
 // render call of spp != 1 or an mfx_sample call (which moves the sample sequence) bumps film_epoch
-// after bringing d_film up to date; a buffer whose frames belong to an older epoch recomputes them
-// from the index it is at, from d_film.
+// after bringing d_film up to date; a held batch whose frames belong to an older epoch is traced
+// again from the sample the next call needs. d_film is brought up to date from the film before the
+// batch by tracing its served samples again, film only (ahead_materialize) — after a batch's last
+// call it is a copy of the film after it.
 static int ahead_alloc(mfx_ctx* c) {
     const size_t plane = 3 * sizeof(double) * (size_t)c->npix, frame = 4 * (size_t)c->npix;
-    const size_t per_sample = plane + frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
+    const size_t per_sample = frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
     size_t fr = 0, tot = 0;
     HIPCHECK(hipMemGetInfo(&fr, &tot));
     // Both buffers within MFX_RENDER_AHEAD_MAX_BYTES (default 2 GiB) and a quarter of the free HBM:
     // a context never takes more than that for render-ahead, whatever K it asked for. K shrinks to
     // fit two buffers (the background batch) while at least 8 samples fit in each; below that one
-    // buffer of as many samples as fit. At 1080p (58 MB per sample) the default cap gives 2 x 16.
+    // buffer of as many samples as fit. At 1080p (8.3 MB per sample, 100 MB of films per buffer)
+    // K = 64 takes 1.26 GB for both.
     size_t budget = std::min<size_t>(fr / 4, (size_t)2 << 30);
     if (const char* e = getenv("MFX_RENDER_AHEAD_MAX_BYTES")) budget = std::min(budget, (size_t)atoll(e));
     int nbuf = 2;
@@ -1223,8 +1242,7 @@ static int ahead_alloc(mfx_ctx* c) {
     if (k < 2) return MFX_E_NOMEM;
     for (int b = 0; b < nbuf; ++b) {
         AheadBuf& B = c->ab[b];
-        hipError_t e = hipMalloc((void**)&B.planes, (size_t)k * plane);
-        if (e == hipSuccess) e = hipMalloc((void**)&B.frames, (size_t)k * frame);
+        hipError_t e = hipMalloc((void**)&B.frames, (size_t)k * frame);
         if (e == hipSuccess) e = hipMalloc((void**)&B.film_in, plane);
         if (e == hipSuccess) e = hipMalloc((void**)&B.film_out, plane);
         if (e == hipSuccess) e = hipMalloc((void**)&B.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
@@ -1237,18 +1255,35 @@ static int ahead_alloc(mfx_ctx* c) {
             return e == hipErrorOutOfMemory ? MFX_E_NOMEM : fail(MFX_E_DEVICE, std::string("render-ahead: ") + hipGetErrorString(e));
         }
     }
+    hipError_t e = hipMalloc((void**)&c->d_counters_aux, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
+    if (e == hipSuccess) e = hipEventCreate(&c->aux_ev0);
+    if (e == hipSuccess) e = hipEventCreate(&c->aux_ev1);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        ahead_free(c);
+        return e == hipErrorOutOfMemory ? MFX_E_NOMEM : fail(MFX_E_DEVICE, std::string("render-ahead: ") + hipGetErrorString(e));
+    }
     c->ab_nbuf = nbuf;
     c->ab_cap = (int)k;
     return MFX_OK;
 }
 
-// d_film = the film as of the last render call (film_in of the buffer it was served from plus that
-// buffer's planes up to it, added in call order)
+// d_film = the film as of the last render call: a copy of the film after the buffer's last call, or
+// the film before the buffer with its samples up to that call traced again, film only (the same
+// paths, added in the same order: the same bits). Its rays are not reported (no call asked for them).
 static int ahead_materialize(mfx_ctx* c) {
     if (c->film_in_dfilm) return MFX_OK;
     const AheadBuf& B = c->ab[c->ab_cur];
-    HIPCHECK(mfx_launch_film_frames(B.planes, B.k0, c->ab_last_k + 1, B.film_in, c->d_film, c->host.width,
-                                    c->host.height, 0.0, nullptr, c->stream));
+    const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
+    if (c->ab_last_k + 1 == B.n) {
+        HIPCHECK(hipMemcpyAsync(c->d_film, B.film_out, plane, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+        HIPCHECK(hipMemcpyAsync(c->d_film, B.film_in, plane, hipMemcpyDeviceToDevice, c->stream));
+        HIPCHECK(hipMemsetAsync(c->d_counters_aux, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
+        const FrameMode fm{c->d_film, nullptr, 0.0};
+        const int rc = wf_trace(c, c->ab_last_k + 1, B.base, &fm, c->d_counters_aux, c->aux_ev0, c->aux_ev1);
+        if (rc) return rc;
+    }
     c->film_in_dfilm = true;
     return MFX_OK;
 }
@@ -1263,33 +1298,27 @@ static int ahead_break(mfx_ctx* c) {
     return MFX_OK;
 }
 
-// frames of B from index k on, starting from film `film_src` and frame count `count0`
-static int ahead_frames(mfx_ctx* c, AheadBuf& B, int64_t k, const double* film_src, double count0) {
-    const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
-    if (film_src != B.film_in)
-        HIPCHECK(hipMemcpyAsync(B.film_in, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHECK(mfx_launch_film_frames(B.planes, k, B.n, B.film_in, B.film_out, c->host.width, c->host.height, count0,
-                                    B.frames, c->stream));
-    HIPCHECK(hipEventRecord(B.ready, c->stream));
-    B.k0 = k;
-    B.expect = k;
-    B.epoch = c->film_epoch;
-    B.count0 = count0;
-    return MFX_OK;
-}
-
-// trace samples [base, base + ab_cap) into B, then their frames from film_src / count0 (enqueued only)
+// trace samples [base, base + ab_cap) into B: their frames from film_src / count0 and the film
+// after them (enqueued only)
 static int ahead_launch(mfx_ctx* c, AheadBuf& B, int64_t base, const double* film_src, double count0) {
+    const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
     B.base = base;
     B.n = c->ab_cap;
     B.reported = false;
+    HIPCHECK(hipMemcpyAsync(B.film_in, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(B.film_out, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
     HIPCHECK(hipMemsetAsync(B.counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
-    const int rc = wf_trace(c, B.n, base, B.planes, B.counters, B.t0, B.t1);
+    const FrameMode fm{B.film_out, B.frames, count0};
+    const int rc = wf_trace(c, B.n, base, &fm, B.counters, B.t0, B.t1);
     if (rc) {
         B.n = 0;
         return rc;
     }
-    return ahead_frames(c, B, 0, film_src, count0);
+    HIPCHECK(hipEventRecord(B.ready, c->stream));
+    B.expect = 0;
+    B.epoch = c->film_epoch;
+    B.count0 = count0;
+    return MFX_OK;
 }
 
 // One render call (spp = 1) served from held frames. Returns MFX_E_NOMEM when no buffer fits (the
@@ -1310,8 +1339,8 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
         xi = (c->ab_cur >= 0 && c->ab_nbuf == 2) ? 1 - c->ab_cur : 0;
         rc = ahead_launch(c, c->ab[xi], s, c->d_film, c->frame_count);
     } else if (c->ab[xi].epoch != c->film_epoch || c->ab[xi].expect != s - c->ab[xi].base) {
-        rc = ahead_materialize(c);  // held, but the frames assumed another film: recompute from here
-        if (!rc) rc = ahead_frames(c, c->ab[xi], s - c->ab[xi].base, c->d_film, c->frame_count);
+        rc = ahead_materialize(c);  // held, but the frames assumed another film: a batch from here
+        if (!rc) rc = ahead_launch(c, c->ab[xi], s, c->d_film, c->frame_count);
     }
     if (rc) return rc;
     AheadBuf& X = c->ab[xi];
@@ -1347,11 +1376,10 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     c->next_sample += 1;
     if (c->ab_nbuf == 2) {  // the next batch, in the background, unless the other buffer holds it
         AheadBuf& Y = c->ab[1 - xi];
-        const double count_end = X.count0 + (double)(X.n - X.k0);  // frameCount after X's last call
-        if (!(Y.n > 0 && Y.base == X.base + X.n))
+        const double count_end = X.count0 + (double)X.n;  // frameCount after X's last call
+        // not held, or held but its frames assumed another film: traced (again) from X's film
+        if (!(Y.n > 0 && Y.base == X.base + X.n) || Y.epoch != c->film_epoch || Y.count0 != count_end)
             rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
-        else if (Y.epoch != c->film_epoch || Y.k0 != 0)  // held, but its frames assumed another film
-            rc = ahead_frames(c, Y, 0, X.film_out, count_end);
         // This call is served: a background batch that does not fit is not its failure (a NOMEM
         // here would make the caller render the call a second time). Y stays empty; the call
         // that needs it launches it, and falls back to one sample per call if it still fails.

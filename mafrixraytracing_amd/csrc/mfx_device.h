@@ -54,8 +54,6 @@ hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st);
 hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st);
 hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h, double spp, double frame_count,
                                 int add, uint8_t* rgba, hipStream_t st);
-hipError_t mfx_launch_film_frames(const double* planes, int64_t k0, int64_t k1, const double* film_src,
-                                  double* film_dst, int w, int h, double count0, uint8_t* frames, hipStream_t st);
 hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_count, double* out, hipStream_t st);
 hipError_t mfx_launch_accum_add(double* dst, const double* src, int64_t n, hipStream_t st);
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo,

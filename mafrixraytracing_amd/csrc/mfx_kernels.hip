@@ -303,11 +303,6 @@ __global__ void mean_kernel(const double* __restrict__ accum, int64_t npix, doub
     out[4 * q + 3] = 1.0;
 }
 
-__device__ __forceinline__ double clamp01(double x) { return x < 0. ? 0. : (x > 1. ? 1. : x); }
-__device__ __forceinline__ double aces1(double x) {  // Scene.fs:280-289
-    const double a = 2.51, b = 0.03, c = 2.43, d = 0.59, e = 0.14;
-    return clamp01((x * (a * x + b)) / (x * (c * x + d) + e));
-}
 
 // Film.AddSample (Film.fs:18-23) with frame = accum / spp, then PostProcessAndToScreenBuffer
 // (Scene.fs:315-330) on target = film / frameCount.
@@ -328,43 +323,9 @@ __global__ void film_post_kernel(const double* __restrict__ accum, double* __res
     if (rgba) {
         const int x = (int)(q / h), y = (int)(q % h);
         uint8_t* o = rgba + ((int64_t)y * w + x) * 4;
-        for (int c = 0; c < 3; ++c) o[c] = (uint8_t)(int)(255.99 * sqrt(aces1(tgt[c])));
+        for (int c = 0; c < 3; ++c) o[c] = post_byte(tgt[c]);
         o[3] = 255;
     }
-}
-
-// Render-ahead: the film and frames of the one-sample render calls that take held samples k0..k1-1
-// in order — per call, film_post_kernel's Film.AddSample of plane k (frame = accum / 1 for a 1-spp
-// image) and PostProcessAndToScreenBuffer of film / frameCount, frameCount advanced by 1.0 per call:
-// the same FP64 operations in the same order, so every frame is the bytes that call would have
-// written. frames == null: only the film (the context's film brought up to date). film_dst gets
-// the film after plane k1 - 1.
-__global__ void film_frames_kernel(const double* __restrict__ planes, int64_t k0, int64_t k1,
-                                   const double* __restrict__ film_src, double* __restrict__ film_dst, int w, int h,
-                                   double count0, uint8_t* __restrict__ frames) {
-    const int64_t npix = (int64_t)w * h;
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= npix) return;
-    double f0 = film_src[q], f1 = film_src[npix + q], f2 = film_src[2 * npix + q];
-    double cnt = count0;
-    const int x = (int)(q / h), y = (int)(q % h);
-    for (int64_t k = k0; k < k1; ++k) {
-        const double* __restrict__ pl = planes + k * 3 * npix;
-        f0 = f0 + pl[q] / 1.0;
-        f1 = f1 + pl[npix + q] / 1.0;
-        f2 = f2 + pl[2 * npix + q] / 1.0;
-        cnt = cnt + 1.0;
-        if (frames) {
-            uint8_t* o = frames + k * npix * 4 + ((int64_t)y * w + x) * 4;
-            o[0] = (uint8_t)(int)(255.99 * sqrt(aces1(f0 / cnt)));
-            o[1] = (uint8_t)(int)(255.99 * sqrt(aces1(f1 / cnt)));
-            o[2] = (uint8_t)(int)(255.99 * sqrt(aces1(f2 / cnt)));
-            o[3] = 255;
-        }
-    }
-    film_dst[q] = f0;
-    film_dst[npix + q] = f1;
-    film_dst[2 * npix + q] = f2;
 }
 
 __global__ void film_mean_kernel(const double* __restrict__ film, int64_t npix, double frame_count, double* __restrict__ out) {
@@ -466,14 +427,6 @@ hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h,
     const int64_t npix = (int64_t)w * h;
     hipLaunchKernelGGL(film_post_kernel, dim3(grid_for(npix, 256)), dim3(256), 0, st, accum, film, w, h, spp,
                        frame_count, add, rgba);
-    return hipGetLastError();
-}
-
-hipError_t mfx_launch_film_frames(const double* planes, int64_t k0, int64_t k1, const double* film_src,
-                                  double* film_dst, int w, int h, double count0, uint8_t* frames, hipStream_t st) {
-    const int64_t npix = (int64_t)w * h;
-    hipLaunchKernelGGL(film_frames_kernel, dim3(grid_for(npix, 256)), dim3(256), 0, st, planes, k0, k1, film_src,
-                       film_dst, w, h, count0, frames);
     return hipGetLastError();
 }
 

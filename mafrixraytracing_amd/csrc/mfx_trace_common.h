@@ -643,6 +643,15 @@ __device__ __forceinline__ void rayf_origin(RayF& r, DV o) {
     r.oix = (float)o.x * r.ix; r.oiy = (float)o.y * r.iy; r.oiz = (float)o.z * r.iz;
 }
 
+// PostProcessAndToScreenBuffer's per-channel byte (Scene.fs:280-289, 315-330): ACES tone curve,
+// clamp, sqrt (gamma 2), 255.99 scale, truncated
+__device__ __forceinline__ double clamp01(double x) { return x < 0. ? 0. : (x > 1. ? 1. : x); }
+__device__ __forceinline__ double aces1(double x) {
+    const double a = 2.51, b = 0.03, c = 2.43, d = 0.59, e = 0.14;
+    return clamp01((x * (a * x + b)) / (x * (c * x + d) + e));
+}
+__device__ __forceinline__ uint8_t post_byte(double t) { return (uint8_t)(int)(255.99 * sqrt(aces1(t))); }
+
 #define MFX_TRAV_EXIT (-0x7fffffff - 1)  // node value: traversal finished (stack empty, no hit child)
 
 // two-level scenes: a node value that enters an instance (~(MFX_INST_FLAG | instance)); leaf codes

@@ -99,8 +99,13 @@ struct WfParams {
     MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
     MfxCamera cam;
     double* accum;  // [3][w*h]
-    double* planes; // non-null: k_resolve writes each sample's 1-spp image to its own [3][w*h] plane
-                    // (plane = the sample's index in the call) instead of adding to accum
+    // render-ahead (k_resolve's frames mode): film != null makes the call's samples one-sample render
+    // calls, added in order to the film state film[3][w*h] instead of accum, frames != null also gets
+    // each call's RGBA8 frame (y-major, w*h*4 per sample index of the call), frameCount = count0 +
+    // the sample's index + 1
+    double* film;
+    uint8_t* frames;
+    double count0;
     // path slots (SoA)
     double *ox, *oy, *oz;  // ray origin; k_extend overwrites it with the hit point
     double *dx, *dy, *dz;  // ray direction

@@ -1054,8 +1054,13 @@ __device__ __forceinline__ void fold_path(const WfParams& P, int64_t j, const Pa
 // The records of WF_RES_SAMPLES samples are loaded together (state words, which carry a finished
 // path's lit mask, then vertex records: two rounds of independent loads), then folded and added in
 // sample order.
-// Render-ahead (P.planes): each sample's 1-spp image goes to its own plane, 0.0 + its path (what a
-// one-sample call adds to its zeroed accumulator), 0.0 for a black one.
+// Render-ahead (P.film, the frames mode): the samples are one-sample render calls. Each adds its
+// 1-spp image — 0.0 + its path, what a one-sample call's zeroed accumulator holds, 0.0 for a black
+// one — to the film state in sample order (Film.AddSample, Film.fs:18-23: film + frame / 1.0),
+// and with P.frames writes that call's RGBA8 frame (PostProcessAndToScreenBuffer of film /
+// frameCount, Scene.fs:315-330; frameCount = count0 + the sample's index + 1): the FP64 operations
+// film_post_kernel runs per call, in the same order, so every frame is that call's bytes. The film
+// state (P.film) carries across a call's generations.
 // ------------------------------------------------------------------------------------------------
 __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     __shared__ double alb[3 * WF_RES_MAT_LDS];
@@ -1074,12 +1079,8 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     const int64_t npix = (int64_t)P.width * P.height;
     const int64_t pixel = (int64_t)x * P.height + y;
     const int64_t end = P.path_base + P.total;
-    double ax = 0.0, ay = 0.0, az = 0.0;
-    if (!P.planes) {
-        ax = P.accum[pixel];
-        ay = P.accum[npix + pixel];
-        az = P.accum[2 * npix + pixel];
-    }
+    double* acc = P.film ? P.film : P.accum;
+    double ax = acc[pixel], ay = acc[npix + pixel], az = acc[2 * npix + pixel];
     constexpr int U = WF_RES_SAMPLES;
     for (int64_t smp0 = P.path_base / per_sample; smp0 * per_sample < end; smp0 += U) {
         int64_t jv[U];
@@ -1106,11 +1107,18 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
             if (!in[u]) continue;
             double fx = 0.0, fy = 0.0, fz = 0.0;
             if (R[u].mask) fold_path(P, jv[u], R[u], alb, fx, fy, fz);
-            if (P.planes) {
-                double* pl = P.planes + (smp0 + u) * 3 * npix;
-                pl[pixel] = 0.0 + fx;
-                pl[npix + pixel] = 0.0 + fy;
-                pl[2 * npix + pixel] = 0.0 + fz;
+            if (P.film) {
+                ax = ax + (0.0 + fx) / 1.0;
+                ay = ay + (0.0 + fy) / 1.0;
+                az = az + (0.0 + fz) / 1.0;
+                if (P.frames) {
+                    const double cnt = P.count0 + (double)(smp0 + u + 1);
+                    uint8_t* o = P.frames + (smp0 + u) * npix * 4 + ((int64_t)y * P.width + x) * 4;
+                    o[0] = post_byte(ax / cnt);
+                    o[1] = post_byte(ay / cnt);
+                    o[2] = post_byte(az / cnt);
+                    o[3] = 255;
+                }
             } else if (R[u].mask) {  // a path with no lit vertex adds nothing
                 ax += fx;
                 ay += fy;
@@ -1118,10 +1126,9 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
             }
         }
     }
-    if (P.planes) return;
-    P.accum[pixel] = ax;
-    P.accum[npix + pixel] = ay;
-    P.accum[2 * npix + pixel] = az;
+    acc[pixel] = ax;
+    acc[npix + pixel] = ay;
+    acc[2 * npix + pixel] = az;
 }
 
 // ------------------------------------------------------------------------------------------------

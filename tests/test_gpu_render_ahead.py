@@ -1,6 +1,7 @@
 """Render-ahead (mfx_options.render_ahead; DESIGN.md §7 "Scene.Render"): one-sample render calls
-served from a batch of the next K samples traced at once by the wavefront, each sample's 1-spp
-image in its own plane. Every frame must be the bytes of the one-sample-per-call path, which the
+served from a batch of the next K samples traced at once by the wavefront, whose k_resolve adds
+them to the film in call order and writes each call's frame. Every frame must be the bytes of the
+one-sample-per-call path, which the
 oracle pins (test_gpu_parity.test_film_render_rgba8_matches_oracle_post); here both contexts run
 side by side, and the first frames are also checked against the oracle's film directly."""
 import numpy as np
@@ -15,7 +16,7 @@ pytestmark = pytest.mark.gpu
                                          ("spot16_instanced@2l", 40, 24, 3), ("two_spheres_plane", 32, 32, 2)])
 def test_render_ahead_frames_are_the_one_sample_frames(gpu, name, w, h, K):
     """12 Scene.Render calls with a reset after the 7th and an spp = 2 call in between (traced by
-    the plain path; the next one-sample call still takes its plane from the held batch): identical
+    the plain path; the next one-sample call needs a batch traced again from the film as it is then): identical
     RGBA8 bytes every call and an identical film."""
     from mafrixraytracing_amd.native import NativeContext
     a = scene(name, w, h)
@@ -58,7 +59,7 @@ def test_render_ahead_pipeline_survives_interleaved_calls(gpu):
 
 
 @pytest.mark.parametrize("budget,label", [(1024, "none fits: one sample per call"),
-                                          (1 << 20, "one buffer, no background batch")])
+                                          (300_000, "one buffer, no background batch")])
 def test_render_ahead_memory_fallbacks(gpu, monkeypatch, budget, label):
     """Render-ahead under a memory budget (MFX_RENDER_AHEAD_MAX_BYTES caps the quarter of free HBM
     the buffers may take): with no room for two samples the context falls back to one sample per
