@@ -482,7 +482,10 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     bool active = false;
     int se = 0;  // the lane's listed entry: slot (WF_ENTRY_SLOT), lit mask << 28, camera-ray flag (sign)
     Trav T{};
-    uint32_t c_primary = 0, c_ext = 0;
+    // rays started by this wave: every listed entry is started, so the wave counts its lists (a
+    // wave-uniform sum) instead of each lane its rays (a per-lane counter spilled to scratch, whose
+    // increment put a scratch round trip into every refill)
+    uint32_t c_listed = 0;
     Stats st{0, 0, 0};
     constexpr bool DG = MFX_DIAG_STAMPS == 1;
     DiagAcc dg{};
@@ -516,11 +519,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             d = vnormalize(vsub(target, o));
             // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH); the
             // key is derived again by k_shadow (stored only for a path that continues)
-            c_primary++;
         } else {
             o = dv(P.ox[s], P.oy[s], P.oz[s]);
             d = dv(P.dx[s], P.dy[s], P.dz[s]);
-            c_ext++;
         }
         trav_begin(T, S, o, d, 99999999.);  // Integrators.fs:108
         active = true;
@@ -573,6 +574,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                 wave_lds_sync();
                 pend_lo = 0;
                 pend_hi = n;
+                c_listed += (uint32_t)n;
                 if (n == 0) break;  // every chunk scanned
             }
             const int avail = pend_hi - pend_lo;
@@ -595,10 +597,13 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         DIAG_MARK(dg, fin, DG);
     }
     unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
-    block_add<4>(cnt + 0, c_primary, red);
+    // a generation's first iteration lists camera rays only (every slot FREE), the others extension
+    // rays only; lane 0 carries the wave's count
+    const uint32_t c_wave = lane == 0 ? c_listed : 0u;
+    block_add<4>(cnt + 0, P.start ? c_wave : 0u, red);
     // extension rays: per iteration where it has a counter (the paths that went on; the host adds
     // them into counter 1)
-    block_add<4>(cnt + (P.iter > 0 && P.iter < WF_ITER_CTRS ? WF_CTR_ITER + P.iter : 1), c_ext, red);
+    block_add<4>(cnt + (P.iter > 0 && P.iter < WF_ITER_CTRS ? WF_CTR_ITER + P.iter : 1), P.start ? 0u : c_wave, red);
     if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
         atomicAdd(cnt + 10, (unsigned long long)dg.fetch);
