@@ -849,7 +849,9 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = live && n <= f;
         m[k] = __ballot(h);
-        const float kd = __shfl(h ? n : 3.0e38f, rep);
+        // the representative lane's entry distance, read across lanes into a scalar register
+        // (v_readlane: rep is wave-uniform; a __shfl is an LDS permute on the step's chain)
+        const float kd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h ? n : 3.0e38f), rep));
         d[k] = m[k] ? kd : __builtin_inff();
         nh += m[k] ? 1 : 0;
     }
@@ -859,17 +861,19 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
     cswap3(d[1], c[1], m[1], d[3], c[3], m[3]);
     cswap3(d[1], c[1], m[1], d[2], c[2], m[2]);
     nh = __builtin_amdgcn_readfirstlane(nh);
-    if (nh >= 2) {
-        stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
-        stm[sp] = nh == 4 ? m[3] : (nh == 3 ? m[2] : m[1]);
-    }
-    if (nh >= 3) {
-        stk[sp + 1] = nh == 4 ? c[2] : c[1];
-        stm[sp + 1] = nh == 4 ? m[2] : m[1];
-    }
-    if (nh >= 4) {
-        stk[sp + 2] = c[1];
-        stm[sp + 2] = m[1];
+    if (__lane_id() == 0) {  // the pushes are wave-uniform: one lane writes them
+        if (nh >= 2) {
+            stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
+            stm[sp] = nh == 4 ? m[3] : (nh == 3 ? m[2] : m[1]);
+        }
+        if (nh >= 3) {
+            stk[sp + 1] = nh == 4 ? c[2] : c[1];
+            stm[sp + 1] = nh == 4 ? m[2] : m[1];
+        }
+        if (nh >= 4) {
+            stk[sp + 2] = c[1];
+            stm[sp + 2] = m[1];
+        }
     }
     int next;
     if (nh > 0) {
