@@ -832,6 +832,10 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
             wf_queue_views(c, P, d);
             // a queue's entries are all live rays: smaller chunks keep the launch's tail short
             P.chunk = P.qcount ? c->wf_qchunk : chunk0;
+            // in place on a small frame (the strong-scaling shares), k_shadow takes half chunks: the
+            // first vertex's last chunks are its launch's tail (r04u: C2 at 8 spp +2.4 %; at 64 spp
+            // the same halving costs 1.5 %, so frames of more than 2^25 paths keep whole chunks)
+            P.chunk_shd = (!P.qcount && total <= ((int64_t)1 << 25)) ? std::max(64, P.chunk / 2) : P.chunk;
             if (!own_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;

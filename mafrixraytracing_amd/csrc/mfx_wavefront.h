@@ -147,6 +147,7 @@ struct WfParams {
     int32_t stack_lds_ext, stack_lds_shd; // of which in LDS, per kernel; the rest in `spill`
     int32_t* spill;                       // [stack_size - stack_lds][grid * 256] deep stack entries
     int32_t chunk;                        // slots per chunk fetch of the kernels
+    int32_t chunk_shd;                    // k_shadow's (half of chunk in place on a frame of at most 2^25 paths)
     int32_t start;                        // 1 in a generation's first iteration: FREE slots start paths
     int32_t tile_padding;                 // 1 if 8 does not divide the film: some path indices are padding
     int64_t base_smp, base_q;             // path_base = base_smp * per_sample + base_q

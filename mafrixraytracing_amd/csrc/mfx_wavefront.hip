@@ -749,7 +749,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk, shard_size, P.state, Q ? P.qcount : nullptr, P.ctl + WF_CTL_CLOSED_SHD)) {
+                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk_shd, shard_size, P.state, Q ? P.qcount : nullptr, P.ctl + WF_CTL_CLOSED_SHD)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
