@@ -3,15 +3,18 @@
 
 Workload (BASELINE.json configs[1]; --config C3/C4/C5 for the others):
 scenes/spot.xml — spot (5,856 triangles)
-on a floor quad under a quad light, 1920x1080, 64 samples per pixel per GPU, maxDepth 3.
-A step = one frame: every GPU traces its disjoint sample partition into an FP64 accumulator,
-then (N > 1) one RCCL sum-reduce of that [3][w*h] buffer to GPU 0.
-  --scaling weak (default): 64 spp per GPU, the N-GPU job renders 64*N spp of the same frame;
-  --scaling strong: the job renders the config's 64 spp, split over the N GPUs.
+on a floor quad under a quad light, 1920x1080, 64 samples per pixel, maxDepth 3.
+A step = one frame: every GPU traces every sample of its disjoint set of the film's 8-pixel tile
+rows (image partition: rows t % N == rank, MFX_F_ROW_PARTITION) into an FP64 accumulator, then
+(N > 1) the ranks' rows are gathered to GPU 0 (RowGather over RCCL: 1/N of the [3][w*h] buffer per
+rank; the merged frame is the 1-GPU frame bit for bit).
+  --scaling strong (default): the job renders the metric's 1080p x 64 spp, each GPU 1/N of the film;
+  --scaling weak: 64 spp of a whole film per GPU (the N-GPU job renders 64*N spp); each N > 1 line
+  carries the other scaling of the same job, measured in the same run, as a sub-object.
 N > 1 runs one process per GPU under torch.distributed.run (the driver's launch;
 mafrixraytracing_amd/distributed.py, RCCL through torch.distributed), or with --single-process
-one process whose library context drives all N devices and reduces with its own RCCL
-communicator (mfx_options.devices, the path the F# host binds).
+one process whose library context drives all N devices (mfx_options.devices: the same tile-row
+partition, merged with the library's own RCCL communicator; the path the F# host binds).
 --api render times the reference's real call pattern instead: Scene.Render = 1 spp per call,
 mfx_render_rgba8(ctx, 1, buf) with the 8 MB RGBA8 readback, the config's spp calls per step.
 
@@ -46,7 +49,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
-XGMI_LINK_GBS = 153.0  # one xGMI link of MI355X (7 per GPU); the reduce model assumes one ring over one link
+XGMI_LINK_GBS = 153.0  # one xGMI link of MI355X (7 per GPU): the exchange models move each rank's bytes over one link
 SPOT_SCENE = os.path.join(ROOT, "scenes", "spot.xml")
 # BASELINE.json configs: scene, spp per GPU per step at N = 1, label. C4 and C5 are
 # 8-GPU configs; at N = 1 a step is one GPU's share of them (256/8 and 512/8 spp).
@@ -77,8 +80,10 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-stats", action="store_true", help="skip the traversal-counter pass")
     ap.add_argument("--megakernel", action="store_true", help="persistent megakernel instead of the wavefront")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: config spp per GPU; strong: config spp per job, split over the GPUs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="strong: the config's spp per job, each GPU 1/N of the film; weak: config spp of a whole film per GPU")
+    ap.add_argument("--partition", default="rows", choices=["rows", "samples"],
+                    help="N > 1 ranks: rows = image partition + RowGather (default); samples = sample partition + sum-reduce")
     ap.add_argument("--single-process", action="store_true",
                     help="N > 1 from one process: one library context over N devices (its own RCCL reduce)")
     ap.add_argument("--render-ahead", type=int, default=0,

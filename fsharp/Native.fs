@@ -135,7 +135,12 @@ module Api =
     extern nativeint mfx_last_error()
     [<DllImport("mafrix_rt", CallingConvention = CallingConvention.Cdecl)>]
     extern int mfx_device_count()
+    [<DllImport("mafrix_rt", CallingConvention = CallingConvention.Cdecl)>]
+    extern int mfx_abi_version()
 
+/// include/mafrix_rt.h MFX_ABI_VERSION these declarations follow: a libmafrix_rt of another ABI
+/// (struct layouts, call semantics) is refused at construction instead of failing silently.
+let MFX_ABI_VERSION = 6
 let MFX_F_NONE = 0
 let MFX_F_HOST_BVH = 4      // build the traversal BVH on the CPU instead of the GPU (the same tree)
 let DefaultSeed = 0x4D414652UL
@@ -149,6 +154,12 @@ let DefaultRenderAhead = 64
 let check (rc : int) (what : string) =
     if rc <> 0 then
         failwithf "%s failed (%d): %s" what rc (Marshal.PtrToStringAnsi(Api.mfx_last_error()))
+
+/// The loaded libmafrix_rt must be the ABI these declarations were written for.
+let checkAbi () =
+    let v = Api.mfx_abi_version()
+    if v <> MFX_ABI_VERSION then
+        failwithf "libmafrix_rt ABI %d, this binding needs ABI %d (rebuild or update the binding)" v MFX_ABI_VERSION
 
 // ---- reference types -> ABI ----------------------------------------------------------------------
 
@@ -236,7 +247,8 @@ let marshalCamera (camera : ICamera) : MfxPinhole =
 
 /// IPixelIntegrator (IIntegrator.fs:35-40) over one libmafrix_rt context.
 ///   devices = [||]: HIP device 0; devices = [|0..7|]: one context drives all eight GPUs of the
-///   node, each rendering its sample partition, reduced with the library's own RCCL communicator.
+///   node by an image partition (GPU g traces the 8-pixel tile rows r % 8 = g of every frame and
+///   batch, and copies its rows of each RGBA8 frame into the buffer): the frames are the one-GPU bytes.
 /// Sample(n) writes the mean of n fresh samples per pixel straight into a pinned Color[w,h]
 /// (Color is a sequential 4 x float struct, Color.fs:3-4; element (i,j) at i*h + j, as
 /// mfx_sample writes it) and returns the Texture2D over it, as PixelIntegrator returns its own
@@ -246,6 +258,7 @@ type NativePixelIntegrator(shapes : IHitable[], light : INewLight, camera : ICam
     let data : Color[,] = Array2D.zeroCreate<Color> width height
     let texture = Texture2D<Color>(data, width, height)
     let ctx =
+        checkAbi ()
         let prims = marshalShapes shapes
         let albedo = marshalAlbedo ()
         let hp = GCHandle.Alloc(prims, GCHandleType.Pinned)

@@ -30,7 +30,7 @@
 extern "C" {
 #endif
 
-#define MFX_ABI_VERSION 5
+#define MFX_ABI_VERSION 6  /* 6: device lists partition the film by tile rows; MFX_F_ROW_PARTITION */
 #define MFX_MAX_DEVICES 64
 #define MFX_MAX_RENDER_AHEAD 1024
 
@@ -96,21 +96,26 @@ typedef struct mfx_scene_desc {
 /* Context options.
  * Devices: with ndevices == 0 the context runs on `device`. With ndevices > 0 it drives
  * devices[0..ndevices) from this one process (the reference's in-process fan-out,
- * Integrators.fs:164, across GPUs): device g renders sample sub-partition
- * part_index + g*part_count of part_count*ndevices on its own stream, and one RCCL reduce
- * (a communicator the library owns, ncclCommInitAll over the list) sums the FP64 accumulators
- * into devices[0], where film and post run. A list that repeats a device (e.g. {0,0}) adds the
- * accumulators in device order instead (RCCL needs distinct devices).                        */
-typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ahead (0 = off) */
+ * Integrators.fs:164, across GPUs) by an image partition: device g of G traces the film's
+ * 8-pixel tile rows r with r % G == g, every sample of the context's sample partition, on its own
+ * stream. Every per-pixel operation (the sample-order sum, Film.AddSample, the post) therefore runs
+ * on one device in the one-device order, and every output is bit-identical to a one-device
+ * context's. mfx_render_rgba8 (render-ahead included) copies each device's rows of the RGBA8
+ * frame straight into the caller's buffer; mfx_sample and mfx_film_mean merge the devices' FP64
+ * buffers on devices[0] (one RCCL reduce over a communicator the library owns, ncclCommInitAll over
+ * the list; a pixel is +0.0 on every device but its own, so the sum is an exact merge). A list that
+ * repeats a device (e.g. {0,0}) merges by device-ordered adds instead (RCCL needs distinct devices). */
+typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ahead (0 = off); layout unchanged since */
     uint64_t seed;      /* counter-RNG seed; the reference uses unseeded System.Random */
     int32_t device;     /* HIP device ordinal when ndevices == 0 */
     int32_t flags;      /* MFX_F_* */
     int32_t part_index; /* this context renders sample partition part_index of part_count */
-    int32_t part_count; /* (multi-process: one context per rank; partitions are disjoint sample sets) */
+    int32_t part_count; /* (multi-process: one context per rank; partitions are disjoint sample sets;
+                           with MFX_F_ROW_PARTITION disjoint sets of tile rows r % part_count == part_index) */
     int32_t ndevices;   /* 0: one device (`device`); 1..MFX_MAX_DEVICES: the device list below */
     int32_t render_ahead; /* 0 or 1: off. K in 2..MFX_MAX_RENDER_AHEAD: one-sample mfx_render_rgba8
-                             calls (Scene.Render) on a one-device context take their sample from a
-                             batch of the next K samples traced at once (see mfx_render_rgba8)    */
+                             calls (Scene.Render) take their sample from a batch of the next K
+                             samples traced at once, on every device of a list (mfx_render_rgba8)  */
     const int32_t* devices; /* [ndevices] HIP device ordinals; devices[0] is the primary */
 } mfx_options; /* 40 bytes */
 
@@ -127,6 +132,10 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
                                flattened when the flat image fits MFX_FLATTEN_MAX_BYTES (env; default
                                2 GiB at 512 B per traversal slot of the expansion) and a sixteenth of
                                the device's free memory, two-level otherwise. Both flags: MFX_E_INVALID */
+#define MFX_F_ROW_PARTITION 64 /* part_index / part_count partition the film's 8-pixel tile rows (r % part_count
+                               == part_index) instead of the samples: a rank traces every sample of its rows,
+                               its accumulator is +0.0 elsewhere, and a sum-reduce over the ranks is an exact
+                               merge (the multi-process image partition; mfx_trace_accumulate)       */
 
 /* One entry of an instanced scene (mfx_create_instanced; an extension: the reference has no
  * instancing, its scenes are flat lists). The world primitive list — the index space Bvh.Build
@@ -187,7 +196,7 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * progressive mean through ACES -> sqrt -> int(255.99 c) as RGBA8, y-major:
  * rgba[(y*w + x)*4 + {0,1,2,3}]. `Scene.Render(delta, buffer)` is this call with spp = 1.
  * rgba may be NULL (accumulate only).
- * Render-ahead (mfx_options.render_ahead = K > 1, one device, part_count 1): one-sample calls are
+ * Render-ahead (mfx_options.render_ahead = K > 1, part_count 1): one-sample calls are
  * served from batches of K samples. A call whose global sample is not held traces the next K
  * samples in one batched pass that runs the film add and post of all K calls ahead, in call
  * order; each call of the batch then only copies its RGBA8 frame, and while a batch is served the
@@ -202,7 +211,9 @@ int mfx_sample(mfx_ctx* ctx, int32_t spp, double* frame_xmajor_rgba);
  * the context frees the buffers and renders one sample per call from then on. A background batch
  * is traced once a batch starts being served, so an application that stops early has traced at
  * most one batch ahead. The accumulator (mfx_accum_read_mean) does not hold the samples of calls
- * served from batches.                                                                        */
+ * served from batches. On a device list every device serves its tile rows from its own batches
+ * (the same K on each: the tightest device's budget, shared by a list's contexts on one GPU).
+ * mfx_film_mean after calls served mid-batch traces each served sample again once, film only.   */
 int mfx_render_rgba8(mfx_ctx* ctx, int32_t spp, uint8_t* rgba_ymajor);
 
 /* The same call under SURVEY.md §8(b)'s name for it (Film.GetFrame + PostProcess). */
@@ -222,8 +233,8 @@ int mfx_film_mean(mfx_ctx* ctx, double* frame_xmajor_rgba);
  * Does not synchronise; mfx_sync() does.                                                     */
 int mfx_trace_accumulate(mfx_ctx* ctx, int32_t spp, int64_t sample_base);
 /* Multi-device context: sum every device's accumulator into the primary's (RCCL reduce, root
- * devices[0]), ordered after each device's trace. No-op on a single-device context.
- * mfx_sample / mfx_render_rgba8 call it themselves.                                          */
+ * devices[0]), ordered after each device's trace: after a clear and a trace, an exact merge of
+ * the devices' tile rows. No-op on a single-device context. mfx_sample calls it itself.       */
 int mfx_accum_reduce(mfx_ctx* ctx);
 int mfx_accum_clear(mfx_ctx* ctx);
 /* Device pointer + byte size of the (primary device's) FP64 accumulator (for an RCCL reduce

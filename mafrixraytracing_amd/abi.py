@@ -23,9 +23,10 @@ MFX_F_HOST_BVH = 4
 MFX_F_WAVEFRONT = 8
 MFX_F_FLATTEN = 16
 MFX_F_TWO_LEVEL = 32
+MFX_F_ROW_PARTITION = 64
 MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
-MFX_ABI_VERSION = 5
+MFX_ABI_VERSION = 6
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")

@@ -124,7 +124,10 @@ struct mfx_ctx {
     unsigned long long* d_counters = nullptr;  // [8]
     uint64_t seed = 0;
     int flags = 0;
-    int part_index = 0, part_count = 1;
+    int part_index = 0, part_count = 1;  // sample partition: global samples part_index mod part_count
+    // image partition: this device traces the film's 8-pixel tile rows r = band_index mod band_count
+    // (device g of a G-device list: g of G; an MFX_F_ROW_PARTITION rank composes with it)
+    int band_index = 0, band_count = 1;
     int64_t next_sample = 0;
     double frame_count = 0.0;
     int grid = 0;
@@ -143,7 +146,11 @@ struct mfx_ctx {
     WfQueue wq[2]{};
     int wf_queue_from = MFX_RAY_QUEUE ? -2 : -1;  // -2: automatic (wf_queue_auto)
     int wf_queue_auto = 1;  // from the last trace's live paths per iteration (note_live); 1 before any
-    bool wf_auto_read = false;  // the first wavefront trace's counters have been read for wf_queue_auto
+    // The first wavefront trace's counters are read once for wf_queue_auto, after every device of
+    // the call has been enqueued (settle_queue_auto). Render-ahead batches settle it from each
+    // batch's counters instead (note_live in ahead_render).
+    bool wf_auto_read = false;
+    bool wf_auto_pending = false;  // a trace whose counters settle wf_queue_auto has been enqueued
     int32_t wf_qchunk = 128;  // entries per chunk fetch on a ray queue (MFX_QCHUNK; r04j: 128 against 256, C2 8 spp +2 %)
     // Path slots of the wavefront pool, at most. A pool as large as a frame's path count (C2: 133 M
     // slots, 15 GB) runs the frame as one generation: no kernel ends with a partly filled pool
@@ -181,6 +188,11 @@ struct mfx_ctx {
     int64_t ab_last_k = -1;          // and its index in that buffer
     uint64_t film_epoch = 1;         // bumped when the film leaves the held frames' sequence
     bool film_in_dfilm = true;       // d_film holds the film (else: ab[ab_cur].film_in + its samples up to ab_last_k)
+    // d_film = ab[dfilm_buf].film_in + that batch's first dfilm_n samples (dfilm_buf >= 0): a later
+    // ahead_materialize traces only the samples after those (a caller alternating
+    // Render and film_mean re-traced 1, 2, ..., K - 1 samples per batch)
+    int dfilm_buf = -1;
+    int64_t dfilm_n = 0;
     unsigned long long* d_counters_aux = nullptr;  // ray counters of a film-only re-trace (not reported)
     hipEvent_t aux_ev0 = nullptr, aux_ev1 = nullptr;
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
@@ -197,6 +209,7 @@ struct mfx_ctx {
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
     std::vector<mfx_ctx*> peers;         // devices[1..G) of the device list, same host scene
     std::vector<ncclComm_t> comms;       // [G] one RCCL communicator per device, rank g = device g
+    double* d_merge = nullptr;           // [3][npix] the devices' films merged (mfx_film_mean), allocated on first use
     double* d_reduce_stage = nullptr;    // repeated-device list: a peer's accumulator copied here
     std::vector<hipEvent_t> peer_done;   // repeated-device list: per peer, its trace has finished
     hipEvent_t reduce_done = nullptr;    // repeated-device list: the primary has read every peer's buffer
@@ -207,6 +220,12 @@ static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
     std::vector<mfx_ctx*> v{c};
     v.insert(v.end(), c->peers.begin(), c->peers.end());
     return v;
+}
+
+// tile rows of the film in a device's band (its image partition)
+static int band_rows(const mfx_ctx* d) {
+    const int tr = (d->host.height + 7) / 8;
+    return tr > d->band_index ? (tr - d->band_index + d->band_count - 1) / d->band_count : 0;
 }
 
 static void ahead_free(mfx_ctx* c) {
@@ -239,6 +258,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
+    if (c->d_merge) (void)hipFree(c->d_merge);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
@@ -400,7 +420,8 @@ static int ctx_setup(mfx_ctx* c) {
             (shd ? c->wf_ntop_shd : c->wf_ntop_ext) = lo;
             // A small scene's whole slot array (80-B test prefixes) in LDS too, when it fits beside the
             // top nodes without costing a resident block: every leaf test then reads LDS (C3: 26 slots)
-            int ns = (int)c->host.slots.size();
+            // (two-level scenes: none — their kernel instances never read slots from LDS)
+            int ns = inst ? 0 : (int)c->host.slots.size();
             if (ns > WF_SLOT_LDS_MAX || (getenv("MFX_SLOT_LDS") && atoi(getenv("MFX_SLOT_LDS")) == 0)) ns = 0;
             if (ns > 0) {
                 int b = 0;
@@ -502,14 +523,21 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         const bool dev = err.rfind("GPU BVH build", 0) == 0;
         return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
     }
-    // device g of G renders sub-partition part_index + g * part_count of part_count * G: the union
-    // over the devices is exactly the caller's partition (global samples s = part_index mod part_count)
+    // Image partition: device g of G traces the film's tile rows r = g mod G, every sample of the
+    // caller's partition, so every per-pixel operation (the sample-order sum, the film add, the post)
+    // runs on one device in the one-device order: images are bit-identical to one device's, and the
+    // devices' buffers merge exactly (a pixel is non-zero on its own device only). With
+    // MFX_F_ROW_PARTITION the caller's part_index / part_count select tile rows too: device g renders
+    // rows part_index + g * part_count of part_count * G (no sample partition).
+    const bool rows = (opt->flags & MFX_F_ROW_PARTITION) != 0;
     auto init = [&](mfx_ctx* d, int g) {
         d->device = devlist[g];
         d->seed = opt->seed;
         d->flags = opt->flags;
-        d->part_index = opt->part_index + g * opt->part_count;
-        d->part_count = opt->part_count * G;
+        d->part_index = rows ? 0 : opt->part_index;
+        d->part_count = rows ? 1 : opt->part_count;
+        d->band_index = rows ? opt->part_index + g * opt->part_count : g;
+        d->band_count = rows ? opt->part_count * G : G;
         d->api_part_count = opt->part_count;
     };
     init(c, 0);
@@ -750,8 +778,10 @@ static void note_live(mfx_ctx* c, const unsigned long long* h);
 static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode* fm = nullptr,
                     unsigned long long* counters = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
     const int W = c->host.width, H = c->host.height;
-    const int64_t per_sample = (int64_t)((W + 7) / 8) * ((H + 7) / 8) * 64;
+    const int brows = band_rows(c);
+    const int64_t per_sample = (int64_t)((W + 7) / 8) * brows * 64;  // the device's band of the film
     const int64_t total = per_sample * ns;
+    if (total == 0) return fail(MFX_E_STATE, "wf_trace: empty band");
     // generations of whole 64-path windows (one 8x8 tile of one sample each: the camera-ray packets)
     const int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
     const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
@@ -767,6 +797,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     P.sample_base = sample_base;
     P.part_index = c->part_index;
     P.part_count = c->part_count;
+    P.band_index = c->band_index;
+    P.band_count = c->band_count;
+    P.band_rows = brows;
     P.width = W;
     P.height = H;
     P.max_depth = c->host.max_depth;
@@ -862,16 +895,10 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     }
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
-    if (c->wf_queue_from == -2 && !c->wf_auto_read) {
-        // The automatic queue start is taken from a trace's per-iteration counters. Read them once,
-        // after the context's first wavefront trace, so a caller that never polls the counters gets
-        // the same kernels as one that does (every later poll re-reads the same scene's shares).
-        unsigned long long h[WF_NCTR * WF_SHARDS];
-        HIPCHECK(hipMemcpyAsync(h, P.counters, sizeof(h), hipMemcpyDeviceToHost, c->stream));
-        HIPCHECK(hipStreamSynchronize(c->stream));
-        note_live(c, h);
-        c->wf_auto_read = true;
-    }
+    // The automatic queue start is taken from a trace's per-iteration counters: read once, after
+    // the context's first wavefront trace (settle_queue_auto, once every device has been
+    // enqueued), so a caller that never polls the counters gets the same kernels as one that does
+    if (c->wf_queue_from == -2 && !c->wf_auto_read) c->wf_auto_pending = true;
     c->it_recorded = iters;
     c->it_per_gen = per_gen;
     c->generations = (int)ngen;
@@ -881,7 +908,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
 // one device's share of mfx_trace_accumulate (its sample partition), enqueued on its stream
 static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(hipSetDevice(c->device));
-    const int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
+    int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
+    if (band_rows(c) == 0) ns = 0;  // a film too small to give this device a tile row
     HIPCHECK(hipMemsetAsync(c->d_work, 0, 64, c->stream));
     HIPCHECK(hipMemsetAsync(c->d_counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
     // One sample per pixel on this device (Scene.Render's call): the megakernel, unless the caller
@@ -916,6 +944,9 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     P.nsamples = ns;
     P.part_index = c->part_index;
     P.part_count = c->part_count;
+    P.band_index = c->band_index;
+    P.band_count = c->band_count;
+    P.band_rows = band_rows(c);
     P.width = c->host.width;
     P.height = c->host.height;
     P.max_depth = c->host.max_depth;
@@ -927,7 +958,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     if (c->mega_chunk > 0) {
         P.chunk = c->mega_chunk;
     } else {
-        const int64_t total = (int64_t)((c->host.width + 7) / 8) * ((c->host.height + 7) / 8) * 64 * ns;
+        const int64_t total = (int64_t)((c->host.width + 7) / 8) * band_rows(c) * 64 * ns;
         int64_t ch = 256;
         while (ch > 64 && total / ch < 16 * (int64_t)c->grid * 4) ch /= 2;
         P.chunk = (int)ch;
@@ -939,8 +970,26 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     return MFX_OK;
 }
 
-// Every device enqueues its partition on its own stream; nothing here waits for a device, so the
-// G devices render concurrently.
+// wf_queue_auto from the first wavefront trace's counters, read once every device of the call has
+// been enqueued (a blocking read inside the per-device loop ran device 0 to completion before the
+// next device was enqueued)
+static int settle_queue_auto(mfx_ctx* c) {
+    for (mfx_ctx* d : devs_of(c)) {
+        if (!d->wf_auto_pending) continue;
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipMemcpyAsync(d->h_counters, d->d_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipStreamSynchronize(d->stream));
+        note_live(d, d->h_counters);
+        d->wf_auto_pending = false;
+        d->wf_auto_read = true;
+    }
+    HIPCHECK(hipSetDevice(c->device));
+    return MFX_OK;
+}
+
+// Every device enqueues its band on its own stream; nothing here waits for a device (bar the
+// one-time settle_queue_auto read), so the G devices render concurrently.
 int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
@@ -950,40 +999,44 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
         if (rc) return rc;
     }
     HIPCHECK(hipSetDevice(c->device));  // the primary stays current for what the caller enqueues next
-    return MFX_OK;
+    return settle_queue_auto(c);
 }
 
 // Sum every device's accumulator into the primary's, stream-ordered after each device's trace, and
 // every peer's later work (a clear or trace of its accumulator) after the reduce: the RCCL reduce
 // runs on each device's own stream; the repeated-device copies run on the primary's stream, so
 // each peer's stream waits for them (reduce_done) before anything the caller enqueues next.
-int mfx_accum_reduce(mfx_ctx* c) {
-    if (!c) return fail(MFX_E_STATE, "null context");
-    if (!c->comms.empty()) {  // RCCL: rank g sends device g's buffer, the root reduces in place
+// The devices' [3][npix] buffers buf(d) summed into dst on the primary (dst may be buf(primary)).
+// A device's buffer is +0.0 outside its band (image partition), so the sum is an exact merge.
+static int reduce_planes(mfx_ctx* c, double* (*buf)(mfx_ctx*), double* dst, const char* what) {
+    if (!c->comms.empty()) {  // RCCL: rank g sends device g's buffer, the root reduces into dst
         const Rccl* R = rccl();  // loaded: the communicators exist
         const size_t count = 3 * (size_t)c->npix;
         const std::vector<mfx_ctx*> ds = devs_of(c);
         ncclResult_t r = R->groupStart();
         for (size_t g = 0; g < ds.size() && r == ncclSuccess; ++g) {
             HIPCHECK(hipSetDevice(ds[g]->device));
-            r = R->reduce(ds[g]->d_accum, ds[g]->d_accum, count, ncclFloat64, ncclSum, 0, c->comms[g], ds[g]->stream);
+            double* src = buf(ds[g]);
+            r = R->reduce(src, g == 0 ? dst : src, count, ncclFloat64, ncclSum, 0, c->comms[g], ds[g]->stream);
         }
         const ncclResult_t r2 = R->groupEnd();
         if (r == ncclSuccess) r = r2;
-        if (r != ncclSuccess) return fail(MFX_E_DEVICE, std::string("mfx_accum_reduce: ") + R->errorString(r));
+        if (r != ncclSuccess) return fail(MFX_E_DEVICE, std::string(what) + ": " + R->errorString(r));
         HIPCHECK(hipSetDevice(c->device));
         return MFX_OK;
     }
-    // a repeated-device list: add the peers' accumulators in device order (a0 + a1) + a2 ...
+    // a repeated-device list: add the peers' buffers in device order (a0 + a1) + a2 ...
     const size_t bytes = 3 * sizeof(double) * (size_t)c->npix;
+    HIPCHECK(hipSetDevice(c->device));
+    if (dst != buf(c)) HIPCHECK(hipMemcpyAsync(dst, buf(c), bytes, hipMemcpyDeviceToDevice, c->stream));
     for (size_t k = 0; k < c->peers.size(); ++k) {
         mfx_ctx* p = c->peers[k];
         HIPCHECK(hipSetDevice(p->device));
         HIPCHECK(hipEventRecord(c->peer_done[k], p->stream));
         HIPCHECK(hipSetDevice(c->device));
         HIPCHECK(hipStreamWaitEvent(c->stream, c->peer_done[k], 0));
-        HIPCHECK(hipMemcpyAsync(c->d_reduce_stage, p->d_accum, bytes, hipMemcpyDefault, c->stream));
-        HIPCHECK(mfx_launch_accum_add(c->d_accum, c->d_reduce_stage, 3 * c->npix, c->stream));
+        HIPCHECK(hipMemcpyAsync(c->d_reduce_stage, buf(p), bytes, hipMemcpyDefault, c->stream));
+        HIPCHECK(mfx_launch_accum_add(dst, c->d_reduce_stage, 3 * c->npix, c->stream));
     }
     if (!c->peers.empty()) {
         HIPCHECK(hipSetDevice(c->device));
@@ -997,10 +1050,16 @@ int mfx_accum_reduce(mfx_ctx* c) {
     return MFX_OK;
 }
 
+int mfx_accum_reduce(mfx_ctx* c) {
+    if (!c) return fail(MFX_E_STATE, "null context");
+    if (c->peers.empty() && c->comms.empty()) return MFX_OK;
+    return reduce_planes(c, [](mfx_ctx* d) { return d->d_accum; }, c->d_accum, "mfx_accum_reduce");
+}
+
 int mfx_trace_timing(mfx_ctx* c, double out[8]) {
     if (!c || !out) return fail(MFX_E_INVALID, "null argument");
     if (c->rep_valid) {  // a call served from held frames: its batch's device time, no stage split
-        for (int k = 0; k < 12; ++k) out[k] = 0.0;
+        for (int k = 0; k < 8; ++k) out[k] = 0.0;
         out[0] = c->rep_ms;
         return MFX_OK;
     }
@@ -1206,7 +1265,7 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
 }
 
 // ---- render-ahead --------------------------------------------------------------------------------
-// mfx_options.render_ahead = K > 1 on a one-device context with the whole sample set. Scene.Render
+// mfx_options.render_ahead = K > 1 with the whole sample set (part_count 1). Scene.Render
 // (Scene.fs:331-333) asks for one sample per call: alone, a 1080p sample is ~21 rays per lane of a
 // persistent grid plus the film/post launch and the readback per call. A sample's 1-spp image
 // depends only on (seed, global sample index), so a call whose sample is not held traces the next K
@@ -1218,24 +1277,49 @@ int mfx_ray_counts(mfx_ctx* c, double out[16]) {
 // trace). Every frame and the film are the bytes the one-sample path gives
 // (tests/test_gpu_render_ahead.py). A buffer holds K frames (4 B per pixel each) and two films: no
 // per-sample FP64 image is kept (round 3 kept one, 24 B per pixel per sample).
+// Device lists: every device runs the same batches over its own band of tile rows, in its own
+// buffers, film and copy stream, and a call copies each device's band rows of its frame straight
+// into the caller's buffer: no FP64 buffer crosses devices, and the frames are the one-device bytes.
+// The batch bookkeeping (base, n, expect, epoch, count0, reported) lives in the primary's ab[]; the
+// peers' ab[] hold their device buffers only.
 // The frames assume the calls follow each other with nothing else touching the film. A reset, a
 // render call of spp != 1 or an mfx_sample call (which moves the sample sequence) bumps film_epoch
 // after bringing d_film up to date; a held batch whose frames belong to an older epoch is traced
-// again from the sample the next call needs. d_film is brought up to date from the film before the
-// batch by tracing its served samples again, film only (ahead_materialize) — after a batch's last
-// call it is a copy of the film after it.
+// again from the sample the next call needs. d_film is brought up to date by tracing, film only,
+// the served samples it lacks (ahead_materialize): from the prefix of the batch it already holds
+// (dfilm_n), else from the film before the batch — after a batch's last call it is a copy of the
+// film after it. So a caller that alternates Render and mfx_film_mean re-traces each sample once.
+static void ahead_free_all(mfx_ctx* c) {
+    for (mfx_ctx* d : devs_of(c)) {
+        (void)hipSetDevice(d->device);
+        ahead_free(d);
+    }
+    (void)hipSetDevice(c->device);
+    c->dfilm_buf = -1;
+}
+
 static int ahead_alloc(mfx_ctx* c) {
     const size_t plane = 3 * sizeof(double) * (size_t)c->npix, frame = 4 * (size_t)c->npix;
     const size_t per_sample = frame, fixed = 2 * plane + WF_NCTR * WF_SHARDS * sizeof(unsigned long long);
-    size_t fr = 0, tot = 0;
-    HIPCHECK(hipMemGetInfo(&fr, &tot));
-    // Both buffers within MFX_RENDER_AHEAD_MAX_BYTES (default 2 GiB) and a quarter of the free HBM:
-    // a context never takes more than that for render-ahead, whatever K it asked for. K shrinks to
-    // fit two buffers (the background batch) while at least 8 samples fit in each; below that one
-    // buffer of as many samples as fit. At 1080p (8.3 MB per sample, 100 MB of films per buffer)
-    // K = 64 takes 1.26 GB for both.
-    size_t budget = std::min<size_t>(fr / 4, (size_t)2 << 30);
-    if (const char* e = getenv("MFX_RENDER_AHEAD_MAX_BYTES")) budget = std::min(budget, (size_t)atoll(e));
+    // Both buffers within MFX_RENDER_AHEAD_MAX_BYTES (default 2 GiB) and a quarter of the free HBM
+    // per device (shared by the contexts a device list puts on one GPU): a context never takes more
+    // than that for render-ahead, whatever K it asked for. K shrinks to fit two buffers (the
+    // background batch) while at least 8 samples fit in each; below that one buffer of as many
+    // samples as fit. At 1080p (8.3 MB per sample, 100 MB of films per buffer) K = 64 takes 1.26 GB
+    // for both. Every device of a list gets the same K (the tightest device's).
+    size_t cap = (size_t)2 << 30;
+    if (const char* e = getenv("MFX_RENDER_AHEAD_MAX_BYTES")) cap = std::min(cap, (size_t)atoll(e));
+    const std::vector<mfx_ctx*> ds = devs_of(c);
+    size_t budget = cap;
+    for (mfx_ctx* d : ds) {
+        size_t fr = 0, tot = 0;
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipMemGetInfo(&fr, &tot));
+        size_t share = 0;  // contexts of this list on the same GPU
+        for (mfx_ctx* o : ds) share += o->device == d->device ? 1 : 0;
+        budget = std::min(budget, std::min(fr / 4, cap) / share);
+    }
+    HIPCHECK(hipSetDevice(c->device));
     int nbuf = 2;
     int64_t k = std::min<int64_t>(c->render_ahead, budget / 2 > fixed ? (int64_t)((budget / 2 - fixed) / per_sample) : 0);
     if (k < std::min(8, c->render_ahead)) {
@@ -1244,50 +1328,64 @@ static int ahead_alloc(mfx_ctx* c) {
         k = std::min<int64_t>(k, c->render_ahead);
     }
     if (k < 2) return MFX_E_NOMEM;
-    for (int b = 0; b < nbuf; ++b) {
-        AheadBuf& B = c->ab[b];
-        hipError_t e = hipMalloc((void**)&B.frames, (size_t)k * frame);
-        if (e == hipSuccess) e = hipMalloc((void**)&B.film_in, plane);
-        if (e == hipSuccess) e = hipMalloc((void**)&B.film_out, plane);
-        if (e == hipSuccess) e = hipMalloc((void**)&B.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipEventCreate(&B.t0);
-        if (e == hipSuccess) e = hipEventCreate(&B.t1);
-        if (e == hipSuccess) e = hipEventCreateWithFlags(&B.ready, hipEventDisableTiming);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            ahead_free(c);
-            return e == hipErrorOutOfMemory ? MFX_E_NOMEM : fail(MFX_E_DEVICE, std::string("render-ahead: ") + hipGetErrorString(e));
+    hipError_t e = hipSuccess;
+    for (mfx_ctx* d : ds) {
+        e = hipSetDevice(d->device);
+        for (int b = 0; b < nbuf && e == hipSuccess; ++b) {
+            AheadBuf& B = d->ab[b];
+            e = hipMalloc((void**)&B.frames, (size_t)k * frame);
+            if (e == hipSuccess) e = hipMalloc((void**)&B.film_in, plane);
+            if (e == hipSuccess) e = hipMalloc((void**)&B.film_out, plane);
+            if (e == hipSuccess) e = hipMalloc((void**)&B.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
+            if (e == hipSuccess) e = hipEventCreate(&B.t0);
+            if (e == hipSuccess) e = hipEventCreate(&B.t1);
+            if (e == hipSuccess) e = hipEventCreateWithFlags(&B.ready, hipEventDisableTiming);
         }
+        if (e == hipSuccess) e = hipMalloc((void**)&d->d_counters_aux, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipEventCreate(&d->aux_ev0);
+        if (e == hipSuccess) e = hipEventCreate(&d->aux_ev1);
+        if (e != hipSuccess) break;
     }
-    hipError_t e = hipMalloc((void**)&c->d_counters_aux, WF_NCTR * WF_SHARDS * sizeof(unsigned long long));
-    if (e == hipSuccess) e = hipEventCreate(&c->aux_ev0);
-    if (e == hipSuccess) e = hipEventCreate(&c->aux_ev1);
     if (e != hipSuccess) {
         (void)hipGetLastError();
-        ahead_free(c);
+        ahead_free_all(c);
         return e == hipErrorOutOfMemory ? MFX_E_NOMEM : fail(MFX_E_DEVICE, std::string("render-ahead: ") + hipGetErrorString(e));
     }
+    HIPCHECK(hipSetDevice(c->device));
     c->ab_nbuf = nbuf;
     c->ab_cap = (int)k;
     return MFX_OK;
 }
 
-// d_film = the film as of the last render call: a copy of the film after the buffer's last call, or
-// the film before the buffer with its samples up to that call traced again, film only (the same
+// d_film (every device's) = the film as of the last render call: a copy of the film after the
+// buffer's last call, or the film before the buffer (or the prefix of the buffer's samples it
+// already holds) with the buffer's samples up to that call traced again, film only (the same
 // paths, added in the same order: the same bits). Its rays are not reported (no call asked for them).
 static int ahead_materialize(mfx_ctx* c) {
     if (c->film_in_dfilm) return MFX_OK;
-    const AheadBuf& B = c->ab[c->ab_cur];
+    const int b = c->ab_cur;
+    const AheadBuf& B = c->ab[b];
     const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
-    if (c->ab_last_k + 1 == B.n) {
-        HIPCHECK(hipMemcpyAsync(c->d_film, B.film_out, plane, hipMemcpyDeviceToDevice, c->stream));
-    } else {
-        HIPCHECK(hipMemcpyAsync(c->d_film, B.film_in, plane, hipMemcpyDeviceToDevice, c->stream));
-        HIPCHECK(hipMemsetAsync(c->d_counters_aux, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
-        const FrameMode fm{c->d_film, nullptr, 0.0};
-        const int rc = wf_trace(c, c->ab_last_k + 1, B.base, &fm, c->d_counters_aux, c->aux_ev0, c->aux_ev1);
+    const int64_t want = c->ab_last_k + 1;  // the batch's samples the film holds
+    const bool prefix = c->dfilm_buf == b && c->dfilm_n <= want;
+    const int64_t from = want == B.n ? want : (prefix ? c->dfilm_n : 0);
+    for (mfx_ctx* d : devs_of(c)) {
+        HIPCHECK(hipSetDevice(d->device));
+        const AheadBuf& D = d->ab[b];
+        if (want == B.n) {
+            HIPCHECK(hipMemcpyAsync(d->d_film, D.film_out, plane, hipMemcpyDeviceToDevice, d->stream));
+            continue;
+        }
+        if (!prefix) HIPCHECK(hipMemcpyAsync(d->d_film, D.film_in, plane, hipMemcpyDeviceToDevice, d->stream));
+        if (from == want || band_rows(d) == 0) continue;
+        HIPCHECK(hipMemsetAsync(d->d_counters_aux, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), d->stream));
+        const FrameMode fm{d->d_film, nullptr, 0.0};
+        const int rc = wf_trace(d, want - from, B.base + from, &fm, d->d_counters_aux, d->aux_ev0, d->aux_ev1);
         if (rc) return rc;
     }
+    HIPCHECK(hipSetDevice(c->device));
+    c->dfilm_buf = b;
+    c->dfilm_n = want;
     c->film_in_dfilm = true;
     return MFX_OK;
 }
@@ -1302,26 +1400,68 @@ static int ahead_break(mfx_ctx* c) {
     return MFX_OK;
 }
 
-// trace samples [base, base + ab_cap) into B: their frames from film_src / count0 and the film
+// trace samples [base, base + ab_cap) into buffer xi of every device: their frames from the film
+// in buffer src's film_out (src < 0: d_film) with count0 = frameCount before them, and the film
 // after them (enqueued only)
-static int ahead_launch(mfx_ctx* c, AheadBuf& B, int64_t base, const double* film_src, double count0) {
+static int ahead_launch(mfx_ctx* c, int xi, int64_t base, int src, double count0) {
     const size_t plane = 3 * sizeof(double) * (size_t)c->npix;
+    AheadBuf& B = c->ab[xi];
     B.base = base;
     B.n = c->ab_cap;
     B.reported = false;
-    HIPCHECK(hipMemcpyAsync(B.film_in, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHECK(hipMemcpyAsync(B.film_out, film_src, plane, hipMemcpyDeviceToDevice, c->stream));
-    HIPCHECK(hipMemsetAsync(B.counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), c->stream));
-    const FrameMode fm{B.film_out, B.frames, count0};
-    const int rc = wf_trace(c, B.n, base, &fm, B.counters, B.t0, B.t1);
-    if (rc) {
-        B.n = 0;
-        return rc;
+    if (c->dfilm_buf == xi) c->dfilm_buf = -1;  // its film_in changes
+    for (mfx_ctx* d : devs_of(c)) {
+        HIPCHECK(hipSetDevice(d->device));
+        AheadBuf& D = d->ab[xi];
+        const double* film_src = src < 0 ? d->d_film : d->ab[src].film_out;
+        HIPCHECK(hipMemcpyAsync(D.film_in, film_src, plane, hipMemcpyDeviceToDevice, d->stream));
+        HIPCHECK(hipMemcpyAsync(D.film_out, film_src, plane, hipMemcpyDeviceToDevice, d->stream));
+        HIPCHECK(hipMemsetAsync(D.counters, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), d->stream));
+        if (band_rows(d) > 0) {
+            const FrameMode fm{D.film_out, D.frames, count0};
+            const int rc = wf_trace(d, B.n, base, &fm, D.counters, D.t0, D.t1);
+            if (rc) {
+                B.n = 0;
+                (void)hipSetDevice(c->device);
+                return rc;
+            }
+        } else {  // a device with no tile row: no rays in no time
+            HIPCHECK(hipEventRecord(D.t0, d->stream));
+            HIPCHECK(hipEventRecord(D.t1, d->stream));
+        }
+        HIPCHECK(hipEventRecord(D.ready, d->stream));
     }
-    HIPCHECK(hipEventRecord(B.ready, c->stream));
+    HIPCHECK(hipSetDevice(c->device));
     B.expect = 0;
     B.epoch = c->film_epoch;
     B.count0 = count0;
+    if (src < 0) {  // film_in is d_film as it is
+        c->dfilm_buf = xi;
+        c->dfilm_n = 0;
+    }
+    return MFX_OK;
+}
+
+// A device's band rows of a y-major RGBA8 frame (device memory) into the caller's frame (host):
+// one copy of the whole frame for a one-device context; on a device list one strided copy of its
+// whole tile rows (8 rows every band_count * 8) plus the film's partial last tile row if it owns it.
+static int copy_band_rgba(const mfx_ctx* d, uint8_t* dst, const uint8_t* src, hipStream_t st) {
+    const int W = d->host.width, H = d->host.height;
+    const size_t row = 4 * (size_t)W;
+    if (d->band_count == 1) {
+        HIPCHECK(hipMemcpyAsync(dst, src, row * (size_t)H, hipMemcpyDeviceToHost, st));
+        return MFX_OK;
+    }
+    const int full = H / 8, tr = (H + 7) / 8, bi = d->band_index, bc = d->band_count;
+    const int nfull = full > bi ? (full - bi + bc - 1) / bc : 0;
+    if (nfull > 0) {
+        const size_t off = (size_t)8 * bi * row, pitch = (size_t)8 * bc * row;
+        HIPCHECK(hipMemcpy2DAsync(dst + off, pitch, src + off, pitch, 8 * row, (size_t)nfull, hipMemcpyDeviceToHost, st));
+    }
+    if (full < tr && (tr - 1) % bc == bi) {
+        const size_t off = (size_t)8 * full * row;
+        HIPCHECK(hipMemcpyAsync(dst + off, src + off, (size_t)(H - 8 * full) * row, hipMemcpyDeviceToHost, st));
+    }
     return MFX_OK;
 }
 
@@ -1341,36 +1481,55 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
         rc = ahead_materialize(c);
         if (rc) return rc;
         xi = (c->ab_cur >= 0 && c->ab_nbuf == 2) ? 1 - c->ab_cur : 0;
-        rc = ahead_launch(c, c->ab[xi], s, c->d_film, c->frame_count);
+        rc = ahead_launch(c, xi, s, -1, c->frame_count);
     } else if (c->ab[xi].epoch != c->film_epoch || c->ab[xi].expect != s - c->ab[xi].base) {
         rc = ahead_materialize(c);  // held, but the frames assumed another film: a batch from here
-        if (!rc) rc = ahead_launch(c, c->ab[xi], s, c->d_film, c->frame_count);
+        if (!rc) rc = ahead_launch(c, xi, s, -1, c->frame_count);
     }
     if (rc) return rc;
     AheadBuf& X = c->ab[xi];
     const int64_t k = s - X.base;
-    // This call's frame, on the copy stream behind this batch's frames only: it overlaps the
-    // background batch. Everything the call reads back goes there before the next batch is
+    const std::vector<mfx_ctx*> ds = devs_of(c);
+    // This call's frame, on each device's copy stream behind this batch's frames only: it overlaps
+    // the background batch. Everything the call reads back goes there before the next batch is
     // enqueued, and the counters go to page-locked memory: a pageable copy enqueued behind the
     // background batch waited for it (r03b: 6,794 Mrays/s, 73 % of batch; r03c: 8,579, 93 %).
     const size_t frame = 4 * (size_t)c->npix;
-    HIPCHECK(hipStreamWaitEvent(c->copy_stream, X.ready, 0));
-    if (rgba) HIPCHECK(hipMemcpyAsync(rgba, X.frames + k * frame, frame, hipMemcpyDeviceToHost, c->copy_stream));
+    for (mfx_ctx* d : ds) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipStreamWaitEvent(d->copy_stream, d->ab[xi].ready, 0));
+        if (rgba) {
+            const int rb = copy_band_rgba(d, rgba, d->ab[xi].frames + k * frame, d->copy_stream);
+            if (rb) return rb;
+        }
+    }
     for (int q = 0; q < 16; ++q) c->rep_counts[q] = 0.0;
     c->rep_ms = 0.0;
-    if (!X.reported) {  // the first call served from a batch reports its rays and device time
-        HIPCHECK(hipMemcpyAsync(c->h_counters, X.counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long),
-                                hipMemcpyDeviceToHost, c->copy_stream));
-        HIPCHECK(hipStreamSynchronize(c->copy_stream));
-        sum_counters(c->h_counters, c->rep_counts);
-        note_live(c, c->h_counters);
+    if (!X.reported) {  // the first call served from a batch reports its rays (all devices) and device time (the slowest)
+        for (mfx_ctx* d : ds) {
+            HIPCHECK(hipSetDevice(d->device));
+            HIPCHECK(hipMemcpyAsync(d->h_counters, d->ab[xi].counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long),
+                                    hipMemcpyDeviceToHost, d->copy_stream));
+        }
+        float worst = 0.f;
+        for (mfx_ctx* d : ds) {
+            HIPCHECK(hipSetDevice(d->device));
+            HIPCHECK(hipStreamSynchronize(d->copy_stream));
+            sum_counters(d->h_counters, c->rep_counts);
+            note_live(d, d->h_counters);
+            float f = 0.f;
+            HIPCHECK(hipEventElapsedTime(&f, d->ab[xi].t0, d->ab[xi].t1));
+            worst = std::max(worst, f);
+        }
         c->rep_counts[3] = c->rep_counts[0];
-        float f = 0.f;
-        HIPCHECK(hipEventElapsedTime(&f, X.t0, X.t1));
-        c->rep_ms = f;
+        c->rep_ms = worst;
         X.reported = true;
     }
-    HIPCHECK(hipStreamSynchronize(c->copy_stream));
+    for (mfx_ctx* d : ds) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipStreamSynchronize(d->copy_stream));
+    }
+    HIPCHECK(hipSetDevice(c->device));
     c->rep_valid = true;
     c->ab_cur = xi;
     c->ab_last_k = k;
@@ -1383,7 +1542,7 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
         const double count_end = X.count0 + (double)X.n;  // frameCount after X's last call
         // not held, or held but its frames assumed another film: traced (again) from X's film
         if (!(Y.n > 0 && Y.base == X.base + X.n) || Y.epoch != c->film_epoch || Y.count0 != count_end)
-            rc = ahead_launch(c, Y, X.base + X.n, X.film_out, count_end);
+            rc = ahead_launch(c, 1 - xi, X.base + X.n, xi, count_end);
         // This call is served: a background batch that does not fit is not its failure (a NOMEM
         // here would make the caller render the call a second time). Y stays empty; the call
         // that needs it launches it, and falls back to one sample per call if it still fails.
@@ -1399,7 +1558,7 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
 int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     if (c->api_part_count != 1)
-        return fail(MFX_E_STATE, "mfx_sample needs the whole sample set (part_count == 1); "
+        return fail(MFX_E_STATE, "mfx_sample needs the whole film and sample set (part_count == 1); "
                                  "partitioned contexts compose with mfx_trace_accumulate + a reduce");
     int rc = ahead_break(c);  // it moves the sample sequence past held frames
     if (rc) return rc;
@@ -1408,20 +1567,22 @@ int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
     c->next_sample += spp;
-    if (!c->peers.empty() || !c->comms.empty()) {
-        rc = mfx_accum_reduce(c);
-        if (rc) return rc;
-    }
+    rc = mfx_accum_reduce(c);  // a device list: its bands merged into the primary's accumulator
+    if (rc) return rc;
     rc = mfx_accum_read_mean(c, (double)spp, frame);
     if (rc) return rc;
     return mfx_sync(c);
 }
 
+// Without render-ahead (or spp != 1): every device traces its band into its accumulator, adds it
+// to its band of the film and post-processes it (film_post_kernel), and copies its band rows of
+// the RGBA8 frame to the caller's buffer. No device buffer is reduced: each pixel's film lives on
+// the device whose band holds it (mfx_film_mean merges them).
 int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     if (!c) return fail(MFX_E_INVALID, "null context");
     if (c->api_part_count != 1) return fail(MFX_E_STATE, "mfx_render_rgba8 needs part_count == 1");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
-    if (spp == 1 && c->render_ahead > 1 && c->peers.empty() && c->comms.empty()) {
+    if (spp == 1 && c->render_ahead > 1) {
         HIPCHECK(hipSetDevice(c->device));
         const int rc = ahead_render(c, rgba);
         if (rc != MFX_E_NOMEM) return rc;
@@ -1430,7 +1591,7 @@ int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
         c->render_ahead = 0;
         const int rb = ahead_break(c);
         if (rb) return rb;
-        ahead_free(c);
+        ahead_free_all(c);
     }
     int rc = ahead_break(c);
     if (rc) return rc;
@@ -1439,17 +1600,18 @@ int mfx_render_rgba8(mfx_ctx* c, int32_t spp, uint8_t* rgba) {
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
     c->next_sample += spp;
-    if (!c->peers.empty() || !c->comms.empty()) {
-        rc = mfx_accum_reduce(c);
-        if (rc) return rc;
-    }
     c->frame_count += 1.0;  // Film.AddSample: frameCount <- frameCount + 1 (Film.fs:19)
-    HIPCHECK(hipSetDevice(c->device));
-    HIPCHECK(mfx_launch_film_post(c->d_accum, c->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
-                                  rgba ? c->d_rgba : nullptr, c->stream));
-    if (rgba)
-        HIPCHECK(hipMemcpyAsync(rgba, c->d_rgba, 4 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
-    HIPCHECK(hipStreamSynchronize(c->stream));
+    c->dfilm_buf = -1;      // d_film moves on
+    const std::vector<mfx_ctx*> ds = devs_of(c);
+    for (mfx_ctx* d : ds) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(mfx_launch_film_post(d->d_accum, d->d_film, c->host.width, c->host.height, (double)spp, c->frame_count, 1,
+                                      rgba ? d->d_rgba : nullptr, d->stream));
+        if (rgba) {
+            const int rb = copy_band_rgba(d, rgba, d->d_rgba, d->stream);
+            if (rb) return rb;
+        }
+    }
     return mfx_sync(c);
 }
 
@@ -1474,26 +1636,36 @@ int mfx_stats(mfx_ctx* c, double* rays, double* seconds) {
 
 int mfx_reset(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
-    HIPCHECK(hipSetDevice(c->device));
     // stream-ordered after anything that reads the film (no wait for a background batch)
-    HIPCHECK(hipMemsetAsync(c->d_film, 0, 3 * sizeof(double) * (size_t)c->npix, c->stream));
+    for (mfx_ctx* d : devs_of(c)) {
+        HIPCHECK(hipSetDevice(d->device));
+        HIPCHECK(hipMemsetAsync(d->d_film, 0, 3 * sizeof(double) * (size_t)d->npix, d->stream));
+    }
+    HIPCHECK(hipSetDevice(c->device));
     c->frame_count = 0.0;
     c->film_in_dfilm = true;
+    c->dfilm_buf = -1;
     if (c->ab_nbuf) {
         c->film_epoch += 1;
         c->ab_cur = -1;
-    } else {
-        HIPCHECK(hipStreamSynchronize(c->stream));
+        return MFX_OK;
     }
-    return MFX_OK;
+    return mfx_sync(c);
 }
 
 int mfx_film_mean(mfx_ctx* c, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     HIPCHECK(hipSetDevice(c->device));
-    const int rc = ahead_materialize(c);
+    int rc = ahead_materialize(c);
     if (rc) return rc;
-    HIPCHECK(mfx_launch_film_mean(c->d_film, c->npix, c->frame_count, c->d_frame, c->stream));
+    const double* film = c->d_film;
+    if (!c->peers.empty() || !c->comms.empty()) {  // a device list: the devices' bands of the film, merged
+        if (!c->d_merge) HIPCHECK(hipMalloc((void**)&c->d_merge, 3 * sizeof(double) * (size_t)c->npix));
+        rc = reduce_planes(c, [](mfx_ctx* d) { return d->d_film; }, c->d_merge, "mfx_film_mean");
+        if (rc) return rc;
+        film = c->d_merge;
+    }
+    HIPCHECK(mfx_launch_film_mean(film, c->npix, c->frame_count, c->d_frame, c->stream));
     return host_readback(c, frame, c->d_frame, 4 * sizeof(double) * (size_t)c->npix, c->stream);
 }
 

@@ -23,6 +23,7 @@ struct TraceParams {
     int64_t sample_base;             // first global sample index of this call
     int64_t nsamples;                // samples this context renders per pixel in this call
     int32_t part_index, part_count;  // global sample = sample_base + part_index + s * part_count
+    int32_t band_index, band_count, band_rows;  // image partition: tile rows band_index + k * band_count (WfParams)
     int32_t width, height, max_depth;
     int32_t stack_size;              // LDS traversal stack entries per lane
     int32_t chunk;                   // path indices a wave takes per atomic

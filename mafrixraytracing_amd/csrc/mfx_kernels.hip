@@ -41,7 +41,7 @@ __global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
     const int W = P.width, H = P.height;
     const int64_t npix = (int64_t)W * H;
     const int tiles_x = (W + 7) >> 3;
-    const int64_t per_sample = (int64_t)tiles_x * ((H + 7) >> 3) * 64;
+    const int64_t per_sample = (int64_t)tiles_x * P.band_rows * 64;  // the band's tile rows (image partition)
     const int64_t total = per_sample * P.nsamples;
 
     // path state. A vertex's direct term a_v and col c_v go to this lane's scratch column and are
@@ -90,7 +90,7 @@ __global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
                 const int64_t tile = q >> 6;
                 const int within = (int)(q & 63);
                 const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-                const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
+                const int y = (P.band_index + (int)(tile / tiles_x) * P.band_count) * 8 + (within >> 3);
                 if (x < W && y < H) {
                     // PixelIntegrator.Sample (Integrators.fs:166-169) + PinholeCamera.GetRay (Camera.fs:134-139)
                     pixel = (int64_t)x * H + y;  // Color[w,h] x-major

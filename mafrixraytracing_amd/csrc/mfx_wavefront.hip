@@ -280,19 +280,22 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 }
 
 // Path index of this generation -> (sample, 8x8 pixel tile, pixel), sample-major and
-// tile-coherent. False for the padding indices of edge tiles (no path).
+// tile-coherent. False for the padding indices of edge tiles (no path). A banded
+// trace (image partition) numbers only its own tile rows: its k-th tile row is film tile row
+// band_index + k * band_count, so pixels, keys and samples are the whole-film trace's.
 __device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x, int& y, int64_t& smp) {
     // p = path_base + s: the 64-bit split of path_base is done once per generation on the host
     // (base_smp, base_q), so only 32-bit divisions remain here (base_q + s < 2^32)
     const unsigned tiles_x = (unsigned)(P.width + 7) >> 3;
-    const unsigned per_sample = tiles_x * (((unsigned)P.height + 7) >> 3) * 64;  // < 2^31 (film limit)
+    const unsigned per_sample = tiles_x * (unsigned)P.band_rows * 64;  // < 2^31 (film limit)
     const unsigned qs = (unsigned)P.base_q + (unsigned)(p - P.path_base);
     const unsigned ds = qs / per_sample;
     smp = P.base_smp + ds;
     const unsigned q = qs - ds * per_sample;
     const unsigned tile = q >> 6, within = q & 63;
-    const unsigned ty = tile / tiles_x;
-    x = (int)((tile - ty * tiles_x) * 8 + (within & 7));
+    const unsigned tyl = tile / tiles_x;
+    const unsigned ty = (unsigned)P.band_index + tyl * (unsigned)P.band_count;
+    x = (int)((tile - tyl * tiles_x) * 8 + (within & 7));
     y = (int)(ty * 8 + (within >> 3));
     return x < P.width && y < P.height;
 }
@@ -1076,13 +1079,13 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     for (int i = threadIdx.x; i < 3 * nm; i += blockDim.x) alb[i] = P.albedo[i];
     __syncthreads();
     const int tiles_x = (P.width + 7) >> 3;
-    const int64_t per_sample = (int64_t)tiles_x * ((P.height + 7) >> 3) * 64;
+    const int64_t per_sample = (int64_t)tiles_x * P.band_rows * 64;
     const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (q >= per_sample) return;
     const int64_t tile = q >> 6;
     const int within = (int)(q & 63);
     const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-    const int y = (int)(tile / tiles_x) * 8 + (within >> 3);
+    const int y = (P.band_index + (int)(tile / tiles_x) * P.band_count) * 8 + (within >> 3);  // the band's film row
     if (x >= P.width || y >= P.height) return;
     const int64_t npix = (int64_t)P.width * P.height;
     const int64_t pixel = (int64_t)x * P.height + y;
@@ -1274,7 +1277,7 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
 }
 
 hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st) {
-    const int64_t per_sample = (int64_t)((P.width + 7) >> 3) * ((P.height + 7) >> 3) * 64;
+    const int64_t per_sample = (int64_t)((P.width + 7) >> 3) * P.band_rows * 64;
     if (P.film) hipLaunchKernelGGL(k_resolve<true>, dim3((unsigned)((per_sample + 255) / 256)), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(k_resolve<false>, dim3((unsigned)((per_sample + 255) / 256)), dim3(256), 0, st, P);
     return hipGetLastError();

@@ -18,7 +18,8 @@ tests/golden/ref_fsharp_decls.json (scripts/extract_ref_decls.py, generated from
    shim's constructor arity and members, Scene's new constructor used by Library.fs;
 6. the blittable structs have the C header's field sequence (via the ctypes mirror abi.py,
    whose offsets tests/test_abi.py checks against the header), and every `extern` names a
-   declared C entry point with its parameter count.
+   declared C entry point with its parameter count; the shim's MFX_ABI_VERSION is the header's and
+   it is checked (mfx_abi_version) before the first mfx_create.
 
 Exit status 0 and "OK" when everything resolves; otherwise one line per problem.
 """
@@ -351,6 +352,22 @@ class Checker:
             nf = len([p for p in params.split(",") if p.strip()])
             if nc != nf:
                 self.err(f"Native.fs: extern {name} has {nf} parameters, the header {nc}")
+        # the ABI version: the shim's constant is the header's, and the constructor checks the loaded
+        # library against it before it creates a context (a stale .so fails loudly, not on a layout)
+        hv = re.search(r"#define\s+MFX_ABI_VERSION\s+(\d+)", hdr)
+        fv = re.search(r"let\s+MFX_ABI_VERSION\s*=\s*(\d+)", self.native_text)
+        if not fv:
+            self.err("Native.fs: no MFX_ABI_VERSION constant")
+        elif hv and fv.group(1) != hv.group(1):
+            self.err(f"Native.fs: MFX_ABI_VERSION {fv.group(1)} != the header's ABI version {hv.group(1)}")
+        chk = re.search(r"let\s+checkAbi\s*\(\)\s*=(.*?)(?=\n\S)", self.native_text, re.S)
+        if not chk or "Api.mfx_abi_version()" not in chk.group(1) or \
+                not re.search(r"\bv\s*<>\s*MFX_ABI_VERSION\b|\bMFX_ABI_VERSION\s*<>\s*v\b", chk.group(1)):
+            self.err("Native.fs: checkAbi must compare Api.mfx_abi_version() with MFX_ABI_VERSION")
+        call = re.search(r"^\s+checkAbi \(\)\s*$", self.native_text, re.M)
+        cc = self.native_text.find("Api.mfx_create(")
+        if not call or cc < 0 or call.start() > cc:
+            self.err("Native.fs: the ABI version check must run before mfx_create")
 
     def run(self):
         self.check_diffs()

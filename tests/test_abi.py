@@ -63,7 +63,7 @@ def test_version_errors_and_no_cpu_fallback():
     import ctypes as C
     from mafrixraytracing_amd.abi import MfxOptions, load_library
     lib = load_library()
-    assert lib.mfx_abi_version() == 5
+    assert lib.mfx_abi_version() == 6
     assert lib.mfx_device_count() >= 0
     h = C.c_void_p()
     opt = MfxOptions(seed=1, device=0, flags=0, part_index=0, part_count=1)

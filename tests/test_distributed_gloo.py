@@ -1,8 +1,9 @@
-"""Multi-rank composition on CPU: world_size 2 over gloo. Each rank renders its
-sample partition into an FP64 accumulator and the partitions are reduced to rank 0; the result
-must equal the single-rank image. The ranks run `native_partitioned_render` — the function
-bench.py's multi-process path runs — over a stand-in context whose trace is the CPU oracle (the
-container has no GPU), so the clear / trace / sync / reduce sequence tested is the bench's."""
+"""Multi-rank composition on CPU: world_size 2 and 3 over gloo. Each rank renders its
+partition into an FP64 accumulator — its tile rows (the image partition bench.py runs: RowGather to
+rank 0) or its samples (a sum-reduce) — and rank 0's merged accumulator must equal the single-rank
+image (the rows: bit for bit). The ranks run `native_partitioned_render` — the function bench.py's
+multi-process path runs — over a stand-in context whose trace is the CPU oracle (the container has
+no GPU), so the clear / trace / sync / exchange sequence tested is the bench's."""
 import os
 import socket
 import sys
@@ -28,8 +29,8 @@ class OracleContext:
     this rank's partition of the frame (global samples s = base + part_index mod part_count,
     mfx_trace_accumulate's contract) to the attached accumulator, with the CPU oracle."""
 
-    def __init__(self, oscene, acc, part_index, part_count):
-        self.o, self.acc, self.pi, self.pc = oscene, acc, part_index, part_count
+    def __init__(self, oscene, acc, part_index, part_count, rows=False):
+        self.o, self.acc, self.pi, self.pc, self.rows = oscene, acc, part_index, part_count, rows
         self.calls = []
 
     def accum_attach(self, ptr, nbytes):
@@ -45,20 +46,26 @@ class OracleContext:
 
     def trace_accumulate(self, spp, base):
         import torch
-        from mafrixraytracing_amd.distributed import partition_samples
-        s = partition_samples(spp, self.pi, self.pc) + base
-        px, py, ss = np.meshgrid(np.arange(W), np.arange(H), s, indexing="ij")
+        from mafrixraytracing_amd.distributed import partition_rows, partition_samples
+        if self.rows:  # MFX_F_ROW_PARTITION: every sample of this rank's tile rows
+            s = np.arange(spp, dtype=np.int64) + base
+            ys = partition_rows(H, self.pi, self.pc)
+        else:
+            s = partition_samples(spp, self.pi, self.pc) + base
+            ys = np.arange(H)
+        px, py, ss = np.meshgrid(np.arange(W), ys, s, indexing="ij")
         out, _ = self.o.paths(px.ravel(), py.ravel(), ss.ravel(), SEED, nthreads=2)
         pix = (px.ravel() * H + py.ravel())
         npix = W * H
         acc_np = np.zeros(3 * npix)
+        # per pixel in sample order (the kernels' k_resolve order): meshgrid's last axis is the sample
         for c in range(3):
             np.add.at(acc_np, c * npix + pix, out[:, c])
         self.acc += torch.from_numpy(acc_np)
         self.calls.append("trace")
 
 
-def _worker(rank, world, port, outdir):
+def _worker(rank, world, port, outdir, rows):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch
@@ -66,30 +73,51 @@ def _worker(rank, world, port, outdir):
 
     import pyoracle
     from conftest import scene
-    from mafrixraytracing_amd.distributed import native_partitioned_render
+    from mafrixraytracing_amd.distributed import RowGather, native_partitioned_render
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     a = scene("spot", W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64)
-    ctx = OracleContext(pyoracle.OracleScene(a), acc, rank, world)
-    native_partitioned_render(ctx, acc, rank, world).frame(SPP, sample_base=7)
-    assert ctx.calls == ["attach", "clear", "trace", "sync"], ctx.calls
-    if rank == 0:
-        np.save(os.path.join(outdir, "reduced.npy"), acc.numpy())
+    ctx = OracleContext(pyoracle.OracleScene(a), acc, rank, world, rows=rows)
+    ex = RowGather(acc, W, H, rank, world) if rows else None
+    pr = native_partitioned_render(ctx, acc, rank, world, exchange=ex)
+    for k, base in enumerate((7, 12)):  # two frames: the gather buffers are reused
+        pr.frame(SPP, sample_base=base)
+        if rank == 0:
+            np.save(os.path.join(outdir, f"merged{k}.npy"), acc.numpy())
+    assert ctx.calls == ["attach"] + ["clear", "trace", "sync"] * 2, ctx.calls
     dist.barrier()
     dist.destroy_process_group()
 
 
-def test_two_rank_partition_reduce_equals_single_rank(oracle, tmp_path):
+@pytest.mark.parametrize("world,rows", [(2, False), (2, True), (3, True)])
+def test_ranks_merge_to_the_single_rank_image(oracle, tmp_path, world, rows):
+    """rows: the image partition with RowGather (12 rows = 2 tile rows, the second partial: with 3
+    ranks one rank owns none) — rank 0's accumulator is the single-rank image bit for bit. Else the
+    sample partition with a sum-reduce, within FP64 summation order."""
     import torch.multiprocessing as mp
     port = _free_port()
-    mp.start_processes(_worker, args=(2, port, str(tmp_path)), nprocs=2, join=True, start_method="spawn")
-    acc = np.load(tmp_path / "reduced.npy")
+    mp.start_processes(_worker, args=(world, port, str(tmp_path), rows), nprocs=world, join=True, start_method="spawn")
     from conftest import scene
-    ref = oracle.OracleScene(scene("spot", W, H)).sample(SPP, SEED, sample_base=7)
+    o = oracle.OracleScene(scene("spot", W, H))
     npix = W * H
-    got = np.stack([acc[c * npix:(c + 1) * npix] for c in range(3)], 1) / SPP
-    assert np.abs(got - ref[:, :3]).max() < 1e-12
+    for k, base in enumerate((7, 12)):
+        acc = np.load(tmp_path / f"merged{k}.npy")
+        ref = o.sample(SPP, SEED, sample_base=base)
+        got = np.stack([acc[c * npix:(c + 1) * npix] for c in range(3)], 1) / SPP
+        if rows:
+            assert np.array_equal(got, ref[:, :3]), k
+        assert np.abs(got - ref[:, :3]).max() < 1e-12, k
+
+
+def test_partition_rows_cover_every_row_once():
+    from mafrixraytracing_amd.distributed import partition_rows
+    for h in (1, 8, 12, 37, 1080):
+        for world in (1, 2, 3, 8):
+            allr = np.concatenate([partition_rows(h, r, world) for r in range(world)])
+            assert sorted(allr.tolist()) == list(range(h))
+            for r in range(world):
+                assert all((y // 8) % world == r for y in partition_rows(h, r, world))
 
 
 def test_partition_covers_every_sample_once():
@@ -104,7 +132,6 @@ def test_step_spp_weak_and_strong():
     from mafrixraytracing_amd.distributed import step_spp
     assert step_spp(64, 8, "weak") == 512 and step_spp(64, 1, "weak") == 64
     assert step_spp(64, 8, "strong") == 64
-    with pytest.raises(ValueError):
-        step_spp(4, 8, "strong")
+    assert step_spp(4, 8, "strong") == 4  # the image partition splits rows, not samples
     with pytest.raises(ValueError):
         step_spp(64, 2, "linear")

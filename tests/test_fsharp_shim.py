@@ -54,6 +54,10 @@ def _mutated(tmp_path, fname, old, new):
     # a struct whose fields do not follow the C layout
     ("Native.fs", "    val mutable ndevices : int32\n    val mutable renderAhead : int32\n",
      "    val mutable ndevices : int32\n", "C layout"),
+    # a binding written for another ABI, or one that never checks the loaded library's
+    ("Native.fs", "let MFX_ABI_VERSION = 6", "let MFX_ABI_VERSION = 5", "ABI version"),
+    ("Native.fs", "        checkAbi ()\n", "\n", "version check"),
+    ("Native.fs", "    if v <> MFX_ABI_VERSION then", "    if v < 0 then", "checkAbi must compare"),
 ])
 def test_checker_catches_binding_errors(tmp_path, fname, old, new, expect):
     if fname.endswith(".diff") and "Compile" in old:

@@ -68,3 +68,53 @@ def test_full_size_partitions_sum_to_whole(gpu):
             ct += ctx.ray_counts()[:3]
     assert np.array_equal(ct, cw)
     assert np.abs(total[:, :3] - whole[:, :3]).max() <= 1e-12 * max(1.0, np.abs(whole).max())
+
+
+@pytest.mark.parametrize("name", ["two_spheres_plane", "cornell"])
+def test_c1_config_matches_oracle(gpu, oracle, name):
+    """BASELINE.json configs[0] at its own size: Scene.xml's two spheres + plane (and the Cornell
+    fallback scene), 256x256, 4 spp, through mfx_sample — the Color[w,h] image, the ray counters and
+    the first Scene.Render frames against the oracle, bit for bit."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, 256, 256)
+    o = oracle.OracleScene(a)
+    ref, st = o.sample(4, SEED, sample_base=0, with_stats=True)
+    with NativeContext(a, seed=SEED) as ctx:
+        img = ctx.sample(4)
+        counts = ctx.ray_counts()
+    assert tuple(counts[:3]) == tuple(st[:3]), (counts[:3], st[:3])
+    assert np.array_equal(img, ref), np.abs(img[:, :3] - ref[:, :3]).max()
+
+
+def test_full_size_row_partition_merges_exactly(gpu):
+    """C2 at 1920x1080, 8 spp, split over 8 MFX_F_ROW_PARTITION ranks (the multi-GPU image
+    partition, one rank per GPU): the ranks' accumulators sum to the whole-film context's bit for
+    bit, and their ray counts to its counts (135 tile rows: 17 or 16 per rank)."""
+    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot")
+    spp, P = 8, 8
+    with NativeContext(a, seed=SEED) as ctx:
+        ctx.trace_accumulate(spp, 3)
+        whole = ctx.accum_read_mean(1.0)
+        cw = ctx.ray_counts()[:3].copy()
+    total = np.zeros_like(whole)
+    ct = np.zeros(3)
+    for p in range(P):
+        with NativeContext(a, seed=SEED, flags=MFX_F_ROW_PARTITION, part_index=p, part_count=P) as ctx:
+            ctx.trace_accumulate(spp, 3)
+            total[:, :3] += ctx.accum_read_mean(1.0)[:, :3]
+            ct += ctx.ray_counts()[:3]
+    assert np.array_equal(ct, cw)
+    assert np.array_equal(total[:, :3], whole[:, :3])
+
+
+def test_full_size_render_ahead_device_list(gpu):
+    """Scene.Render at C2's film size on a two-device list with render-ahead (K = 4): 10 frames
+    byte-identical to the one-device context's, then the film."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot")
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, devices=[0, 0], render_ahead=4) as c2:
+        for k in range(10):
+            assert np.array_equal(c1.render_rgba8(1), c2.render_rgba8(1)), k
+        assert np.array_equal(c1.film_mean(), c2.film_mean())

@@ -1,11 +1,14 @@
 """Multi-device contexts through the C ABI (mfx_options.devices).
 
-One context drives a device list from one process: device g renders sample sub-partition g of G
-on its own stream, and the library's own reduce sums the FP64 accumulators into devices[0]:
-- a list of distinct devices reduces with RCCL (a communicator the library creates with
-  ncclCommInitAll); devices=[0] runs that code path on the 1-GPU box (a 1-rank reduce);
-- a list that repeats a device (devices=[0,0]) adds the peers' accumulators in device order.
-The 8-GPU case is the driver's; every bit of bookkeeping it uses is exercised here with G = 1-3.
+One context drives a device list from one process by an image partition: device g of G traces the
+film's 8-pixel tile rows r % G == g (every sample) on its own stream, so every per-pixel operation
+runs on one device in the one-device order and every output is the one-device context's, bit for
+bit. FP64 buffers (mfx_sample's accumulator, mfx_film_mean's film) merge on devices[0]:
+- a list of distinct devices with RCCL (a communicator the library creates with ncclCommInitAll);
+  devices=[0] runs that code path on the 1-GPU box (a 1-rank reduce);
+- a list that repeats a device (devices=[0,0]) by device-ordered adds.
+A pixel is +0.0 on every device but its own, so either sum is an exact merge. The 8-GPU case is the
+driver's; every bit of bookkeeping it uses is exercised here with G = 1-3.
 """
 import ctypes as C
 
@@ -30,36 +33,60 @@ def test_single_device_list_is_bit_identical(gpu):
 
 
 @pytest.mark.parametrize("G", [2, 3])
-def test_repeated_device_list_sums_partitions_in_device_order(gpu, oracle, G):
-    """devices=[0]*G: device g renders partition g of G; the primary's accumulator is
-    (a_0 + a_1) + a_2 ..., bit for bit the partitioned single-device contexts summed in that order;
-    ray counts equal the whole sample set's; the image matches the oracle."""
+def test_repeated_device_list_partitions_rows_exactly(gpu, oracle, G):
+    """devices=[0]*G: device g traces tile rows g mod G; after the merge the primary's accumulator is
+    the one-device context's bit for bit, and so are the Sample image and the ray counters; the
+    image matches the oracle. cube_cornell at 48x27: 4 tile rows, the last one partial."""
     from mafrixraytracing_amd.native import NativeContext
     a = scene("cube_cornell", 48, 27)
     spp = 7
-    parts = []
-    for g in range(G):
-        with NativeContext(a, seed=SEED, part_index=g, part_count=G) as ctx:
-            ctx.accum_clear()
-            ctx.trace_accumulate(spp, 0)
-            parts.append(ctx.accum_read_mean(1.0))
-    want = parts[0].copy()
-    for p in parts[1:]:
-        want[:, :3] = want[:, :3] + p[:, :3]
+    with NativeContext(a, seed=SEED) as s:
+        s.accum_clear()
+        s.trace_accumulate(spp, 0)
+        want = s.accum_read_mean(1.0)
+        want_counts = s.ray_counts()
     with NativeContext(a, seed=SEED, devices=[0] * G) as m:
         m.accum_clear()
         m.trace_accumulate(spp, 0)
+        counts = m.ray_counts()
         m.accum_reduce()
         got = m.accum_read_mean(1.0)
-        counts = m.ray_counts()
         img = m.sample(spp)  # the same frame through mfx_sample (trace_accumulate does not advance it)
     assert np.array_equal(got, want)
-    with NativeContext(a, seed=SEED) as s:
-        s.sample(spp)
-        assert np.array_equal(counts[:4], s.ray_counts()[:4])
+    assert np.array_equal(counts[:4], want_counts[:4])
     ref = oracle.OracleScene(a).sample(spp, SEED, sample_base=0)
-    diff = np.abs(img[:, :3] - ref[:, :3])
-    assert np.sqrt((diff ** 2).mean(axis=0)).max() <= 1e-4 and diff.max() <= 1e-12
+    assert np.array_equal(img, ref)
+
+
+@pytest.mark.parametrize("P", [2, 3])
+def test_row_partition_ranks_merge_exactly(gpu, P):
+    """MFX_F_ROW_PARTITION (the multi-process image partition): P one-device contexts, rank p traces
+    every sample of tile rows p mod P; each rank's accumulator is +0.0 outside its rows, and the sum
+    over the ranks is the whole-film context's accumulator bit for bit (so is the ray total)."""
+    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.native import NativeContext
+    w, h = 50, 29  # 4 tile rows, the last one partial; 7 tile columns, the last one partial
+    a = scene("spot", w, h)
+    spp = 5
+    with NativeContext(a, seed=SEED) as s:
+        s.trace_accumulate(spp, 11)
+        want = s.accum_read_mean(1.0)
+        want_rays = s.ray_counts()[:4]
+    total = np.zeros_like(want)
+    rays = np.zeros(4)
+    rows = np.arange(h) // 8
+    for p in range(P):
+        with NativeContext(a, seed=SEED, flags=MFX_F_ROW_PARTITION, part_index=p, part_count=P) as c:
+            c.trace_accumulate(spp, 11)
+            part = c.accum_read_mean(1.0)
+            rays += c.ray_counts()[:4]
+        own = np.tile(rows % P == p, w)  # x-major pixels: pixel = x * h + y
+        assert not np.any(part[~own, :3]), p
+        assert np.array_equal(part[own], want[own]), p
+        total[:, :3] += part[:, :3]
+    total[:, 3] = want[:, 3]
+    assert np.array_equal(total, want)
+    assert np.array_equal(rays, want_rays)
 
 
 def test_repeated_device_reduce_orders_later_work(gpu):
@@ -82,16 +109,21 @@ def test_repeated_device_reduce_orders_later_work(gpu):
     assert np.array_equal(out[0], out[1])
 
 
-def test_repeated_device_render_and_stats(gpu, oracle):
-    """Scene.Render on a 2-device context: the film on devices[0] holds the reduced frames;
-    mfx_stats sums rays over the devices."""
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+def test_repeated_device_render_and_stats(gpu, devices):
+    """Scene.Render (no render-ahead) on a device list: each device adds its rows to its band of the
+    film and copies its rows of the RGBA8 frame; frames, the merged film and the ray counts equal the
+    one-device context's, bit for bit, across spp != 1 calls and a reset."""
     from mafrixraytracing_amd.native import NativeContext
     a = scene("two_spheres_plane", 40, 30)
-    with NativeContext(a, seed=SEED, devices=[0, 0]) as m, NativeContext(a, seed=SEED) as s:
-        for _ in range(3):
-            m.render_rgba8(2)
-            s.render_rgba8(2)
-        assert np.abs(m.film_mean() - s.film_mean()).max() <= 1e-12
+    with NativeContext(a, seed=SEED, devices=devices) as m, NativeContext(a, seed=SEED) as s:
+        for k in range(5):
+            spp = 1 + (k % 3)
+            assert np.array_equal(m.render_rgba8(spp), s.render_rgba8(spp)), k
+            if k == 2:
+                m.reset()
+                s.reset()
+        assert np.array_equal(m.film_mean(), s.film_mean())
         rays, sec = m.stats()
         n = s.ray_counts()
         assert rays == n[0] + n[1] + n[2] and sec > 0

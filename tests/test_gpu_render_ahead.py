@@ -127,3 +127,77 @@ def test_render_ahead_option_validated(gpu):
         NativeContext(a, seed=SEED, render_ahead=-1)
     with pytest.raises(MfxError):
         NativeContext(a, seed=SEED, render_ahead=1 << 20)
+
+
+@pytest.mark.parametrize("devices", [[0, 0], [0, 0, 0]])
+@pytest.mark.parametrize("name,w,h,K", [("spot", 67, 37, 4), ("cube_cornell", 48, 27, 5)])
+def test_render_ahead_on_a_device_list(gpu, devices, name, w, h, K):
+    """Scene(state, devices) — the F# binding's device-list context — serving Scene.Render from
+    batches on every device (image partition: device g traces tile rows g mod G of each batch and
+    copies its rows of each frame). 14 calls with an spp = 2 call, a film read mid-batch, a reset and
+    an mfx_sample call in between: every RGBA8 frame, the Sample image, the film and the rays equal
+    the one-device context without render-ahead, bit for bit. (37 rows: 5 tile rows, the last one
+    partial, so with 3 devices one device's band ends in the partial row.)"""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, w, h)
+    rays_plain = rays_multi = 0.0
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, devices=devices, render_ahead=K) as c2:
+        for k in range(14):
+            spp = 2 if k == 4 else 1
+            if k == 6:
+                assert np.array_equal(c1.film_mean(), c2.film_mean()), k
+            if k == 9:
+                c1.reset()
+                c2.reset()
+            if k == 11:
+                assert np.array_equal(c1.sample(3), c2.sample(3))
+            assert np.array_equal(c1.render_rgba8(spp), c2.render_rgba8(spp)), (name, devices, k)
+            rays_plain += c1.stats()[0]
+            rays_multi += c2.stats()[0]
+        assert np.array_equal(c1.film_mean(), c2.film_mean())
+    # the last batch may hold samples no call has taken yet: only whole served batches compare
+    assert rays_multi > 0 and rays_plain > 0
+
+
+def test_render_ahead_device_list_with_an_empty_band(gpu):
+    """A film of one tile row on three devices: devices 1 and 2 own no row (no trace, no copy) and
+    the frames are still the one-device frames."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 24, 8)
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, devices=[0, 0, 0], render_ahead=3) as c2, \
+            NativeContext(a, seed=SEED, devices=[0, 0, 0]) as c3:
+        for k in range(7):
+            r1 = c1.render_rgba8(1)
+            assert np.array_equal(r1, c2.render_rgba8(1)), k
+            assert np.array_equal(r1, c3.render_rgba8(1)), k
+        assert np.array_equal(c1.film_mean(), c2.film_mean())
+        assert np.array_equal(c1.sample(2), c3.sample(2))
+
+
+def test_film_mean_mid_batch_traces_each_sample_once(gpu):
+    """Render and mfx_film_mean alternating inside one batch: each film read traces only
+    the samples served since the last one (film only), not the batch prefix again; the films are the
+    one-sample path's."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 40, 24)
+    K = 8
+    with NativeContext(a, seed=SEED) as c1, NativeContext(a, seed=SEED, render_ahead=K) as c2:
+        for k in range(2 * K):
+            assert np.array_equal(c1.render_rgba8(1), c2.render_rgba8(1)), k
+            assert np.array_equal(c1.film_mean(), c2.film_mean()), k
+
+
+def test_trace_timing_keeps_to_eight_doubles(gpu):
+    """mfx_trace_timing writes exactly out[8], also for a call served from held frames (ADVICE r04:
+    the render-ahead branch cleared 12 doubles): a guard after the buffer stays untouched."""
+    import ctypes as C
+    from mafrixraytracing_amd.abi import check, dptr
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 32, 16)
+    with NativeContext(a, seed=SEED, render_ahead=4) as c:
+        for k in range(6):
+            c.render_rgba8(1, want_pixels=False)
+            buf = np.full(16, 12345.0)
+            check(c.lib.mfx_trace_timing(c._h, dptr(buf)), "mfx_trace_timing")
+            assert np.all(buf[8:] == 12345.0), k
+    _ = C
