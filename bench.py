@@ -231,62 +231,69 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
                         "to pageable host memory, synchronize"}
 
 
-def xgmi_reduce_ms(nbytes, n):
-    """Modeled N-rank sum-reduce of an nbytes buffer to one rank: a ring reduce-scatter then a gather
-    to the root over one xGMI link per hop, each moving (N - 1) / N of the buffer; RCCL's rings over
-    several of the 7 links only make it faster, so this bounds the transfer from above."""
-    return 2.0 * nbytes * (n - 1) / n / (XGMI_LINK_GBS * 1e9) * 1e3
-
-
-def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=3, flags=0):
-    """One GPU's share of a strong-scaled job, measured on this GPU: the config's spp split over N
-    GPUs is spp / N samples per GPU per step (C2: 32 / 16 / 8). Timed per N: the share's trace
-    (clear + trace + sync, the step's fixed per-generation costs included), and the library's RCCL
-    reduce of the FP64 accumulator on a devices=[0] context (a 1-rank communicator: its launch and
-    local cost). The N-rank reduce's xGMI transfer is modeled (xgmi_reduce_ms). predicted_efficiency
-    = (t_1GPU / N) / (t_share + t_reduce_modeled), the reduce not overlapped; with the bench's
-    pipelined frames (frame k's reduce under frame k + 1's trace) it is (t_1GPU / N) / max(t_share,
-    t_reduce_modeled): predicted_efficiency_pipelined."""
+def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=2, flags=0):
+    """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
+    measured on this GPU: rank r traces all `spp` samples of the film's tile rows r mod N
+    (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
+    fixed per-generation costs included); the slowest rank is the step's trace. The exchange is
+    RowGather: its pack (the largest rank's rows) and rank 0's unpack of the others' are timed here
+    (torch index kernels on this accumulator); the transfer is modeled as the largest sending rank's
+    bytes over one xGMI link (every rank sends to rank 0 over its own link, in parallel).
+    predicted_efficiency = (t_1GPU / N) / (t_slowest_rank + t_pack + t_transfer + t_unpack): the
+    exchange not overlapped (the bench overlaps it with the next frame's trace; not counted here)."""
+    import torch
+    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.distributed import RowGather
     from mafrixraytracing_amd.native import NativeContext
-    out = {}
-    with NativeContext(arrays, seed=seed, devices=[0], flags=flags) as rc:
-        for _ in range(3):
-            rc.accum_reduce()
-        rc.sync()
+    W, H = arrays.width, arrays.height
+    acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda")
+
+    def timed(fn, reps=20):
+        fn()
+        torch.cuda.synchronize()
         t0 = time.perf_counter()
-        n_red = 20
-        for _ in range(n_red):
-            rc.accum_reduce()
-        rc.sync()
-        t_red = (time.perf_counter() - t0) / n_red * 1e3
-    acc_bytes = 3 * 8 * arrays.width * arrays.height
-    with NativeContext(arrays, seed=seed, flags=flags) as ctx:
-        for n in (2, 4, 8):
-            share = spp // n
-            if share < 1:
-                continue
-            ctx.accum_clear()
-            ctx.trace_accumulate(share, 0)
-            ctx.sync()
-            rays, t0 = 0.0, time.perf_counter()
-            for k in range(steps):
-                ctx.accum_clear()
-                ctx.trace_accumulate(share, (k + 1) * spp)
+        for _ in range(reps):
+            fn()
+        torch.cuda.synchronize()
+        return (time.perf_counter() - t0) / reps * 1e3
+
+    out = {}
+    for n in (2, 4, 8):
+        rank_ms, rank_rays = [], []
+        for r in range(n):
+            with NativeContext(arrays, seed=seed, flags=flags | MFX_F_ROW_PARTITION, part_index=r, part_count=n) as ctx:
+                ctx.trace_accumulate(spp, 0)  # the pool's first allocation, untimed
                 ctx.sync()
-                c = ctx.ray_counts()
-                rays += c[0] + c[1] + c[2]
-            t = (time.perf_counter() - t0) / steps * 1e3
-            t_x = max(t_red, xgmi_reduce_ms(acc_bytes, n))
-            out[str(n)] = {"spp_per_gpu": share, "ms_per_step": round(t, 3),
-                           "mrays_per_s_per_gpu": round(rays / steps / (t / 1e3) / 1e6, 2),
-                           "vs_full_step_rate": round(rays / steps / (t / 1e3) / 1e6 / value_1gpu, 4),
-                           "reduce_ms_modeled": round(t_x, 4),
-                           "predicted_efficiency": round((ms_1gpu / n) / (t + t_x), 4),
-                           "predicted_efficiency_pipelined": round((ms_1gpu / n) / max(t, t_x), 4)}
-    return {"reduce_ms_1rank": round(t_red, 4), "shares": out,
-            "note": "per-GPU share of --scaling strong at N GPUs, measured on one GPU; reduce_ms_1rank is the "
-                    "devices=[0] RCCL reduce (no xGMI transfer); reduce_ms_modeled = max(that, a one-link ring "
-                    f"reduce of the {acc_bytes / 1e6:.1f} MB FP64 accumulator at {XGMI_LINK_GBS:.0f} GB/s)"}
+                rays, t0 = 0.0, time.perf_counter()
+                for k in range(steps):
+                    ctx.accum_clear()
+                    ctx.trace_accumulate(spp, (k + 1) * spp)
+                    ctx.sync()
+                    c = ctx.ray_counts()
+                    rays += c[0] + c[1] + c[2]
+                rank_ms.append((time.perf_counter() - t0) / steps * 1e3)
+                rank_rays.append(rays / steps)
+        g0 = RowGather(acc, W, H, 0, n)
+        t_pack = timed(lambda: g0.pack(acc))  # rank 0 holds the most rows: the largest pack
+        t_unpack = timed(lambda: g0.unpack(acc))
+        t_xfer = max(g0.bytes_per_rank[1:]) / (XGMI_LINK_GBS * 1e9) * 1e3
+        t_rank = max(rank_ms)
+        t_ex = t_pack + t_xfer + t_unpack
+        job_rays = sum(rank_rays)
+        out[str(n)] = {"film_share_per_gpu": round(1.0 / n, 6), "spp_per_gpu": spp,
+                       "rank_ms_per_step": [round(t, 3) for t in rank_ms],
+                       "slowest_rank_ms": round(t_rank, 3),
+                       "imbalance": round(t_rank / (sum(rank_ms) / n), 4),
+                       "mrays_per_s_per_gpu": round(job_rays / n / (t_rank / 1e3) / 1e6, 2),
+                       "vs_full_step_rate": round(job_rays / n / (t_rank / 1e3) / 1e6 / value_1gpu, 4),
+                       "gather_ms": {"pack": round(t_pack, 4), "transfer_modeled": round(t_xfer, 4),
+                                     "unpack": round(t_unpack, 4)},
+                       "predicted_efficiency": round((ms_1gpu / n) / (t_rank + t_ex), 4)}
+    return {"shares": out, "partition": "image: tile rows r mod N per rank (MFX_F_ROW_PARTITION), RowGather to rank 0",
+            "note": "every rank's share of --scaling strong at N GPUs, measured on one GPU one after another; "
+                    "the exchange's pack/unpack measured here, its transfer modeled at one xGMI link "
+                    f"({XGMI_LINK_GBS:.0f} GB/s) per sending rank; predicted_efficiency counts the exchange in full "
+                    "(not overlapped)"}
 
 
 def main():
@@ -323,8 +330,9 @@ def main():
     use_dist = world > 1 or os.environ.get("MFX_BENCH_FORCE_DIST") == "1"
 
     import numpy as np
-    from mafrixraytracing_amd.abi import MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE, MFX_F_WAVEFRONT
-    from mafrixraytracing_amd.distributed import PipelinedNativeRender, step_spp
+    from mafrixraytracing_amd.abi import (MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE, MFX_F_ROW_PARTITION,
+                                          MFX_F_WAVEFRONT)
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, step_spp
     from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
@@ -338,16 +346,27 @@ def main():
     arrays = load_scene_file(args.scene)
     W, H = arrays.width, arrays.height
     npix = W * H
-    spp_step = step_spp(args.spp, ngpu, args.scaling)  # the whole job's spp per step
+    # the whole job's spp per step (strong: the config's spp over the job; weak: per GPU)
+    spp_step = step_spp(args.spp, ngpu, args.scaling)
+    rows = args.partition == "rows"
     mode = (MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE) | CONFIG_FLAGS.get(args.config, 0)
-    devices = list(range(args.gpus)) if args.single_process else None
-    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=mode, part_index=rank, part_count=world,
+    # one process per GPU: rank r traces tile rows r mod N (image partition) or samples r mod N
+    rank_mode = mode | (MFX_F_ROW_PARTITION if rows else 0)
+    devices = None
+    if args.single_process:  # one context over the device list (the library's own tile-row partition)
+        devices = list(range(args.gpus))
+        if os.environ.get("MFX_BENCH_DEVICE") is not None:  # the one-GPU rehearsal: every device is that one
+            devices = [int(os.environ["MFX_BENCH_DEVICE"])] * args.gpus
+    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank, part_count=world,
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
     pr = None
     if use_dist:
-        # two attached accumulators: frame k's RCCL reduce runs while frame k + 1 traces
+        # two attached accumulators: frame k's exchange runs while frame k + 1 traces. The image
+        # partition gathers each rank's rows to rank 0 (RCCL); gloo (the one-GPU rehearsal, CUDA
+        # tensors) has no CUDA gather, so there the rows merge by all_reduce (an exact sum too)
         accs = [torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}") for _ in range(2)]
-        pr = PipelinedNativeRender(ctx, accs, rank, world)
+        gathers = [RowGather(a, W, H, rank, world) for a in accs] if rows and backend != "gloo" else None
+        pr = PipelinedNativeRender(ctx, accs, rank, world, gathers=gathers)
     rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
@@ -363,9 +382,9 @@ def main():
         if args.api == "render":  # Scene.Render x spp: 1 spp per call, film + post + readback
             for _ in range(spp_step):
                 ctx.render_rgba8(1, out=rbuf)
-        elif pr is not None:  # one process per GPU: trace own partition, RCCL reduce via torch
+        elif pr is not None:  # one process per GPU: trace own partition, gather (or reduce) via torch
             pr.frame(spp_step, base, all_ranks=backend == "gloo")  # (gloo reduces CUDA tensors with all_reduce)
-        else:  # one GPU, or one context over the device list (the library's RCCL reduce)
+        else:  # one GPU, or one context over the device list (the library's RCCL merge)
             ctx.accum_clear()
             ctx.trace_accumulate(spp_step, base)
             if devices:
@@ -415,33 +434,38 @@ def main():
 
     elapsed, rays_all = job_max_sum(elapsed, rays)
 
-    strong = None
-    if ngpu > 1 and args.api == "batch" and args.scaling == "weak":
-        # the same job strong-scaled, in the same run: the config's spp per step split over the N GPUs
-        # (each traces about spp / N), timed like the weak steps (barriers, max over ranks)
-        def strong_step(k):
-            base = (args.warmup + args.steps) * spp_step + k * args.spp
+    other = None
+    if ngpu > 1 and args.api == "batch":
+        # the same job under the other scaling, in the same run (barriers, max over ranks): strong
+        # lines carry the weak job (the config's spp of a whole film per GPU), weak lines the strong
+        # one (the config's spp split over the GPUs)
+        o_scaling = "weak" if args.scaling == "strong" else "strong"
+        o_spp = step_spp(args.spp, ngpu, o_scaling)
+
+        def other_step(k):
+            base = (args.warmup + args.steps) * spp_step + k * o_spp
             if pr is not None:
-                pr.frame(args.spp, base, all_ranks=backend == "gloo")
+                pr.frame(o_spp, base, all_ranks=backend == "gloo")
             else:
                 ctx.accum_clear()
-                ctx.trace_accumulate(args.spp, base)
+                ctx.trace_accumulate(o_spp, base)
                 ctx.accum_reduce()
                 ctx.sync()
-        strong_step(0)
+        other_step(0)
         barrier()
-        ts, srays = time.perf_counter(), 0.0
+        ts, orays = time.perf_counter(), 0.0
         for k in range(args.steps):
-            strong_step(1 + k)
+            other_step(1 + k)
             c = ctx.ray_counts()
-            srays += c[0] + c[1] + c[2]
+            orays += c[0] + c[1] + c[2]
         barrier()
-        s_el, s_rays = job_max_sum(time.perf_counter() - ts, srays)
-        strong = {"scaling": "strong", "global_spp_per_step": args.spp, "spp_per_gpu": args.spp / ngpu,
-                  "value": round(s_rays / s_el / 1e6, 2), "unit": "Mrays/s", "steps": args.steps,
-                  "ms_per_step": round(s_el / args.steps * 1e3, 3), "rays_per_step": s_rays / args.steps,
-                  "note": "the config's spp per step split over the GPUs (whole-job Mrays/s); the line's value is "
-                          "the weak-scaled job"}
+        o_el, o_rays = job_max_sum(time.perf_counter() - ts, orays)
+        other = {"scaling": o_scaling, "global_spp_per_step": o_spp,
+                 "spp_per_gpu": o_spp if rows else o_spp / ngpu,
+                 "film_share_per_gpu": round(1.0 / ngpu, 6) if rows else 1.0,
+                 "value": round(o_rays / o_el / 1e6, 2), "unit": "Mrays/s", "steps": args.steps,
+                 "ms_per_step": round(o_el / args.steps * 1e3, 3), "rays_per_step": o_rays / args.steps,
+                 "note": f"the same job {o_scaling}-scaled (whole-job Mrays/s), measured after the line's steps"}
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
                 for k in ("total_ms", "camera_ms", "extend_ms", "camera_launches", "shadow_ms", "iterations", "launches",
                           "generations")}
@@ -612,6 +636,7 @@ def main():
                 bc = fixture["closest"]["B_ray"] if fixture else bytes_per_ray(stats["closest"])
                 bs = fixture["shadow"]["B_ray"] if fixture else bytes_per_ray(stats["shadow"])
                 ks = []
+                b_cam = bc
                 if cl > 0:
                     # k_camera's bytes are its packets' own fetches: per camera ray its
                     # share of the wave-uniform 128-B node steps and 80-B slot prefixes (scalar loads,
@@ -634,10 +659,26 @@ def main():
                 ks.sort(key=lambda x: -x[0])
                 roofline = dict(ks[0][1])
                 roofline["other_kernels"] = [k for _, k in ks[1:]]
-                step_bytes = (closest_rays * bc + (rays - closest_rays) * bs) / nt
+                # the whole step priced with each kernel's own bytes per ray: camera rays at k_camera's
+                # packet bytes when they ran as packets (pricing them at k_extend's 628 B
+                # put this entry above 1), extension rays at the closest-hit figure, shadow rays at theirs
+                cam_rays = primary_rays if cl > 0 else 0.0
+                step_bytes = (cam_rays * b_cam + (closest_rays - cam_rays) * bc + (rays - closest_rays) * bs) / nt
                 roofline["step"] = {"achieved": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9, 2),
                                     "frac": round(step_bytes / (stage_ms["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
-                                    "note": "both kernels' algorithmic bytes over the whole traced step"}
+                                    "note": "every kernel's algorithmic bytes (camera rays at k_camera's packet bytes, "
+                                            "extension and shadow rays at the frozen fixture's) over the whole traced step"}
+                # the same SURVEY §8(d) formula on this run's own traversal counters (BVH4 visits as
+                # the kernels count them) instead of the frozen BVH2 fixture: what the bytes are now
+                lc, ls = bytes_per_ray(stats["closest"]), bytes_per_ray(stats["shadow"])
+                live_step = (cam_rays * b_cam + (closest_rays - cam_rays) * lc + (rays - closest_rays) * ls) / nt
+                roofline["live_bytes_per_ray"] = {
+                    "closest": round(lc, 1), "shadow": round(ls, 1), "camera_packets": round(b_cam, 1),
+                    "step_achieved": round(live_step / (stage_ms["total_ms"] / 1e3) / 1e9, 2),
+                    "step_frac": round(live_step / (stage_ms["total_ms"] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+                    "note": "32 B per node or leaf-cluster visit + 36 B per primitive test + 64 B per ray (SURVEY.md "
+                            "§8d) on this run's MFX_F_COUNT_STATS counters (the kernels' BVH4 visits), not the "
+                            "frozen BVH2 fixture"}
             roofline["stage_ms"] = {k: round(v, 3) for k, v in stage_ms.items()}
             roofline["counters"] = {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
                                         else round(d, 4)) for g, d in stats.items()}
@@ -666,11 +707,18 @@ def main():
         elif ngpu == 1:
             par = "one GPU"
         elif args.single_process:
-            par = f"sample-partition x{ngpu}, one process, library RCCL reduce (mfx_options.devices)"
+            par = (f"image partition x{ngpu} (tile rows t % {ngpu}), one process, the library's RCCL merge "
+                   "(mfx_options.devices)")
+        elif rows:
+            par = (f"image partition x{ngpu} (tile rows t % {ngpu} per rank, MFX_F_ROW_PARTITION), one process per GPU, "
+                   + ("rows gathered to rank 0 over RCCL (RowGather)" if backend != "gloo" else
+                      "rows merged by gloo all_reduce (the one-GPU rehearsal)")
+                   + "; frame k's exchange overlapped with frame k+1's trace")
         else:
             par = (f"sample-partition x{ngpu}, one process per GPU, RCCL reduce via torch.distributed "
                    "(frame k's reduce overlapped with frame k+1's trace)")
-        per_gpu = spp_step / ngpu
+        image_part = ngpu > 1 and (rows or args.single_process)
+        per_gpu = spp_step if image_part else spp_step / ngpu
         api = ("Scene.Render pattern: mfx_render_rgba8(ctx, 1, buf) x spp, readback included"
                if args.api == "render" else "mfx_trace_accumulate of the step's spp (inputs resident in HBM)")
         result = {
@@ -683,12 +731,13 @@ def main():
                        "baseline_config": args.config,
                        "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
                        "spp_per_gpu": per_gpu, "global_spp_per_step": spp_step, "max_depth": 3,
+                       "film_share_per_gpu": round(1.0 / ngpu, 6) if image_part else 1.0,
                        "pipeline": "megakernel" if args.megakernel else "wavefront", "api": api,
                        "parallelism": par},
             "roofline": roofline, "render_api": rapi, "sample_api": sapi, "strong_share": share, "cpu_baseline": cpu,
         }
-        if strong is not None:
-            result["strong"] = strong
+        if other is not None:
+            result[other["scaling"]] = other
         print(json.dumps(result), file=json_out, flush=True)
     ctx.close()
     if use_dist:

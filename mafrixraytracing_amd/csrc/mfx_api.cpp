@@ -758,6 +758,9 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.inst = c->d_inst;
     P.light = c->host.light;
     P.cam = c->host.camera;
+    // a gray light (bitwise equal intensities): k_shadow records a lit vertex's direct term itself
+    P.gray_light = std::memcmp(&P.light.color[0], &P.light.color[1], sizeof(double)) == 0 &&
+                   std::memcmp(&P.light.color[0], &P.light.color[2], sizeof(double)) == 0 && !getenv("MFX_NO_GRAY_LIGHT");
     P.accum = c->d_accum;
     P.albedo = c->d_albedo;
     P.nmat = (int32_t)(c->host.albedo.size() / 3);

@@ -111,7 +111,11 @@ struct WfParams {
     double *dx, *dy, *dz;  // ray direction
     double* vei;           // [vertex][stride] the vertex's cosine ei = n . wi (Material.fs:35)
     WfMat* vmat;           // [vertex][stride] its material (MaterialManager slot)
-    double* vls;           // [vertex][2][stride] a lit vertex's cs = unit . n and solid = |cos_o| A / dist^2
+    double* vls;           // [vertex][2][stride] a lit vertex's cs = unit . n and solid = |cos_o| A / dist^2;
+                           // gray_light: [vertex][0][stride] its direct term a_v itself
+    int32_t gray_light;    // 1: the light's three intensities are bitwise equal, so a_v = (cs * (solid * I)) /
+                           // pdf_li is one value for every channel: k_shadow records it (one double, one
+                           // store) and k_resolve reads it instead of cs and solid (the same expression)
     int64_t vstride;       // slots per vertex-record row (the allocated pool)
     const double* albedo;  // [nmat][3] Lambert albedo per material (Material.fs:29-37)
     int32_t nmat;

@@ -732,7 +732,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     bool active = false;
     int s = 0;
     Trav T{};
-    double scs = 0.0, ssolid = 0.0;  // the operands of this vertex's direct term a_v (cs, solid)
+    double scs = 0.0, ssolid = 0.0;  // the operands of this vertex's direct term a_v (cs, solid; gray light: a_v, -)
     int vflag = 0;  // the lane's vertex: bit 0 the path continues, bit 1 lightable (cos_o < 0),
                     // bits 2..5 its index v, bits 8.. the path's lit mask so far (PD_* below)
     uint32_t c_shadow = 0;
@@ -853,7 +853,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
-                    pd.v[4 * 64 + lane] = cs; pd.v[5 * 64 + lane] = solid;
+                    // a gray light: the direct term itself, (cs * (solid * I)) / pdf_li (Integrators.fs:52,
+                    // Light.fs:52-53), the expression k_resolve evaluates per channel otherwise
+                    pd.v[4 * 64 + lane] = P.gray_light ? (cs * (solid * P.light.color[0])) / P.light.pdf : cs;
+                    pd.v[5 * 64 + lane] = solid;
                     c_shadow++;
                 }
                 // the unshaded rest of the list moves to its front
@@ -875,7 +878,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 const int e = pend_lo + rank;
                 s = pd.slot[e];
                 vflag = pd.flag[e];
-                scs = pd.v[4 * 64 + e]; ssolid = pd.v[5 * 64 + e];
+                scs = pd.v[4 * 64 + e];
+                ssolid = P.gray_light ? 0.0 : pd.v[5 * 64 + e];
                 // origin = the hit point k_extend stored (a cache hit: the shading just read it), or
                 // its copy in the next queue. That copy (nox..noz, and nslot below) was stored in this
                 // kernel by the lane that shaded the hit, which may be another lane of this wave: the
@@ -930,7 +934,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 const int jr = nq ? P.nslot[s] : ((Q && P.qslot) ? P.qslot[s] : s);
                 double* vl = P.vls + (int64_t)(2 * v) * P.vstride + jr;
                 vl[0] = scs;
-                vl[P.vstride] = ssolid;
+                if (!P.gray_light) vl[P.vstride] = ssolid;
                 mask |= 1 << v;
             }
             const bool cont = (vflag & 1) != 0;
@@ -1007,8 +1011,8 @@ __device__ __forceinline__ void load_path(const WfParams& P, int64_t j, int mask
             R.mat[v] = P.vmat[v * P.vstride + j];
             if ((mask >> v) & 1) {
                 const double* vl = P.vls + (int64_t)(2 * v) * P.vstride + j;
-                R.cs[v] = vl[0];
-                R.so[v] = vl[P.vstride];
+                R.cs[v] = vl[0];  // (a gray light: a_v itself)
+                if (!P.gray_light) R.so[v] = vl[P.vstride];
             }
         }
     }
@@ -1026,7 +1030,9 @@ __device__ __forceinline__ void fold_vertex(const WfParams& P, bool lit, double 
     const double cy = TWOPI * (ei * (INVPI * al[1]));
     const double cz = TWOPI * (ei * (INVPI * al[2]));
     double ax = 0.0, ay = 0.0, az = 0.0;
-    if (lit) {
+    if (lit && P.gray_light) {  // cs holds a_v, recorded by k_shadow with the same expression
+        ax = ay = az = cs;
+    } else if (lit) {
         ax = (cs * (so * LT.color[0])) / LT.pdf;
         ay = (cs * (so * LT.color[1])) / LT.pdf;
         az = (cs * (so * LT.color[2])) / LT.pdf;

@@ -10,6 +10,7 @@
 #   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   overlap              scripts/overlap_probe.py: exchange kernels / copies beside the persistent trace
 #   diag:CFG             one MFX_DIAG_ITER=1 frame (per-iteration ray counts and stage times)
 #   dispatch:CFG[:SPP]   per-dispatch duration and HBM bytes of one frame (kernel trace + FETCH_SIZE and
 #                        WRITE_SIZE passes, scripts/per_dispatch.py) -> dispatch_CFG.txt
@@ -55,6 +56,9 @@ for step in "$@"; do
         timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
+    overlap)
+      timeout -k 10 300 python3 scripts/overlap_probe.py > $O/overlap.json 2> $O/overlap.err
+      cat $O/overlap.json ;;
     diag)
       MFX_DIAG_ITER=1 timeout -k 10 300 python3 bench.py --config $a1 --steps 1 --warmup 1 --no-cpu-baseline \
         --no-render-api --no-stats > $O/diag_$a1.json 2> $O/diag_$a1.txt ;;

@@ -51,32 +51,37 @@ def _plain_accumulators(name, frames, part_index=0, part_count=1):
     return out
 
 
-def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False):
+def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
     import torch.distributed as dist
 
     from conftest import scene
-    from mafrixraytracing_amd.distributed import PipelinedNativeRender, native_partitioned_render
+    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, native_partitioned_render
     from mafrixraytracing_amd.native import NativeContext
 
     torch.cuda.set_device(0)
     dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     a = scene(name, W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
-    with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world) as ctx:
+    gather = rows and backend == "nccl"  # (gloo has no CUDA gather: rows merge by all_reduce there)
+    with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world,
+                       flags=MFX_F_ROW_PARTITION if rows else 0) as ctx:
         got = []
         if pipelined:  # back to back, no waits between frames; the last two buffers checked after drain
             acc1 = torch.zeros_like(acc)
-            pr = PipelinedNativeRender(ctx, [acc, acc1], rank, world)
+            gs = [RowGather(b, W, H, rank, world) for b in (acc, acc1)] if gather else None
+            pr = PipelinedNativeRender(ctx, [acc, acc1], rank, world, gathers=gs)
             for spp, base in frames:
                 pr.frame(spp, base, all_ranks=all_ranks)
             pr.drain()
             got = [pr.buffer(k).cpu().numpy().copy() for k in range(len(frames) - 2, len(frames))]
             pr.close()
         else:
-            pr = native_partitioned_render(ctx, acc, rank, world)
+            pr = native_partitioned_render(ctx, acc, rank, world,
+                                           exchange=RowGather(acc, W, H, rank, world) if gather else None)
             for spp, base in frames:
                 pr.frame(spp, base, all_ranks=all_ranks)
                 got.append(acc.cpu().numpy().copy())
@@ -87,10 +92,10 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False):
+def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False):
     import torch.multiprocessing as mp
     mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks,
-                                           pipelined),
+                                           pipelined, rows),
                        nprocs=world, join=True, start_method="spawn")
     return np.load(os.path.join(outdir, "frames.npy"))
 
@@ -116,6 +121,28 @@ def test_world1_nccl_pipelined_frames_bit_identical(gpu, tmp_path):
     want = _plain_accumulators("spot", FRAMES)
     for k in range(2):
         assert np.array_equal(got[k], want[len(FRAMES) - 2 + k]), k
+
+
+@pytest.mark.parametrize("pipelined", [False, True])
+def test_world1_nccl_row_gather_bit_identical(gpu, tmp_path, pipelined):
+    """The bench's default exchange at world 1: MFX_F_ROW_PARTITION context, RowGather (pack, RCCL
+    gather, unpack) per frame, plain and pipelined — every checked frame equals the plain context's."""
+    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False, pipelined=pipelined, rows=True)
+    want = _plain_accumulators("spot", FRAMES)
+    ks = range(len(FRAMES) - 2, len(FRAMES)) if pipelined else range(len(FRAMES))
+    for i, k in enumerate(ks):
+        assert np.array_equal(got[i], want[k]), k
+
+
+def test_two_ranks_row_partition_gloo_merge_exact(gpu, tmp_path):
+    """Two ranks sharing device 0, each tracing its tile rows (MFX_F_ROW_PARTITION, 36 rows = 5 tile
+    rows, the last partial), pipelined, merged by gloo all_reduce: every merged accumulator is the
+    whole-film context's bit for bit (a pixel is non-zero on one rank only)."""
+    frames = [(2, 0), (3, 2), (1, 5), (2, 6)]
+    got = _spawn(2, "gloo", "cube_cornell", frames, tmp_path, True, pipelined=True, rows=True)
+    want = _plain_accumulators("cube_cornell", frames)
+    for k in range(2):
+        assert np.array_equal(got[k], want[len(frames) - 2 + k]), k
 
 
 def test_two_ranks_pipelined_gloo_allreduce(gpu, tmp_path):
@@ -169,29 +196,51 @@ def test_bench_multiprocess_path_under_torchrun(gpu, tmp_path):
     assert line["rays_per_step"] == plain["rays_per_step"] > 0
 
 
+def _bench(args, env=None, torchrun=0):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py")] + args
+    if torchrun:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={torchrun}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port())] + cmd[1:]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
 def test_bench_two_ranks_rehearsal_under_torchrun(gpu):
     """The driver's N-GPU launch rehearsed on one GPU: bench.py under torch.distributed.run with 2
     ranks, both on device 0 over gloo (MFX_BENCH_DEVICE / MFX_BENCH_BACKEND; RCCL refuses two ranks
-    on one device). The whole world > 1 path runs — partitions, pipelined frames and reduces, the
-    barrier, max-over-ranks timing, the rays summed over ranks — and the line reports 2 GPUs,
-    weak scaling, and the rays of the 2x larger sample set (equal to a 1-rank run of that set)."""
+    on one device). The whole world > 1 path runs — the image partition, pipelined frames and row
+    merges, the barrier, max-over-ranks timing, the rays summed over ranks — and the line reports 2
+    GPUs, strong scaling of the metric's job (the config's spp over the whole film, each rank half of
+    the rows) with the rays of a 1-rank run of that job; the weak sub-object has the rays of the 2x
+    larger sample set."""
     common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
     env = dict(os.environ, MFX_BENCH_DEVICE="0", MFX_BENCH_BACKEND="gloo")
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
-           "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"), "--spp", "2"] + common
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300, env=env, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
-    line = json.loads(r.stdout.strip().splitlines()[-1])
-    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
-    assert line["config"]["global_spp_per_step"] == 4
-    # one process, the same 4-spp-per-step sample set: the same rays per step
-    r1 = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--spp", "4"] + common, capture_output=True,
-                        text=True, timeout=300, cwd=ROOT)
-    assert r1.returncode == 0, r1.stderr[-3000:]
-    one = json.loads(r1.stdout.strip().splitlines()[-1])
+    line = _bench(["--spp", "2"] + common, env=env, torchrun=2)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong"
+    assert line["config"]["global_spp_per_step"] == 2 and line["config"]["film_share_per_gpu"] == 0.5
+    assert "image partition" in line["config"]["parallelism"]
+    one = _bench(["--spp", "2"] + common)
     assert line["rays_per_step"] == one["rays_per_step"] > 0
-    # the strong split of the same job in the same run: the config's 2 spp per step over the 2 ranks
-    st = line["strong"]
-    assert st["scaling"] == "strong" and st["global_spp_per_step"] == 2 and st["spp_per_gpu"] == 1
-    assert 0 < st["rays_per_step"] < line["rays_per_step"] and st["value"] > 0
+    wk = line["weak"]
+    assert wk["scaling"] == "weak" and wk["global_spp_per_step"] == 4
+    # (the sub-object continues the sample sequence after the line's steps: other samples of the same
+    # 4-spp-per-step job, so its rays per step agree with a 1-rank run's to sampling noise)
+    four = _bench(["--spp", "4"] + common)
+    assert abs(wk["rays_per_step"] / four["rays_per_step"] - 1) < 2e-3 and wk["value"] > 0
 
+
+def test_bench_single_process_device_list_rehearsal(gpu):
+    """bench.py --single-process --gpus 2 on the one-GPU box (MFX_BENCH_DEVICE=0: the device list
+    [0, 0]): the library's own image partition and merge in the timed step, the batch line and the
+    Scene.Render line (--api render, render-ahead on the device list), each with the rays of the
+    one-GPU run of the same job."""
+    common = ["--steps", "2", "--warmup", "1", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    env = dict(os.environ, MFX_BENCH_DEVICE="0")
+    line = _bench(["--spp", "4", "--single-process", "--gpus", "2"] + common, env=env)
+    one = _bench(["--spp", "4"] + common)
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["rays_per_step"] == one["rays_per_step"]
+    ra = ["--spp", "8", "--api", "render", "--render-ahead", "4"]
+    rl = _bench(ra + ["--single-process", "--gpus", "2"] + common, env=env)
+    r1 = _bench(ra + common)
+    assert rl["n_gpus"] == 2 and rl["rays_per_step"] == r1["rays_per_step"] > 0

@@ -261,3 +261,27 @@ def test_survey_named_entry_points(gpu):
         n = c2.ray_counts()
         assert rays == n[0] + n[1] + n[2] and rays > 0
         assert 0 < sec < 10 and abs(sec * 1e3 - c2.last_trace_ms()) < 1e-9
+
+
+@pytest.mark.parametrize("name", ["spot", "cube_cornell"])
+def test_colored_and_gray_light_records(gpu, oracle, monkeypatch, name):
+    """A lit vertex's direct term is recorded as a_v itself for a gray light (one double) and as its
+    operands cs and solid otherwise (k_resolve evaluates a_v per channel): a colored light through the
+    second form equals the oracle bit for bit, and the scene's own gray light gives the same image and
+    frames through either form (MFX_NO_GRAY_LIGHT pins the general one)."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, 40, 24)
+    a.light = dict(a.light, intensity=(3.0, 2.5, 1.0))
+    ref = oracle.OracleScene(a).sample(6, SEED, sample_base=0)
+    with NativeContext(a, seed=SEED) as ctx:
+        assert np.array_equal(ctx.sample(6), ref)
+    g = scene(name, 40, 24)
+    out = []
+    for general in (False, True):
+        if general:
+            monkeypatch.setenv("MFX_NO_GRAY_LIGHT", "1")
+        with NativeContext(g, seed=SEED) as ctx, NativeContext(g, seed=SEED, render_ahead=3) as ra:
+            out.append((ctx.sample(5), [ra.render_rgba8(1) for _ in range(4)]))
+    assert np.array_equal(out[0][0], out[1][0])
+    assert all(np.array_equal(x, y) for x, y in zip(out[0][1], out[1][1]))
+    assert np.array_equal(out[0][0], oracle.OracleScene(g).sample(5, SEED, sample_base=0))
