@@ -10,6 +10,7 @@
 #   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   vparity              scripts/variant_parity.py: every build_variants/*.so bit-exact vs the oracle
 #   overlap              scripts/overlap_probe.py: exchange kernels / copies beside the persistent trace
 #   diag:CFG             one MFX_DIAG_ITER=1 frame (per-iteration ray counts and stage times)
 #   dispatch:CFG[:SPP]   per-dispatch duration and HBM bytes of one frame (kernel trace + FETCH_SIZE and
@@ -56,6 +57,9 @@ for step in "$@"; do
         timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
+    vparity)
+      timeout -k 10 600 python3 scripts/variant_parity.py build_variants/*.so > $O/vparity.txt 2>&1
+      cat $O/vparity.txt ;;
     overlap)
       timeout -k 10 300 python3 scripts/overlap_probe.py > $O/overlap.json 2> $O/overlap.err
       cat $O/overlap.json ;;
