@@ -231,7 +231,7 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
                         "to pageable host memory, synchronize"}
 
 
-def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=2, flags=0):
+def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=4, flags=0):
     """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
     measured on this GPU: rank r traces all `spp` samples of the film's tile rows r mod N
     (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
@@ -288,15 +288,15 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=2, flags=0):
             with NativeContext(arrays, seed=seed, flags=flags | MFX_F_ROW_PARTITION, part_index=r, part_count=n) as ctx:
                 ctx.trace_accumulate(spp, 0)  # the pool's first allocation, untimed
                 ctx.sync()
-                rays, t0 = 0.0, time.perf_counter()
-                for k in range(steps):
+                ctx.ray_counts_total(reset=True)
+                t0 = time.perf_counter()
+                for k in range(steps):  # back to back, as the bench's steps run
                     ctx.accum_clear()
                     ctx.trace_accumulate(spp, (k + 1) * spp)
-                    ctx.sync()
-                    c = ctx.ray_counts()
-                    rays += c[0] + c[1] + c[2]
+                ctx.sync()
                 rank_ms.append((time.perf_counter() - t0) / steps * 1e3)
-                rank_rays.append(rays / steps)
+                c = ctx.ray_counts_total(reset=True)
+                rank_rays.append((c[0] + c[1] + c[2]) / steps)
                 if r == 0:
                     ov = overlap(ctx, RowGather(acc, W, H, 0, n))
         g0 = RowGather(acc, W, H, 0, n)
@@ -418,16 +418,17 @@ def main():
                 ctx.render_rgba8(1, out=rbuf)
         elif pr is not None:  # one process per GPU: trace own partition, gather (or reduce) via torch
             pr.frame(spp_step, base, all_ranks=backend == "gloo")  # (gloo reduces CUDA tensors with all_reduce)
-        else:  # one GPU, or one context over the device list (the library's RCCL merge)
+        else:  # one GPU, or one context over the device list (the library's RCCL merge); no host wait:
+            # steps run back to back on the context's stream(s), as a render loop enqueues them
             ctx.accum_clear()
             ctx.trace_accumulate(spp_step, base)
             if devices:
                 ctx.accum_reduce()
-            ctx.sync()
 
     for k in range(args.warmup):
         step(k)
     barrier()
+    ctx.ray_counts_total(reset=True)  # the timed steps' rays: device-side totals, read after the final barrier
     t0 = time.perf_counter()
     rays = 0.0
     closest_rays = 0.0
@@ -446,16 +447,20 @@ def main():
                 primary_rays += c[0]
                 timings.append(ctx.trace_timing())
             continue
-        step(args.warmup + k)
-        c = ctx.ray_counts()
-        rays += c[0] + c[1] + c[2]
-        closest_rays += c[0] + c[1]
-        primary_rays += c[0]
-        timings.append(ctx.trace_timing())
+        step(args.warmup + k)  # enqueued; the steps run back to back (no per-step host read)
     barrier()
     elapsed = time.perf_counter() - t0
     if args.api == "render":
         elapsed = call_s
+    else:
+        c = ctx.ray_counts_total(reset=True)  # every timed step's counters, summed on the device
+        rays, closest_rays, primary_rays = c[0] + c[1] + c[2], c[0] + c[1], c[0]
+        # per-stage device times (HIP events around each launch) from two more steps of the same
+        # workload, each read after it (the timed steps above carry no per-step host read)
+        for k in range(2):
+            step(args.warmup + args.steps + k)
+            timings.append(ctx.trace_timing())
+        barrier()
 
     def job_max_sum(el, ry):  # the slowest rank's time, the job's rays
         if not use_dist:
@@ -484,16 +489,15 @@ def main():
                 ctx.accum_clear()
                 ctx.trace_accumulate(o_spp, base)
                 ctx.accum_reduce()
-                ctx.sync()
         other_step(0)
         barrier()
-        ts, orays = time.perf_counter(), 0.0
+        ctx.ray_counts_total(reset=True)
+        ts = time.perf_counter()
         for k in range(args.steps):
             other_step(1 + k)
-            c = ctx.ray_counts()
-            orays += c[0] + c[1] + c[2]
         barrier()
-        o_el, o_rays = job_max_sum(time.perf_counter() - ts, orays)
+        c = ctx.ray_counts_total(reset=True)
+        o_el, o_rays = job_max_sum(time.perf_counter() - ts, c[0] + c[1] + c[2])
         other = {"scaling": o_scaling, "global_spp_per_step": o_spp,
                  "spp_per_gpu": o_spp if rows else o_spp / ngpu,
                  "film_share_per_gpu": round(1.0 / ngpu, 6) if rows else 1.0,

@@ -178,7 +178,11 @@ int mfx_expand_instances(const mfx_prim* prims, int64_t nprims, const mfx_instan
  * All 0 but [5..7] for a flat context.                                                         */
 int mfx_instancing_info(mfx_ctx* ctx, double out[8]);
 /* Host-only (no device needed): the same figures for a scene built on the host from an instanced
- * description (MFX_F_FLATTEN honoured), plus the traversal stack bound.                       */
+ * description (MFX_F_FLATTEN honoured), plus the traversal stack bound. Without a device it
+ * applies MFX_FLATTEN_MAX_BYTES alone: mfx_create_instanced also caps the flat image at a
+ * sixteenth of the device's free memory, so on a nearly full device a context may trace two-level
+ * where this reports flat (mfx_instancing_info out[0] > 0 tells a context's actual choice; the
+ * images are the same either way).                                                              */
 int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* instances, int32_t ninstances,
                              int32_t flags, double out[8], int32_t* stack_entries);
 
@@ -273,6 +277,12 @@ int mfx_trace_timing(mfx_ctx* ctx, double out[8]);
  * out[10] / out[11] = the camera-ray packets' own fetches (k_camera: wave-uniform 128-B node
  * steps and leaf slots, once per wave; the per-ray visits of packet lanes are in out[4..6]).    */
 int mfx_ray_counts(mfx_ctx* ctx, double out[16]);
+
+/* The same counters summed over every mfx_trace_accumulate (and mfx_sample / mfx_render_rgba8
+ * without render-ahead) since the context was created or last reset: each trace adds its counters
+ * to device-side totals in stream order, so back-to-back traces need no host read in between (the
+ * benchmark's timed steps). Waits for the context's work; reset != 0 zeroes the totals after the read. */
+int mfx_ray_counts_total(mfx_ctx* ctx, double out[16], int32_t reset);
 
 /* SURVEY.md §8(b)'s stats call, for the Mrays/s metric (§8(d)): rays = primary + extension +
  * shadow rays traced by the last mfx_sample / mfx_render_rgba8 / mfx_trace_accumulate call (the

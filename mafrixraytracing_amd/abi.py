@@ -164,6 +164,7 @@ def _bind(lib):
         "mfx_ray_counts": (C.c_int, [C.c_void_p, _dp]),
         "mfx_last_trace_ms": (C.c_int, [C.c_void_p, _dp]),
         "mfx_trace_timing": (C.c_int, [C.c_void_p, _dp]),
+        "mfx_ray_counts_total": (C.c_int, [C.c_void_p, _dp, C.c_int32]),
         "mfx_closest_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, C.c_double, _dp, _ip, _dp]),
         "mfx_any_hit": (C.c_int, [C.c_void_p, C.c_int64, _dp, C.c_double, _dp, _ip]),
         "mfx_ref_leaves": (C.c_int, [C.c_void_p, _ip, _ip, _ip, _ip]),
@@ -186,7 +187,7 @@ EXPORTED_SYMBOLS = [
     "mfx_create", "mfx_create_instanced", "mfx_expand_instances", "mfx_instancing_info", "mfx_build_instanced_info", "mfx_destroy", "mfx_sample", "mfx_render_rgba8", "mfx_accumulate_render_rgba8", "mfx_reset",
     "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
-    "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
+    "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_ray_counts_total", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
     "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 

@@ -121,7 +121,8 @@ struct mfx_ctx {
     double* d_frame = nullptr;   // [npix][4] staging for x-major outputs
     uint8_t* d_rgba = nullptr;   // [npix][4]
     unsigned long long* d_work = nullptr;
-    unsigned long long* d_counters = nullptr;  // [8]
+    unsigned long long* d_counters = nullptr;  // [WF_SHARDS][WF_NCTR] the last trace's counters
+    unsigned long long* d_counters_total = nullptr;  // [WF_SHARDS][WF_NCTR] running totals (mfx_ray_counts_total)
     uint64_t seed = 0;
     int flags = 0;
     int part_index = 0, part_count = 1;  // sample partition: global samples part_index mod part_count
@@ -260,7 +261,7 @@ static void free_ctx(mfx_ctx* c) {
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     if (c->d_merge) (void)hipFree(c->d_merge);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     ahead_free(c);
@@ -328,6 +329,8 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipMalloc((void**)&c->d_rgba, 4 * (size_t)c->npix));
     CK(hipMalloc((void**)&c->d_work, 64));
     CK(hipMalloc((void**)&c->d_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
+    CK(hipMalloc((void**)&c->d_counters_total, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
+    CK(hipMemset(c->d_counters_total, 0, WF_NCTR * WF_SHARDS * sizeof(unsigned long long)));
     CK(hipMalloc((void**)&c->d_wfctl, WF_CTL_ALLOC * sizeof(unsigned long long)));
     {
         size_t mfree = 0, mtotal = 0;
@@ -928,7 +931,12 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
         c->generations = 0;
         return MFX_OK;
     }
-    if (!c->mega_last) return wf_trace(c, ns, sample_base);
+    if (!c->mega_last) {
+        const int rc = wf_trace(c, ns, sample_base);
+        if (rc) return rc;
+        HIPCHECK(mfx_launch_counters_add(c->d_counters_total, c->d_counters, WF_NCTR * WF_SHARDS, c->stream));
+        return MFX_OK;
+    }
     TraceParams P;
     std::memset(&P, 0, sizeof(P));
     P.nodes = c->d_nodes;
@@ -970,6 +978,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     HIPCHECK(mfx_launch_trace(P, (c->flags & MFX_F_COUNT_STATS) != 0, c->grid, c->stream));
     HIPCHECK(hipEventRecord(c->ev1, c->stream));
     c->ev_valid = true;
+    HIPCHECK(mfx_launch_counters_add(c->d_counters_total, c->d_counters, WF_NCTR * WF_SHARDS, c->stream));
     return MFX_OK;
 }
 
@@ -1246,6 +1255,22 @@ static void note_live(mfx_ctx* c, const unsigned long long* h) {
             break;
         }
     c->wf_queue_auto = from;
+}
+
+int mfx_ray_counts_total(mfx_ctx* c, double out[16], int32_t reset) {
+    if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    for (int k = 0; k < 16; ++k) out[k] = 0.0;
+    for (mfx_ctx* d : devs_of(c)) {  // summed over the context's devices
+        HIPCHECK(hipSetDevice(d->device));
+        unsigned long long h[WF_NCTR * WF_SHARDS];
+        HIPCHECK(hipMemcpyAsync(h, d->d_counters_total, sizeof(h), hipMemcpyDeviceToHost, d->stream));
+        HIPCHECK(hipStreamSynchronize(d->stream));
+        sum_counters(h, out);
+        if (reset) HIPCHECK(hipMemsetAsync(d->d_counters_total, 0, sizeof(h), d->stream));
+    }
+    HIPCHECK(hipSetDevice(c->device));
+    out[3] = out[0];  // paths == primary rays
+    return MFX_OK;
 }
 
 int mfx_ray_counts(mfx_ctx* c, double out[16]) {

@@ -57,6 +57,7 @@ hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h,
                                 int add, uint8_t* rgba, hipStream_t st);
 hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_count, double* out, hipStream_t st);
 hipError_t mfx_launch_accum_add(double* dst, const double* src, int64_t n, hipStream_t st);
+hipError_t mfx_launch_counters_add(unsigned long long* total, const unsigned long long* c, int n, hipStream_t st);
 hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n, double* dvo, double* sqo,
                                     hipStream_t st);
 hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st);

@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <stdint.h>
 
 #include "mfx_layout.h"
@@ -290,6 +291,123 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     Q.occ_out[k] = traverse<true, false, INST>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, B, st) ? 1 : 0;
 }
 
+// Experiment (VERDICT r04 Next #4a; MFX_ANYHIT_PACKET=16 switches mfx_any_hit to it): the any-hit
+// query traced as four 16-lane sub-packets per wave. A sub-packet walks the BVH4 together: its
+// lanes load the same node (per-lane loads of one address), each tests the four children with its
+// own FP32 ray and limit, a child is visited when some live lane of the sub-packet hits it, far to
+// near by the exit distances of the sub-packet's first live lane, and the stack (node + the 64-bit
+// mask of the lanes whose own test hit it, only this sub-packet's 16 bits set) is the sub-packet's,
+// in LDS. A lane tests exactly the leaves its own ray's box tests reach, as its single-ray walk
+// would (child boxes lie inside their parents'), and leaves its sub-packet once occluded; whether a
+// ray is occluded does not depend on the visit order (node_step's FAR note), so every answer is the
+// single-ray kernel's (tests/test_gpu_edge_parity.py). STATS: wave node steps and leaf rounds in
+// steps[0], steps[1] (one count per wave iteration), per-lane visits in steps[2], steps[3].
+template <bool STATS>
+__global__ void __launch_bounds__(256) anyhit_packet16_kernel(QueryParams Q, unsigned long long* steps) {
+    extern __shared__ int lds[];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, g = lane >> 4;
+    const uint64_t gbits = 0xffffULL << (16 * g);
+    int* stk = lds + (wave * 4 + g) * Q.stack_size * 3;  // per entry: node, mask low, mask high
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool act = k < Q.n;
+    const SceneView S{Q.nodes, Q.slots, Q.slot_ref, Q.ref_blob, Q.inst, nullptr, 0};
+    DV o = dv(0, 0, 0), d = dv(0, 0, 1);
+    double tmax = 0.0;
+    if (act) {
+        o = ld3(Q.rays + 6 * k);
+        d = ld3(Q.rays + 6 * k + 3);
+        tmax = Q.tmax_per_ray[k];
+    }
+    const RayF rf = make_rayf(o, d);
+    const float tlim = f_tlim(tmax);
+    bool alive = act;  // not (yet) found occluded
+    bool occ = false;
+    uint64_t mask = __ballot(alive) & gbits;  // sub-packet-uniform: its lanes whose test hit `node`
+    int node = mask ? 0 : MFX_TRAV_EXIT, sp = 0;
+    Best B;
+    Stats st{0, 0, 0};
+    uint32_t w_nodes = 0, w_leaves = 0;
+    while (__any(node != MFX_TRAV_EXIT)) {
+        const bool mine = ((mask >> lane) & 1) && alive;
+        bool pop = false;
+        if (node >= 0) {  // the sub-packet's node step
+            if (STATS) w_nodes += lane == 0 ? 1 : 0;
+            if (STATS && mine) st.nodes++;
+            const float4* __restrict__ q = (const float4*)(Q.nodes + node);
+            const float4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+            const int4 ch = *(const int4*)(q + 6);
+            Slab4 SL;
+            slab4(lx, hx, ly, hy, lz, hz, rf, SL);
+            const uint64_t live = __ballot(alive) & gbits;
+            const int rep = __builtin_ctzll((mask & live) | (1ULL << (16 * g)));  // the sub-packet's first live lane
+            float dk[4];
+            int c[4] = {ch.x, ch.y, ch.z, ch.w};
+            uint64_t m[4];
+            int nh = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const float n = fmaxf(fmaxf(fminf(SL.a0[j], SL.a1[j]), fminf(SL.b0[j], SL.b1[j])), fmaxf(fminf(SL.c0[j], SL.c1[j]), 0.0f));
+                const float f = fminf(fminf(fmaxf(SL.a0[j], SL.a1[j]), fmaxf(SL.b0[j], SL.b1[j])), fminf(fmaxf(SL.c0[j], SL.c1[j]), tlim));
+                const bool h = mine && n <= f;
+                m[j] = __ballot(h) & gbits;
+                const float kd = __shfl(h ? -f : 3.0e38f, rep);  // far first: the representative's exit
+                dk[j] = m[j] ? kd : __builtin_inff();
+                nh += m[j] ? 1 : 0;
+            }
+            cswap3(dk[0], c[0], m[0], dk[1], c[1], m[1]);
+            cswap3(dk[2], c[2], m[2], dk[3], c[3], m[3]);
+            cswap3(dk[0], c[0], m[0], dk[2], c[2], m[2]);
+            cswap3(dk[1], c[1], m[1], dk[3], c[3], m[3]);
+            cswap3(dk[1], c[1], m[1], dk[2], c[2], m[2]);
+            if (lane == 16 * g) {  // far-first pushes, one lane per sub-packet
+                for (int j = nh - 1; j >= 1; --j) {
+                    int* e = stk + 3 * (sp + nh - 1 - j);
+                    e[0] = c[j];
+                    e[1] = (int)(uint32_t)m[j];
+                    e[2] = (int)(uint32_t)(m[j] >> 32);
+                }
+            }
+            if (nh > 0) {
+                sp += nh - 1;
+                node = c[0];
+                mask = m[0];
+            } else {
+                pop = true;
+            }
+        } else if (node != MFX_TRAV_EXIT) {  // a leaf: its live lanes test it (any hit)
+            if (STATS) w_leaves += lane == 0 ? 1 : 0;
+            if (mine && leaf_hit<true, STATS>(S, ~node, o, d, Q.tmin, tmax, B, st)) {
+                occ = true;
+                alive = false;
+            }
+            pop = true;
+        }
+        if (pop) {  // the next entry with a live lane, or the end of the sub-packet's walk
+            const uint64_t live = __ballot(alive) & gbits;
+            node = MFX_TRAV_EXIT;
+            while (sp > 0) {
+                --sp;
+                const int* e = stk + 3 * sp;
+                const uint64_t mm = ((uint64_t)(uint32_t)e[2] << 32) | (uint32_t)e[1];
+                if (mm & live) {
+                    node = e[0];
+                    mask = mm & live;
+                    break;
+                }
+            }
+        }
+    }
+    if (act) Q.occ_out[k] = occ ? 1 : 0;
+    if (STATS && steps) {
+        if (lane == 0) {
+            atomicAdd(steps + 0, (unsigned long long)w_nodes);
+            atomicAdd(steps + 1, (unsigned long long)w_leaves);
+        }
+        atomicAdd(steps + 2, (unsigned long long)st.nodes);
+        atomicAdd(steps + 3, (unsigned long long)st.clusters);
+    }
+}
+
 // ----------------------------------------------------------------------------------------------
 // Film + post (FP64, reference order)
 // ----------------------------------------------------------------------------------------------
@@ -340,6 +458,13 @@ __global__ void film_mean_kernel(const double* __restrict__ film, int64_t npix, 
 __global__ void accum_add_kernel(double* __restrict__ dst, const double* __restrict__ src, int64_t n) {
     const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k < n) dst[k] = dst[k] + src[k];
+}
+
+// a trace's ray / traversal counters added to the context's running totals (mfx_ray_counts_total):
+// stream-ordered, so back-to-back traces need no host read in between
+__global__ void counters_add_kernel(unsigned long long* __restrict__ total, const unsigned long long* __restrict__ c, int n) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < n) total[k] += c[k];
 }
 
 __global__ void fp64_selftest_kernel(const double* a, const double* b, int64_t n, double* dv_out, double* sq_out) {
@@ -408,7 +533,11 @@ hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st) {
     const size_t lds = (size_t)4 * Q.stack_size * 64 * sizeof(int);
     const dim3 g(grid_for(Q.n, 256));
     if (shadow) {
-        if (Q.inst) hipLaunchKernelGGL(anyhit_kernel<true>, g, dim3(256), lds, st, Q);
+        const char* pk = getenv("MFX_ANYHIT_PACKET");  // the sub-packet experiment (flat scenes)
+        if (pk && atoi(pk) == 16 && !Q.inst)
+            hipLaunchKernelGGL(anyhit_packet16_kernel<false>, g, dim3(256), (size_t)16 * Q.stack_size * 3 * sizeof(int),
+                               st, Q, nullptr);
+        else if (Q.inst) hipLaunchKernelGGL(anyhit_kernel<true>, g, dim3(256), lds, st, Q);
         else hipLaunchKernelGGL(anyhit_kernel<false>, g, dim3(256), lds, st, Q);
     } else {
         if (Q.inst) hipLaunchKernelGGL(closest_kernel<true>, g, dim3(256), lds, st, Q);
@@ -442,6 +571,11 @@ hipError_t mfx_launch_fp64_selftest(const double* a, const double* b, int64_t n,
 
 hipError_t mfx_launch_aabb_selftest(const double* rec, int64_t n, int32_t* out, hipStream_t st) {
     hipLaunchKernelGGL(aabb_selftest_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, rec, n, out);
+    return hipGetLastError();
+}
+
+hipError_t mfx_launch_counters_add(unsigned long long* total, const unsigned long long* c, int n, hipStream_t st) {
+    hipLaunchKernelGGL(counters_add_kernel, dim3(grid_for(n, 256)), dim3(256), 0, st, total, c, n);
     return hipGetLastError();
 }
 

@@ -746,6 +746,26 @@ __device__ __forceinline__ int inst_frame(const SceneView& S, int node, int& ins
     return node;
 }
 
+// The slab distances of a BVH4 node's four children for one FP32 ray: plane * (1/d) - o * (1/d),
+// one rounding each (fmaf). (Two children per v_pk_fma_f32, gfx950's packed FP32 FMA — the same
+// fused operation, the same bits — measured: k_camera unchanged, the per-lane kernels' extra
+// register pairs C2 -2.6 %, C4 -2.2 %; r05f_ab_pk_slab.txt. Not kept.)
+struct Slab4 {
+    float a0[4], a1[4], b0[4], b1[4], c0[4], c1[4];
+};
+__device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const float4& ly, const float4& hy,
+                                      const float4& lz, const float4& hz, const RayF& r, Slab4& S) {
+    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
+    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
+    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        S.a0[k] = fmaf(LX[k], r.ix, -r.oix); S.a1[k] = fmaf(HX[k], r.ix, -r.oix);
+        S.b0[k] = fmaf(LY[k], r.iy, -r.oiy); S.b1[k] = fmaf(HY[k], r.iy, -r.oiy);
+        S.c0[k] = fmaf(LZ[k], r.iz, -r.oiz); S.c1[k] = fmaf(HZ[k], r.iz, -r.oiz);
+    }
+}
+
 template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
@@ -771,14 +791,11 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     float d[4];
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     int nh = 0;
-    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    Slab4 SL;
+    slab4(lx, hx, ly, hy, lz, hz, r, SL);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float a0 = fmaf(LX[k], r.ix, -r.oix), a1 = fmaf(HX[k], r.ix, -r.oix);
-        const float b0 = fmaf(LY[k], r.iy, -r.oiy), b1 = fmaf(HY[k], r.iy, -r.oiy);
-        const float c0 = fmaf(LZ[k], r.iz, -r.oiz), c1 = fmaf(HZ[k], r.iz, -r.oiz);
+        const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = n <= f;
@@ -837,14 +854,12 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     uint64_t m[4];
     int nh = 0;
-    const float LX[4] = {lx.x, lx.y, lx.z, lx.w}, HX[4] = {hx.x, hx.y, hx.z, hx.w};
-    const float LY[4] = {ly.x, ly.y, ly.z, ly.w}, HY[4] = {hy.x, hy.y, hy.z, hy.w};
-    const float LZ[4] = {lz.x, lz.y, lz.z, lz.w}, HZ[4] = {hz.x, hz.y, hz.z, hz.w};
+    Slab4 SL;
+    slab4(float4{lx.x, lx.y, lx.z, lx.w}, float4{hx.x, hx.y, hx.z, hx.w}, float4{ly.x, ly.y, ly.z, ly.w},
+          float4{hy.x, hy.y, hy.z, hy.w}, float4{lz.x, lz.y, lz.z, lz.w}, float4{hz.x, hz.y, hz.z, hz.w}, r, SL);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float a0 = fmaf(LX[k], r.ix, -r.oix), a1 = fmaf(HX[k], r.ix, -r.oix);
-        const float b0 = fmaf(LY[k], r.iy, -r.oiy), b1 = fmaf(HY[k], r.iy, -r.oiy);
-        const float c0 = fmaf(LZ[k], r.iz, -r.oiz), c1 = fmaf(HZ[k], r.iz, -r.oiz);
+        const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];
         const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
         const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
         const bool h = live && n <= f;

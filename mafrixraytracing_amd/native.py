@@ -134,6 +134,13 @@ class NativeContext:
         check(self.lib.mfx_ray_counts(self._h, dptr(out)), "mfx_ray_counts")
         return out
 
+    def ray_counts_total(self, reset: bool = True) -> np.ndarray:
+        """The ray counters summed over every trace since creation or the last reset
+        (mfx_ray_counts_total): no host read between back-to-back traces."""
+        out = np.zeros(16)
+        check(self.lib.mfx_ray_counts_total(self._h, dptr(out), 1 if reset else 0), "mfx_ray_counts_total")
+        return out
+
     def stats(self) -> tuple[float, float]:
         """(rays traced, device seconds) of the last trace call (mfx_stats)."""
         rays, sec = C.c_double(), C.c_double()

@@ -10,6 +10,7 @@
 #   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   subpk:SCENE          scripts/shadow_packets.py under rocprofv3: per-lane vs 16-lane sub-packet any-hit kernels
 #   vparity              scripts/variant_parity.py: every build_variants/*.so bit-exact vs the oracle
 #   overlap              scripts/overlap_probe.py: exchange kernels / copies beside the persistent trace
 #   diag:CFG             one MFX_DIAG_ITER=1 frame (per-iteration ray counts and stage times)
@@ -57,6 +58,14 @@ for step in "$@"; do
         timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
+    subpk)
+      D=$R/$O/subpk_$a1
+      mkdir -p $D
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $D/trace -o run -- \
+         python3 $R/scripts/shadow_packets.py --scene $R/scenes/$a1 > $D/run.json 2> $D/run.err)
+      cat $D/run.json
+      grep -h "anyhit" $D/trace/*kernel_stats.csv | cut -d, -f1-4 ;;
     vparity)
       timeout -k 10 600 python3 scripts/variant_parity.py build_variants/*.so > $O/vparity.txt 2>&1
       cat $O/vparity.txt ;;

@@ -177,3 +177,27 @@ def test_one_sample_calls_megakernel_equals_wavefront(gpu):
     with NativeContext(a, seed=SEED, devices=[0, 0]) as m2, NativeContext(a, seed=SEED, devices=[0, 0],
                                                                          flags=MFX_F_WAVEFRONT) as w2:
         assert np.array_equal(m2.sample(2), w2.sample(2))
+
+
+@pytest.mark.parametrize("devices", [None, [0, 0]])
+def test_ray_counts_total_sums_back_to_back_traces(gpu, devices):
+    """mfx_ray_counts_total: the counters of traces enqueued back to back (no host read between
+    them, as the bench's timed steps run) summed on the device, over every device of a list; equal
+    to the per-trace counters read one by one; reset zeroes them."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot", 48, 27)
+    frames = [(3, 0), (1, 3), (5, 4)]  # a one-sample frame runs the megakernel: counted too
+    with NativeContext(a, seed=SEED, devices=devices) as one:
+        want = np.zeros(16)
+        for spp, base in frames:
+            one.trace_accumulate(spp, base)
+            want += one.ray_counts()
+    with NativeContext(a, seed=SEED, devices=devices) as c:
+        c.trace_accumulate(2, 100)
+        c.ray_counts_total(reset=True)
+        for spp, base in frames:
+            c.accum_clear()
+            c.trace_accumulate(spp, base)
+        got = c.ray_counts_total(reset=True)
+        assert np.array_equal(got[:3], want[:3]) and got[3] == got[0]
+        assert not np.any(c.ray_counts_total(reset=False)[:3])

@@ -7,6 +7,8 @@ adds a pixel's samples in sample order like the oracle. The one exception is the
 more than one sample per pixel, which adds a pixel's paths with FP64 atomics in arrival order:
 within 1e-12 there (and inside north_star's 1e-4 per-channel RMSE gate, asserted too).
 """
+import os
+
 import numpy as np
 import pytest
 
@@ -285,3 +287,27 @@ def test_colored_and_gray_light_records(gpu, oracle, monkeypatch, name):
     assert np.array_equal(out[0][0], out[1][0])
     assert all(np.array_equal(x, y) for x, y in zip(out[0][1], out[1][1]))
     assert np.array_equal(out[0][0], oracle.OracleScene(g).sample(5, SEED, sample_base=0))
+
+
+@pytest.mark.parametrize("name", ["spot", "renault", "cube_cornell", "two_spheres_plane"])
+def test_shadow_subpackets_answer_like_single_rays(gpu, oracle, monkeypatch, name):
+    """The 16-lane sub-packet any-hit experiment (anyhit_packet16_kernel, MFX_ANYHIT_PACKET=16):
+    first-vertex shadow rays in k_shadow's tile order and random rays, every answer the per-lane
+    kernel's and the oracle's."""
+    import sys as _sys
+    from conftest import ROOT
+    _sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    from shadow_packets import tile_shadow_rays
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, 96, 54)
+    rng = np.random.default_rng(5)
+    with NativeContext(a) as ctx:
+        srays, tmax = tile_shadow_rays(ctx, a, 2)
+        rr = random_rays(a, 4000, rng)
+        srays = np.concatenate([srays, rr])
+        tmax = np.concatenate([tmax, rng.uniform(0.1, 5.0, len(rr))])
+        single = ctx.any_hit(srays, tmax)
+        monkeypatch.setenv("MFX_ANYHIT_PACKET", "16")
+        packet = ctx.any_hit(srays, tmax)
+    assert np.array_equal(single, packet), (single != packet).sum()
+    assert np.array_equal(single, oracle.OracleScene(a).any_hit(srays, tmax))
