@@ -221,16 +221,6 @@ def aabb_selftest(rec: np.ndarray, device: int = 0):
     return out[:, 0], out[:, 1], out[:, 2]
 
 
-def tri_screen_selftest(rec: np.ndarray, device: int = 0):
-    """(FP64 Triangle.Hit hit, its t, the FP32 screen's skip) for n x 18 records
-    (mfx_tri_screen_selftest)."""
-    lib = load_library()
-    rec = np.ascontiguousarray(rec, dtype=np.float64).reshape(-1, 18)
-    out = np.zeros((len(rec), 3))
-    check(lib.mfx_tri_screen_selftest(device, len(rec), dptr(rec), dptr(out)), "mfx_tri_screen_selftest")
-    return out[:, 0].astype(bool), out[:, 1], out[:, 2].astype(bool)
-
-
 # ---- the reference's object model -----------------------------------------------------------
 class Film:
     """Film (Film.fs:13-34): progressive accumulation; here the accumulator lives on the GPU."""

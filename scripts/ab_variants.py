@@ -22,7 +22,8 @@ res = []
 for k in range(STEPS + 1):
     ctx.accum_clear(); t = time.perf_counter(); ctx.trace_accumulate(SPP, k * SPP); ctx.sync(); dt = time.perf_counter() - t
     c = ctx.ray_counts(); ms = ctx.last_trace_ms(); tt = ctx.trace_timing()
-    if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms, tt["total_ms"] - tt["extend_ms"] - tt["shadow_ms"]))
+    if k: res.append(((c[0] + c[1] + c[2]) / dt / 1e6, ms, tt["total_ms"] - tt["extend_ms"] - tt["shadow_ms"],
+                      tt["camera_ms"], tt["extend_ms"] - tt["camera_ms"], tt["shadow_ms"]))
 st = {}
 if os.environ.get("MFX_AB_STATS") == "1":  # per-ray traversal work of one sample (per-lane camera rays)
     os.environ["MFX_CAMERA_PACKETS"] = "0"
@@ -30,7 +31,8 @@ if os.environ.get("MFX_AB_STATS") == "1":  # per-ray traversal work of one sampl
     cs.trace_accumulate(1, 0); cs.sync(); c = cs.ray_counts()
     st = {"nodes/closest": c[4] / (c[0] + c[1]), "leaves/closest": c[5] / (c[0] + c[1]), "prims/closest": c[6] / (c[0] + c[1]),
           "nodes/shadow": c[7] / max(c[2], 1), "leaves/shadow": c[8] / max(c[2], 1), "prims/shadow": c[9] / max(c[2], 1)}
-print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest": [r[2] for r in res], "stats": st}))
+print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest": [r[2] for r in res],
+                  "stage": [[r[3], r[4], r[5]] for r in res], "stats": st}))
 '''
 
 
@@ -58,7 +60,8 @@ def main():
             d = json.loads(p.stdout.strip().splitlines()[-1])
             out[os.path.basename(l)] += d["mrays"]
             print(os.path.basename(l), "round", r, ["%.1f" % x for x in d["mrays"]], "ms", ["%.2f" % x for x in d["ms"]],
-                  "rest ms (resolve + memsets)", ["%.3f" % x for x in d.get("rest", [])], flush=True)
+                  "rest ms (resolve + memsets)", ["%.3f" % x for x in d.get("rest", [])],
+                  "camera/extend/shadow ms", ["/".join("%.2f" % y for y in x) for x in d.get("stage", [])], flush=True)
             if d.get("stats"):
                 print(os.path.basename(l), "stats", {k: round(v, 3) for k, v in d["stats"].items()}, flush=True)
     print("SUMMARY", json.dumps({k: (max(v) if v else None) for k, v in out.items()}))
