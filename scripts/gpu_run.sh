@@ -10,6 +10,7 @@
 #   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   inflight             scripts/frames_in_flight.py: one context vs two frames in flight on two streams
 #   subpk:SCENE          scripts/shadow_packets.py under rocprofv3: per-lane vs 16-lane sub-packet any-hit kernels
 #   vparity              scripts/variant_parity.py: every build_variants/*.so bit-exact vs the oracle
 #   overlap              scripts/overlap_probe.py: exchange kernels / copies beside the persistent trace
@@ -58,6 +59,9 @@ for step in "$@"; do
         timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
+    inflight)
+      timeout -k 10 300 python3 scripts/frames_in_flight.py > $O/inflight.json 2> $O/inflight.err
+      cat $O/inflight.json ;;
     subpk)
       D=$R/$O/subpk_$a1
       mkdir -p $D
