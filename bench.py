@@ -231,7 +231,7 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
                         "to pageable host memory, synchronize"}
 
 
-def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=4, flags=0):
+def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
     """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
     measured on this GPU: rank r traces all `spp` samples of the film's tile rows r mod N
     (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
@@ -243,7 +243,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=4, flags=0):
     exchange not overlapped (the bench overlaps it with the next frame's trace; not counted here)."""
     import torch
     from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
-    from mafrixraytracing_amd.distributed import RowGather
+    from mafrixraytracing_amd.distributed import RowGather, frames_in_flight
     from mafrixraytracing_amd.native import NativeContext
     W, H = arrays.width, arrays.height
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda")
@@ -284,21 +284,32 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=4, flags=0):
     for n in (2, 4, 8):
         rank_ms, rank_rays = [], []
         ov = None
+        nif = frames_in_flight(W, H, spp, n)  # the bench's rank alternates its frames over nif contexts
         for r in range(n):
-            with NativeContext(arrays, seed=seed, flags=flags | MFX_F_ROW_PARTITION, part_index=r, part_count=n) as ctx:
-                ctx.trace_accumulate(spp, 0)  # the pool's first allocation, untimed
-                ctx.sync()
-                ctx.ray_counts_total(reset=True)
-                t0 = time.perf_counter()
-                for k in range(steps):  # back to back, as the bench's steps run
-                    ctx.accum_clear()
-                    ctx.trace_accumulate(spp, (k + 1) * spp)
-                ctx.sync()
-                rank_ms.append((time.perf_counter() - t0) / steps * 1e3)
-                c = ctx.ray_counts_total(reset=True)
-                rank_rays.append((c[0] + c[1] + c[2]) / steps)
-                if r == 0:
-                    ov = overlap(ctx, RowGather(acc, W, H, 0, n))
+            cs = [NativeContext(arrays, seed=seed, flags=flags | MFX_F_ROW_PARTITION, part_index=r, part_count=n)
+                  for _ in range(nif)]
+            for c in cs:
+                c.trace_accumulate(spp, 0)  # the pool's first allocation, untimed
+            for c in cs:
+                c.sync()
+                c.ray_counts_total(reset=True)
+            t0 = time.perf_counter()
+            for k in range(steps):  # back to back, as the bench's steps run
+                c = cs[k % nif]
+                c.accum_clear()
+                c.trace_accumulate(spp, (k + 1) * spp)
+            for c in cs:
+                c.sync()
+            rank_ms.append((time.perf_counter() - t0) / steps * 1e3)
+            rays = 0.0
+            for c in cs:
+                t = c.ray_counts_total(reset=True)
+                rays += t[0] + t[1] + t[2]
+            rank_rays.append(rays / steps)
+            if r == 0:
+                ov = overlap(cs[0], RowGather(acc, W, H, 0, n))
+            for c in cs:
+                c.close()
         g0 = RowGather(acc, W, H, 0, n)
         t_pack = timed(lambda: g0.pack(acc))  # rank 0 holds the most rows: the largest pack
         t_unpack = timed(lambda: g0.unpack(acc))
@@ -306,7 +317,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=4, flags=0):
         t_rank = max(rank_ms)
         t_ex = t_pack + t_xfer + t_unpack
         job_rays = sum(rank_rays)
-        out[str(n)] = {"film_share_per_gpu": round(1.0 / n, 6), "spp_per_gpu": spp,
+        out[str(n)] = {"film_share_per_gpu": round(1.0 / n, 6), "spp_per_gpu": spp, "frames_in_flight": nif,
                        "rank_ms_per_step": [round(t, 3) for t in rank_ms],
                        "slowest_rank_ms": round(t_rank, 3),
                        "imbalance": round(t_rank / (sum(rank_ms) / n), 4),
@@ -366,7 +377,7 @@ def main():
     import numpy as np
     from mafrixraytracing_amd.abi import (MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE, MFX_F_ROW_PARTITION,
                                           MFX_F_WAVEFRONT)
-    from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, step_spp
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, frames_in_flight, step_spp
     from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
 
@@ -393,6 +404,17 @@ def main():
             devices = [int(os.environ["MFX_BENCH_DEVICE"])] * args.gpus
     ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank, part_count=world,
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
+    # one process per GPU: a rank whose frame is small (its share at 4+ GPUs) alternates its frames
+    # over two contexts, two frames in flight (distributed.frames_in_flight)
+    nif = frames_in_flight(W, H, spp_step, world, rows) if use_dist and args.api == "batch" else 1
+    ctxs = [ctx] + [NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank,
+                                  part_count=world) for _ in range(nif - 1)]
+
+    def totals():  # the timed steps' rays, summed on the device over this rank's contexts
+        t = np.zeros(16)
+        for c in ctxs:
+            t += c.ray_counts_total(reset=True)
+        return t
     pr = None
     if use_dist:
         # two attached accumulators: frame k's exchange runs while frame k + 1 traces. The image
@@ -400,16 +422,17 @@ def main():
         # tensors) has no CUDA gather, so there the rows merge by all_reduce (an exact sum too)
         accs = [torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}") for _ in range(2)]
         gathers = [RowGather(a, W, H, rank, world) for a in accs] if rows and backend != "gloo" else None
-        pr = PipelinedNativeRender(ctx, accs, rank, world, gathers=gathers)
+        pr = PipelinedNativeRender(ctxs, accs, rank, world, gathers=gathers)
     rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
         if pr is not None:
-            pr.drain()  # every frame's reduce has finished
+            pr.drain()  # every frame's exchange has finished
         if use_dist:
             dist.barrier()
             torch.cuda.synchronize()
-        ctx.sync()
+        for c in ctxs:
+            c.sync()
 
     def step(k):
         base = k * spp_step
@@ -428,7 +451,7 @@ def main():
     for k in range(args.warmup):
         step(k)
     barrier()
-    ctx.ray_counts_total(reset=True)  # the timed steps' rays: device-side totals, read after the final barrier
+    totals()  # the timed steps' rays: device-side totals, read after the final barrier
     t0 = time.perf_counter()
     rays = 0.0
     closest_rays = 0.0
@@ -453,7 +476,7 @@ def main():
     if args.api == "render":
         elapsed = call_s
     else:
-        c = ctx.ray_counts_total(reset=True)  # every timed step's counters, summed on the device
+        c = totals()  # every timed step's counters, summed on the device
         rays, closest_rays, primary_rays = c[0] + c[1] + c[2], c[0] + c[1], c[0]
         # per-stage device times (HIP events around each launch) from two more steps of the same
         # workload, each read after it (the timed steps above carry no per-step host read)
@@ -480,25 +503,35 @@ def main():
         # one (the config's spp split over the GPUs)
         o_scaling = "weak" if args.scaling == "strong" else "strong"
         o_spp = step_spp(args.spp, ngpu, o_scaling)
+        po = pr
+        if pr is not None:  # the other job's frames in flight, by its own frame size
+            pr.drain()
+            o_nif = frames_in_flight(W, H, o_spp, world, rows)
+            po = PipelinedNativeRender(ctxs[:o_nif], accs, rank, world, gathers=gathers)
 
         def other_step(k):
             base = (args.warmup + args.steps) * spp_step + k * o_spp
-            if pr is not None:
-                pr.frame(o_spp, base, all_ranks=backend == "gloo")
+            if po is not None:
+                po.frame(o_spp, base, all_ranks=backend == "gloo")
             else:
                 ctx.accum_clear()
                 ctx.trace_accumulate(o_spp, base)
                 ctx.accum_reduce()
         other_step(0)
+        if po is not None:
+            po.drain()
         barrier()
-        ctx.ray_counts_total(reset=True)
+        totals()
         ts = time.perf_counter()
         for k in range(args.steps):
             other_step(1 + k)
+        if po is not None:
+            po.drain()
         barrier()
-        c = ctx.ray_counts_total(reset=True)
+        c = totals()
         o_el, o_rays = job_max_sum(time.perf_counter() - ts, c[0] + c[1] + c[2])
         other = {"scaling": o_scaling, "global_spp_per_step": o_spp,
+                 "frames_in_flight": frames_in_flight(W, H, o_spp, world, rows) if use_dist else 1,
                  "spp_per_gpu": o_spp if rows else o_spp / ngpu,
                  "film_share_per_gpu": round(1.0 / ngpu, 6) if rows else 1.0,
                  "value": round(o_rays / o_el / 1e6, 2), "unit": "Mrays/s", "steps": args.steps,
@@ -770,6 +803,7 @@ def main():
                        "scene": os.path.relpath(args.scene, ROOT), "width": W, "height": H,
                        "spp_per_gpu": per_gpu, "global_spp_per_step": spp_step, "max_depth": 3,
                        "film_share_per_gpu": round(1.0 / ngpu, 6) if image_part else 1.0,
+                       "frames_in_flight": nif,
                        "pipeline": "megakernel" if args.megakernel else "wavefront", "api": api,
                        "parallelism": par},
             "roofline": roofline, "render_api": rapi, "sample_api": sapi, "strong_share": share, "cpu_baseline": cpu,
@@ -777,7 +811,8 @@ def main():
         if other is not None:
             result[other["scaling"]] = other
         print(json.dumps(result), file=json_out, flush=True)
-    ctx.close()
+    for c in ctxs:
+        c.close()
     if use_dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -176,27 +176,43 @@ def native_partitioned_render(ctx, acc, rank: int, world: int, exchange: Callabl
                              clear_fn=ctx.accum_clear, sync_fn=ctx.sync, after_reduce=sync_torch, exchange=exchange)
 
 
+def frames_in_flight(width: int, height: int, spp: int, world: int, rows: bool = True) -> int:
+    """Contexts a rank alternates frames over: 2 when its frame is at most 2^25 paths (one rank's
+    image-partition share at 4 or more GPUs), else 1. Every persistent launch fills the GPU, so a
+    second context's launches (its own pool and stream) take CUs as the first one's blocks retire:
+    the next frame's dense launches fill the previous frame's tails. Measured on C2
+    (profiles/r05/r05i_frames_in_flight.json): a 1/8 share +8.5 %, 1/4 +2.3 %, 1/2 -2 %, the whole
+    film -4 % (two frames' working sets in one L2)."""
+    tr = (height + 7) // 8
+    rows_per_rank = -(-tr // world) if rows else tr
+    paths = ((width + 7) // 8) * rows_per_rank * 64 * spp
+    return 2 if paths <= (1 << 25) else 1
+
+
 class PipelinedNativeRender:
     """Frames over two attached accumulators, so a frame's exchange overlaps the next frame's trace:
-    frame k traces into accs[k % 2] on the context's HIP stream; torch's stream waits for that trace
-    (an event on the context stream, no host sync) and runs the exchange — a RowGather per buffer
-    (image partition) or the sum-reduce; frame k + 2 reuses the buffer only after that exchange has
-    finished (an event on torch's stream, waited on the host just before the buffer is cleared, while
-    the GPU is still tracing frame k + 1). Each frame is the same clear / trace / exchange as
-    PartitionedRender.frame; only the waits move. drain() waits for every outstanding exchange;
-    `buffer(k)` is where frame k's merged accumulator lands (on rank 0)."""
+    frame k traces into accs[k % 2] on the HIP stream of context ctxs[k % len(ctxs)]; torch's stream
+    waits for that trace (an event on the context stream, no host sync) and runs the exchange — a
+    RowGather per buffer (image partition) or the sum-reduce; frame k + 2 reuses the buffer only
+    after that exchange has finished (an event on torch's stream, waited on the host just before the
+    buffer is cleared, while the GPU is still tracing frame k + 1). With two contexts (two pools, two
+    streams: frames_in_flight) frame k + 1's trace runs beside frame k's. Each frame is the same
+    clear / trace / exchange as PartitionedRender.frame; only the waits move. drain() waits for every
+    outstanding exchange; `buffer(k)` is where frame k's merged accumulator lands (on rank 0)."""
 
     def __init__(self, ctx, accs, rank: int, world: int, gathers: list | None = None):
         import torch
-        self.ctx = ctx
+        self.ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
+        assert len(self.ctxs) in (1, 2)
+        self.ctx = self.ctxs[0]
         self.accs = list(accs)
         assert len(self.accs) == 2 and all(a.is_cuda for a in self.accs)
         self.gathers = gathers
         assert gathers is None or len(gathers) == 2
         self.rank, self.world = rank, world
-        self.multi = len(getattr(ctx, "devices", [0])) > 1
+        self.multi = len(getattr(self.ctx, "devices", [0])) > 1
         self.device = self.accs[0].device
-        self.ctx_stream = torch.cuda.ExternalStream(ctx.stream(), device=self.device)
+        self.ctx_streams = [torch.cuda.ExternalStream(c.stream(), device=self.device) for c in self.ctxs]
         self.pending = [None, None]
         self.k = 0
 
@@ -212,16 +228,18 @@ class PipelinedNativeRender:
         import torch
         import torch.distributed as dist
         i = self.k % 2
+        ci = self.k % len(self.ctxs)
         self.k += 1
         acc = self.accs[i]
+        ctx = self.ctxs[ci]
         self._wait(i)  # frame k - 2's exchange has read this buffer
-        self.ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
-        self.ctx.accum_clear()
-        self.ctx.trace_accumulate(spp, sample_base)
+        ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
+        ctx.accum_clear()
+        ctx.trace_accumulate(spp, sample_base)
         if self.multi:
-            self.ctx.accum_reduce()
+            ctx.accum_reduce()
         traced = torch.cuda.Event()
-        traced.record(self.ctx_stream)
+        traced.record(self.ctx_streams[ci])
         cur = torch.cuda.current_stream(self.device)
         cur.wait_event(traced)
         if self.gathers is not None:
@@ -242,8 +260,10 @@ class PipelinedNativeRender:
     def drain(self):
         for i in (0, 1):
             self._wait(i)
-        self.ctx.sync()
+        for c in self.ctxs:
+            c.sync()
 
     def close(self):
         self.drain()
-        self.ctx.accum_attach(None)
+        for c in self.ctxs:
+            c.accum_attach(None)

@@ -46,12 +46,12 @@ def main():
     from mafrixraytracing_amd.scene_io import load_scene_file
     arr = load_scene_file(a.scene)
     out = {"scene": os.path.basename(a.scene), "spp": a.spp, "steps": a.steps}
-    for parts in (1, 8):
+    for parts in (1, 2, 4, 8):
         kw = dict(flags=MFX_F_ROW_PARTITION, part_index=0, part_count=parts) if parts > 1 else {}
         row = {}
         for inflight in (1, 2, 1, 2):  # interleaved
             ctxs = [NativeContext(arr, seed=DEFAULT_SEED, **kw) for _ in range(inflight)]
-            ms, rays = run(ctxs, a.spp, a.steps * (1 if parts == 1 else 4))
+            ms, rays = run(ctxs, a.spp, a.steps * max(1, parts // 2))
             for c in ctxs:
                 c.close()
             r = row.setdefault(str(inflight), {"ms_per_frame": [], "rays_per_frame": rays})

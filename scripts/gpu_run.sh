@@ -10,6 +10,7 @@
 #   td:CFG               TD roof PMC pass of the bench step and the td_gather peak (pmc_td_roof.sh)
 #   pmc:CFG              the TD / TCP / SQ counter groups (pmc_td.sh)
 #   ab:ROUNDS:SPP:SCENES A/B of build_variants/*.so (ab_variants.py), SCENES comma-separated
+#   rehearse:N           bench.py under torchrun with N ranks all on device 0 over gloo (the driver's launch)
 #   inflight             scripts/frames_in_flight.py: one context vs two frames in flight on two streams
 #   subpk:SCENE          scripts/shadow_packets.py under rocprofv3: per-lane vs 16-lane sub-packet any-hit kernels
 #   vparity              scripts/variant_parity.py: every build_variants/*.so bit-exact vs the oracle
@@ -59,6 +60,13 @@ for step in "$@"; do
         timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
+    rehearse)
+      # the driver's N-rank launch on this one GPU: every rank on device 0, gloo (RCCL refuses two
+      # ranks on one device); a rehearsal of the code path, not a scaling figure
+      MFX_BENCH_DEVICE=0 MFX_BENCH_BACKEND=gloo timeout -k 10 600 python3 -m torch.distributed.run --nnodes=1 \
+        --nproc-per-node=$a1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus $a1 --no-cpu-baseline \
+        --no-stats --steps 5 --warmup 1 > $O/rehearse_$a1.json 2> $O/rehearse_$a1.err
+      python3 -c "import json; d=json.load(open('$O/rehearse_$a1.json')); print('rehearse', d['n_gpus'], d['scaling'], d['value'], d['config']['global_spp_per_step'], d['config']['frames_in_flight'])" ;;
     inflight)
       timeout -k 10 300 python3 scripts/frames_in_flight.py > $O/inflight.json 2> $O/inflight.err
       cat $O/inflight.json ;;

@@ -51,7 +51,8 @@ def _plain_accumulators(name, frames, part_index=0, part_count=1):
     return out
 
 
-def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False):
+def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False,
+                 two_ctx=False):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
@@ -68,12 +69,14 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
     gather = rows and backend == "nccl"  # (gloo has no CUDA gather: rows merge by all_reduce there)
     with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world,
-                       flags=MFX_F_ROW_PARTITION if rows else 0) as ctx:
+                       flags=MFX_F_ROW_PARTITION if rows else 0) as ctx, \
+            NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world,
+                          flags=MFX_F_ROW_PARTITION if rows else 0) as ctx2:
         got = []
         if pipelined:  # back to back, no waits between frames; the last two buffers checked after drain
             acc1 = torch.zeros_like(acc)
             gs = [RowGather(b, W, H, rank, world) for b in (acc, acc1)] if gather else None
-            pr = PipelinedNativeRender(ctx, [acc, acc1], rank, world, gathers=gs)
+            pr = PipelinedNativeRender([ctx, ctx2] if two_ctx else ctx, [acc, acc1], rank, world, gathers=gs)
             for spp, base in frames:
                 pr.frame(spp, base, all_ranks=all_ranks)
             pr.drain()
@@ -92,10 +95,10 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False):
+def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False, two_ctx=False):
     import torch.multiprocessing as mp
     mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks,
-                                           pipelined, rows),
+                                           pipelined, rows, two_ctx),
                        nprocs=world, join=True, start_method="spawn")
     return np.load(os.path.join(outdir, "frames.npy"))
 
@@ -131,6 +134,15 @@ def test_world1_nccl_row_gather_bit_identical(gpu, tmp_path, pipelined):
     want = _plain_accumulators("spot", FRAMES)
     ks = range(len(FRAMES) - 2, len(FRAMES)) if pipelined else range(len(FRAMES))
     for i, k in enumerate(ks):
+        assert np.array_equal(got[i], want[k]), k
+
+
+def test_world1_nccl_two_frames_in_flight(gpu, tmp_path):
+    """Frames alternating over two contexts (two pools, two streams: frames_in_flight), row gather,
+    pipelined: the last two buffers equal the plain context's accumulators bit for bit."""
+    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False, pipelined=True, rows=True, two_ctx=True)
+    want = _plain_accumulators("spot", FRAMES)
+    for i, k in enumerate(range(len(FRAMES) - 2, len(FRAMES))):
         assert np.array_equal(got[i], want[k]), k
 
 
