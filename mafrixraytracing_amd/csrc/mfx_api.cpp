@@ -671,7 +671,7 @@ int mfx_build_instanced_info(const mfx_scene_desc* scene, const mfx_instance* in
 void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 
 // Allocate (or grow) the wavefront path-slot pool (SoA). queues: the trace runs ray queues
-// (MFX_RAY_QUEUE), whose arrays (7 doubles and 7 words per slot) are allocated only then.
+// (MFX_RAY_QUEUE), whose arrays (6 doubles and 7 words per slot) are allocated only then.
 static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     if (pool <= c->wf_pool && (!queues || c->wf_pool_q)) return MFX_OK;
     if (c->wf_mem) (void)hipFree(c->wf_mem);
@@ -692,23 +692,20 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     c->wf.vls = (double*)take(P * 8 * 2 * nv);
     c->wf.vmat = (WfMat*)take(P * sizeof(WfMat) * nv);
     c->wf.vstride = (int64_t)P;
-    c->wf.key = (uint64_t*)take(P * 8);
     c->wf.rn = (uint32_t*)take(P * 4);
     c->wf.depth = (int32_t*)take(P * 4);
     c->wf.state = (int32_t*)take(P * 4);
 #if MFX_RAY_QUEUE
     if (queues) {
-    // queue 0: its own arrays; queue 1: the pool's ray arrays (o, d, key, rn: dead once the
+    // queue 0: its own arrays; queue 1: the pool's ray arrays (o, d, rn: dead once the
     // iterations run on queues) and its own depth, state and slot words
     WfQueue& q0 = c->wq[0];
     double** q0d[6] = {&q0.ox, &q0.oy, &q0.oz, &q0.dx, &q0.dy, &q0.dz};
     for (double** d : q0d) *d = (double*)take(P * 8);
-    q0.key = (uint64_t*)take(P * 8);
     q0.rn = (uint32_t*)take(P * 4);
     WfQueue& q1 = c->wq[1];
     q1.ox = c->wf.ox; q1.oy = c->wf.oy; q1.oz = c->wf.oz;
     q1.dx = c->wf.dx; q1.dy = c->wf.dy; q1.dz = c->wf.dz;
-    q1.key = c->wf.key;
     q1.rn = c->wf.rn;
     for (WfQueue* q : {&q0, &q1}) {
         q->depth = (int32_t*)take(P * 4);
@@ -730,7 +727,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
 static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
     const WfParams& A = c->wf;
     P.ox = A.ox; P.oy = A.oy; P.oz = A.oz; P.dx = A.dx; P.dy = A.dy; P.dz = A.dz;
-    P.key = A.key; P.rn = A.rn; P.depth = A.depth; P.state = A.state;
+    P.rn = A.rn; P.depth = A.depth; P.state = A.state;
     P.fstate = A.state;
     P.qslot = nullptr;
     P.qcount = nullptr;
@@ -740,14 +737,14 @@ static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
     if (d > q) {
         const WfQueue& R = c->wq[(d - q - 1) & 1];
         P.ox = R.ox; P.oy = R.oy; P.oz = R.oz; P.dx = R.dx; P.dy = R.dy; P.dz = R.dz;
-        P.key = R.key; P.rn = R.rn; P.depth = R.depth; P.state = R.state;
+        P.rn = R.rn; P.depth = R.depth; P.state = R.state;
         P.qslot = R.slot;
         P.qcount = R.count;
     }
     if (d >= q && d < P.max_depth) {
         const WfQueue& N = c->wq[(d - q) & 1];
         P.nox = N.ox; P.noy = N.oy; P.noz = N.oz; P.ndx = N.dx; P.ndy = N.dy; P.ndz = N.dz;
-        P.nkey = N.key; P.nrn = N.rn; P.ndepth = N.depth; P.nstate = N.state; P.nslot = N.slot;
+        P.nrn = N.rn; P.ndepth = N.depth; P.nstate = N.state; P.nslot = N.slot;
         P.ncount = N.count;
     }
 }
@@ -764,6 +761,7 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     // a gray light (bitwise equal intensities): k_shadow records a lit vertex's direct term itself
     P.gray_light = std::memcmp(&P.light.color[0], &P.light.color[1], sizeof(double)) == 0 &&
                    std::memcmp(&P.light.color[0], &P.light.color[2], sizeof(double)) == 0 && !getenv("MFX_NO_GRAY_LIGHT");
+    P.lit_in_hit = c->host.max_depth <= 3 && c->host.shade.size() <= ((size_t)1 << 25) && !getenv("MFX_NO_LIT_IN_HIT");
     P.accum = c->d_accum;
     P.albedo = c->d_albedo;
     P.nmat = (int32_t)(c->host.albedo.size() / 3);

@@ -116,16 +116,18 @@ struct WfParams {
     int32_t gray_light;    // 1: the light's three intensities are bitwise equal, so a_v = (cs * (solid * I)) /
                            // pdf_li is one value for every channel: k_shadow records it (one double, one
                            // store) and k_resolve reads it instead of cs and solid (the same expression)
+    int32_t lit_in_hit;    // 1 (max_depth <= 3, shade indices < 2^25): in place, a HIT state word carries the
+                           // path's lit mask in bits 29..31 and k_shadow takes the remaining depth from the
+                           // iteration, so no depth word is written or read in place
     int64_t vstride;       // slots per vertex-record row (the allocated pool)
     const double* albedo;  // [nmat][3] Lambert albedo per material (Material.fs:29-37)
     int32_t nmat;
-    uint64_t* key;         // RNG key of the path
     uint32_t* rn;          // RNG draws used so far
     int32_t* depth;        // remaining depth (PathIntegrator's d)
     int32_t* state;
     // Ray queues (MFX_RAY_QUEUE; null: every iteration works on the slot pool in place). From the
     // second iteration on, the arrays above are a queue's: entry i holds a continuing path's ray,
-    // key, draw count, depth word and state, and qslot[i] names its slot, which keeps the path's
+    // draw count, depth word and state, and qslot[i] names its slot, which keeps the path's
     // vertex records (vei, vmat, vls) and its final state word (fstate, with the lit mask: what
     // k_resolve reads). k_shadow appends the paths that continue to the next queue (n*), so the
     // sparse later bounces read and write dense memory instead of scattered slots.
@@ -133,7 +135,6 @@ struct WfParams {
     const unsigned long long* qcount; // [WF_SHARDS * WF_HS] entries of each shard range of this iteration's queue (null: the pool)
     int32_t* fstate;                  // the slot pool's state words (== state in place)
     double *nox, *noy, *noz, *ndx, *ndy, *ndz;  // the next queue (null: continue in place)
-    uint64_t* nkey;
     uint32_t* nrn;
     int32_t *ndepth, *nstate, *nslot;
     unsigned long long* ncount;       // [WF_SHARDS * WF_HS] its counts (beside ctl; zeroed with the heads)
@@ -169,15 +170,15 @@ struct WfParams {
 #ifndef MFX_RAY_QUEUE
 #define MFX_RAY_QUEUE 1  // continuing paths move to dense ray queues after the first vertex (MFX_RAY_QUEUE=0 at run time: in place)
 #endif
-// 8-byte and 4-byte words per slot in the SoA pool: o, d, key, and per vertex ei, cs, solid (8 B)
-// and the material (4 B); with ray queues, two queues of o, d, key (8 B) and rn, depth, state,
-// slot (4 B) per slot
-// (queue 0 its own o, d, key, rn, depth, state, slot; queue 1 reuses the pool's o, d, key and rn,
-// dead after the pool's last iteration, plus its own depth, state and slot)
-#define WF_DOUBLES_PER_SLOT(nvert) (7 + 3 * (nvert) + (MFX_RAY_QUEUE ? 7 : 0))
+// 8-byte and 4-byte words per slot in the SoA pool: o, d, and per vertex ei, cs, solid (8 B) and
+// the material (4 B); with ray queues, two queues of o, d (8 B) and rn, depth, state, slot (4 B)
+// per slot (queue 0 its own o, d, rn, depth, state, slot; queue 1 reuses the pool's o, d and rn,
+// dead after the pool's last iteration, plus its own depth, state and slot). No RNG key is
+// stored: k_shadow derives it from the path's slot at every vertex.
+#define WF_DOUBLES_PER_SLOT(nvert) (6 + 3 * (nvert) + (MFX_RAY_QUEUE ? 6 : 0))
 #define WF_WORDS_PER_SLOT(nvert) (3 + (nvert) + (MFX_RAY_QUEUE ? 7 : 0))  // rn, depth, state + the vertices' materials
-// the two ray queues' share of that (queue 0's ray, key and draw count; both queues' depth, state and slot)
-#define WF_QUEUE_BYTES_PER_SLOT (MFX_RAY_QUEUE ? 7 * 8 + 7 * 4 : 0)
+// the two ray queues' share of that (queue 0's ray and draw count; both queues' depth, state and slot)
+#define WF_QUEUE_BYTES_PER_SLOT (MFX_RAY_QUEUE ? 6 * 8 + 7 * 4 : 0)
 
 #ifndef WF_STACK_LDS
 #define WF_STACK_LDS 16  // traversal stack entries per lane kept in LDS (deeper ones spill to HBM/L2)
@@ -201,7 +202,6 @@ hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu);
 // a ray queue's arrays (MFX_RAY_QUEUE): entries in the pool's shard ranges, counts per shard
 struct WfQueue {
     double *ox, *oy, *oz, *dx, *dy, *dz;
-    uint64_t* key;
     uint32_t* rn;
     int32_t *depth, *state, *slot;
     unsigned long long* count;  // [WF_SHARDS * WF_HS]

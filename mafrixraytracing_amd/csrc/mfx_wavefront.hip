@@ -321,9 +321,9 @@ struct PendShd {
     }
 };
 
-// k_shadow derives a camera ray's path key from its slot (as k_extend did) instead of reading it:
-// k_extend stores no keys, and only continuing paths get theirs stored, at their first vertex
-// (r02bs: C2 +0.9 to +2.5 %, C3 +2.5 to +4.3 %; derived at every vertex, r03av: -0.3 to -1.2 %)
+// k_shadow derives a path's key from its slot (as k_extend did for the camera ray) at every vertex:
+// no key is stored (r02bs: derived at the first vertex, C2 +0.9 to +2.5 %; at every vertex, r03av:
+// -0.3 to -1.2 % then, r05m: C2 +0.5 %, Renault +0.7 % once the depth word was gone too)
 #ifndef MFX_HEMI_WAVE_FIRST
 #define MFX_HEMI_WAVE_FIRST 1  // trials each owner makes alone before the wave shares them (r02bi: 1 vs 2, C3 +0.8 %, C4 +0.6 %, C2 -0.5 %)
 #endif
@@ -521,7 +521,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
             o = ld3(CAM.position);
             d = vnormalize(vsub(target, o));
             // throughput 1, radiance 0, rn 2 and depth max_depth stay implicit (WF_FRESH); the
-            // key is derived again by k_shadow (stored only for a path that continues)
+            // key is derived again by k_shadow
         } else {
             o = dv(P.ox[s], P.oy[s], P.oz[s]);
             d = dv(P.dx[s], P.dy[s], P.dz[s]);
@@ -537,7 +537,9 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         if (T.B.found) {
             const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
             P.ox[s] = hp.x; P.oy[s] = hp.y; P.oz[s] = hp.z;
-            P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl;
+            // in place (lit_in_hit): the path's lit mask rides in bits 29..31 for k_shadow
+            const int lm = (P.lit_in_hit && lit_in_entry && !fresh) ? ((se >> 28) & 7) << 29 : 0;
+            P.state[s] = ((T.B.info & MFX_INFO_SHADE_MASK) << WF_SHADE_SHIFT) | WF_HIT | fl | lm;
         } else {  // a later miss finishes the path: its lit mask goes into the state word
             const int lm = fresh || Q ? 0 : (lit_in_entry ? (se >> 28) & 7 : (P.depth[s] >> WF_LIT_SHIFT) & 0xffff);
             P.state[s] = WF_MISS | (lm << WF_SHADE_SHIFT) | fl;
@@ -767,8 +769,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
-                        shl[r] = (sv & WF_FRESH) ? (j | (int)0x80000000) : j;  // sign bit: first vertex
-                        shl[WF_SHD_LIST + r] = (int)((unsigned)sj >> WF_SHADE_SHIFT);
+                        // sign bit: first vertex; lit_in_hit: the lit mask in bits 28..30 (slots < 2^28)
+                        const bool lh = P.lit_in_hit && !(Q && P.qslot);
+                        shl[r] = (sv & WF_FRESH) ? (j | (int)0x80000000) : (lh ? j | (int)(((unsigned)sj >> 29) << 28) : j);
+                        shl[WF_SHD_LIST + r] = (int)(((unsigned)sj >> WF_SHADE_SHIFT) & (lh ? 0x1ffffffu : 0x0fffffffu));
                     }
                     nshade += __popcll(hm);
                     sc.advance(P.state);
@@ -786,25 +790,30 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 uint64_t key = 0;
                 uint32_t rn = 0;
                 if (own) {
-                    j = shl[lane] & 0x7fffffff;
+                    j = shl[lane] & WF_ENTRY_SLOT;
                     first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
                     const int slot = shl[WF_SHD_LIST + lane];
                     jr = (Q && P.qslot) ? P.qslot[j] : j;
-                    dw = first ? P.max_depth : P.depth[j];  // remaining depth | lit mask << 8
+                    // remaining depth | lit mask << 8: in place with lit_in_hit, the iteration's and
+                    // the mask the state word carried; otherwise the depth word
+                    dw = first ? P.max_depth
+                               : ((P.lit_in_hit && !(Q && P.qslot))
+                                      ? (P.max_depth - P.iter) | ((((unsigned)shl[lane] >> 28) & 7) << WF_LIT_SHIFT)
+                                      : P.depth[j]);
                     hp = dv(P.ox[j], P.oy[j], P.oz[j]);
                     const MfxShade sh = P.shade[slot];
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
                     else nm = ld3(sh.n);
                     mat = sh.material;
-                    // the key k_extend derived for the path's camera ray (same expressions)
-                    if (first) {
+                    // the key k_extend derived for the path's camera ray (same expressions), derived
+                    // again at every vertex from the path's slot instead of stored (8 B written at the
+                    // first vertex and read at every later one: C2 +0.5 %, r05m)
+                    {
                         int x, y;
                         int64_t smp;
                         path_pixel(P, P.path_base + jr, x, y, smp);
                         const int64_t pixel = (int64_t)x * P.height + y;
                         key = path_key(P.seed, (uint64_t)pixel, (uint64_t)(P.sample_base + P.part_index + smp * P.part_count));
-                    } else {
-                        key = P.key[j];
                     }
                     rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
                 }
@@ -840,11 +849,9 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                                            // state are written after the shadow ray)
                         P.nox[qi] = hp.x; P.noy[qi] = hp.y; P.noz[qi] = hp.z;
                         P.ndx[qi] = wi.x; P.ndy[qi] = wi.y; P.ndz[qi] = wi.z;
-                        P.nkey[qi] = key;
                         P.nrn[qi] = rn;
                         P.nslot[qi] = jr;
                     } else if (cn) {  // what the next vertex reads, in place
-                        if (first) P.key[j] = key;
                         P.rn[j] = rn;
                         P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
                     }
@@ -949,7 +956,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             } else if (Q && (P.ncount || P.qslot)) {  // finished; the pool's slot keeps its final words
                 if (mask) P.fstate[P.qslot ? P.qslot[s] : s] = WF_DONE | (mask << WF_SHADE_SHIFT);
             } else {
-                if (cont) P.depth[s] = dwn;
+                if (cont && !P.lit_in_hit) P.depth[s] = dwn;
                 P.state[s] = cont ? need : (mask ? WF_DONE | (mask << WF_SHADE_SHIFT) : WF_FREE);
             }
             active = false;

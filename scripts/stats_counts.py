@@ -17,4 +17,6 @@ with NativeContext(load_scene_file(scene), seed=DEFAULT_SEED, flags=MFX_F_COUNT_
 rc, rs = s[0] + s[1], s[2]
 print(os.path.basename(sys.argv[1]), json.dumps({
     "closest": [round(s[4] / rc, 3), round(s[5] / rc, 3), round(s[6] / rc, 3)],
-    "shadow": [round(s[7] / rs, 3), round(s[8] / rs, 3), round(s[9] / rs, 3)]}))
+    "shadow": [round(s[7] / rs, 3), round(s[8] / rs, 3), round(s[9] / rs, 3)],
+    # camera packets (k_camera): wave node steps and leaf slots per camera ray
+    "camera_packets": [round(s[10] / s[3], 3), round(s[11] / s[3], 3)]}))

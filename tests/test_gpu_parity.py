@@ -311,3 +311,33 @@ def test_shadow_subpackets_answer_like_single_rays(gpu, oracle, monkeypatch, nam
         packet = ctx.any_hit(srays, tmax)
     assert np.array_equal(single, packet), (single != packet).sum()
     assert np.array_equal(single, oracle.OracleScene(a).any_hit(srays, tmax))
+
+
+_CONE_CAMERAS = [
+    # (scene, camera): the camera on a wall's plane, at a vertex, grazing the floor, inside the
+    # mesh, close to it, far and narrow
+    ("cube_cornell", {"position": (0.0, 0.0, 0.5), "direction": (0.0, 0.2, -1.0), "fov": 100.0}),
+    ("cube_cornell", {"position": (-1.0, 0.0, 0.99), "direction": (1.0, 0.8, -1.0), "fov": 90.0}),
+    ("cube_cornell", {"position": (0.0, 1e-7, 0.9), "direction": (0.0, 0.0, -1.0), "fov": 120.0}),
+    ("spot", {"position": (0.0, 0.0, 0.0), "direction": (0.3, -0.2, 1.0), "fov": 110.0}),
+    ("spot", {"position": (0.33, -0.39, 0.45), "direction": (-0.1, -0.05, -1.0), "fov": 60.0}),
+    ("spot", {"position": (240.0, 120.0, -340.0), "direction": (-2.4, -1.2, 3.4), "fov": 0.6}),
+    ("renault", None),
+]
+
+
+@pytest.mark.parametrize("name,cam", _CONE_CAMERAS)
+def test_camera_packets_at_edge_case_cameras(gpu, oracle, name, cam):
+    """Camera-ray packets (k_camera) at cameras on a triangle's plane, at a vertex, grazing a wall,
+    inside the mesh, far and narrow: images equal the oracle's bit for bit."""
+    from mafrixraytracing_amd.abi import SceneArrays
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene(name, 40, 24)
+    if cam is not None:
+        c = dict(a.camera)
+        c.update(cam)
+        a = SceneArrays(a.prims, a.albedo, a.light, c, a.width, a.height, a.max_depth)
+    ref = oracle.OracleScene(a).sample(2, SEED)
+    with NativeContext(a, seed=SEED) as ctx:
+        img = ctx.sample(2)
+    assert np.array_equal(img, ref), np.abs(img - ref).max()
