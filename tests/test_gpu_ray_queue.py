@@ -3,7 +3,7 @@ paths that continue into dense queues, and the later iterations read and write t
 the scattered slots. The choice only moves data, so every mode must give the oracle's image bit for
 bit with the same ray counts: in place (-1), queues from the first vertex (0) or the second (1, 2),
 automatic (-2: the live share per iteration of the previous trace decides), small chunks, odd
-films, max_depth 5 (three queue hand-overs, both queues reused), two-level instancing, several
+films, max_depth 1, 2 and 5 (three queue hand-overs, both queues reused), two-level instancing, several
 generations (a small pool), and the render-ahead planes. Each mode runs with small and large
 chunks of queue entries."""
 import os
@@ -36,7 +36,9 @@ def _ctx(a, env, **kw):
 
 @pytest.mark.parametrize("name,w,h,spp,depth", [
     ("spot", 67, 45, 6, 3), ("cube_cornell", 40, 32, 4, 3), ("renault", 48, 40, 3, 3),
-    ("spot16_instanced@2l", 56, 40, 3, 3), ("cornell", 33, 31, 3, 5), ("two_spheres_plane", 32, 32, 4, 4)])
+    ("spot16_instanced@2l", 56, 40, 3, 3), ("cornell", 33, 31, 3, 5), ("two_spheres_plane", 32, 32, 4, 4),
+    # max_depth 1 and 2: the lit mask rides in the HIT state word (lit_in_hit) with fewer iterations
+    ("spot", 40, 24, 3, 2), ("cube_cornell", 40, 24, 3, 1)])
 def test_queue_modes_match_oracle(gpu, oracle, name, w, h, spp, depth):
     """Round 3's one red run of this test (r03am, before the ray queues were committed) failed in the
     in-place mode (-1) with 21 extension and 35 shadow rays fewer than the oracle. The library was
