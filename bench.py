@@ -47,6 +47,12 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# Hardware queues per process, read by the HIP runtime when it initializes (before any GPU call
+# here). A rank keeps up to three contexts' streams in flight (distributed.frames_in_flight) beside
+# torch's and RCCL's; with HIP's default of 4 queues two of them share one and serialize, and C2's
+# 1/8 share runs 5.03 instead of 4.70 ms per step (profiles/r05/r05w_*). An explicit setting wins.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+
 METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 XGMI_LINK_GBS = 153.0  # one xGMI link of MI355X (7 per GPU): the exchange models move each rank's bytes over one link
@@ -242,7 +248,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
     predicted_efficiency = (t_1GPU / N) / (t_slowest_rank + t_pack + t_transfer + t_unpack): the
     exchange not overlapped (the bench overlaps it with the next frame's trace; not counted here)."""
     import torch
-    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.abi import MFX_F_IN_FLIGHT, MFX_F_ROW_PARTITION
     from mafrixraytracing_amd.distributed import RowGather, frames_in_flight
     from mafrixraytracing_amd.native import NativeContext
     W, H = arrays.width, arrays.height
@@ -286,8 +292,8 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
         ov = None
         nif = frames_in_flight(W, H, spp, n)  # the bench's rank alternates its frames over nif contexts
         for r in range(n):
-            cs = [NativeContext(arrays, seed=seed, flags=flags | MFX_F_ROW_PARTITION, part_index=r, part_count=n)
-                  for _ in range(nif)]
+            fl = flags | MFX_F_ROW_PARTITION | (MFX_F_IN_FLIGHT if nif > 1 else 0)
+            cs = [NativeContext(arrays, seed=seed, flags=fl, part_index=r, part_count=n) for _ in range(nif)]
             for c in cs:
                 c.trace_accumulate(spp, 0)  # the pool's first allocation, untimed
             for c in cs:
@@ -375,8 +381,8 @@ def main():
     use_dist = world > 1 or os.environ.get("MFX_BENCH_FORCE_DIST") == "1"
 
     import numpy as np
-    from mafrixraytracing_amd.abi import (MFX_F_COUNT_STATS, MFX_F_MEGAKERNEL, MFX_F_NONE, MFX_F_ROW_PARTITION,
-                                          MFX_F_WAVEFRONT)
+    from mafrixraytracing_amd.abi import (MFX_F_COUNT_STATS, MFX_F_IN_FLIGHT, MFX_F_MEGAKERNEL, MFX_F_NONE,
+                                          MFX_F_ROW_PARTITION, MFX_F_WAVEFRONT)
     from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, frames_in_flight, step_spp
     from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
@@ -402,13 +408,19 @@ def main():
         devices = list(range(args.gpus))
         if os.environ.get("MFX_BENCH_DEVICE") is not None:  # the one-GPU rehearsal: every device is that one
             devices = [int(os.environ["MFX_BENCH_DEVICE"])] * args.gpus
+    # one process per GPU: a rank whose frame is small (its share at 4+ GPUs) alternates its frames
+    # over several contexts, frames in flight (distributed.frames_in_flight; MFX_F_IN_FLIGHT), for the
+    # line's job and for the other scaling's job measured after it
+    nif = frames_in_flight(W, H, spp_step, world, rows) if use_dist and args.api == "batch" else 1
+    o_nif = (frames_in_flight(W, H, step_spp(args.spp, ngpu, "weak" if args.scaling == "strong" else "strong"),
+                              world, rows) if use_dist and args.api == "batch" and ngpu > 1 else 1)
+    nctx = max(nif, o_nif)
+    if nctx > 1:
+        rank_mode |= MFX_F_IN_FLIGHT
     ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank, part_count=world,
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
-    # one process per GPU: a rank whose frame is small (its share at 4+ GPUs) alternates its frames
-    # over two contexts, two frames in flight (distributed.frames_in_flight)
-    nif = frames_in_flight(W, H, spp_step, world, rows) if use_dist and args.api == "batch" else 1
     ctxs = [ctx] + [NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank,
-                                  part_count=world) for _ in range(nif - 1)]
+                                  part_count=world) for _ in range(nctx - 1)]
 
     def totals():  # the timed steps' rays, summed on the device over this rank's contexts
         t = np.zeros(16)
@@ -417,12 +429,17 @@ def main():
         return t
     pr = None
     if use_dist:
-        # two attached accumulators: frame k's exchange runs while frame k + 1 traces. The image
-        # partition gathers each rank's rows to rank 0 (RCCL); gloo (the one-GPU rehearsal, CUDA
-        # tensors) has no CUDA gather, so there the rows merge by all_reduce (an exact sum too)
-        accs = [torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}") for _ in range(2)]
+        # attached accumulators (two, or one per context in flight): frame k's exchange runs while
+        # the next frames trace. The image partition gathers each rank's rows to rank 0 (RCCL); gloo
+        # (the one-GPU rehearsal, CUDA tensors) has no CUDA gather, so there the rows merge by
+        # all_reduce (an exact sum too)
+        accs = [torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{local}") for _ in range(max(2, nctx))]
         gathers = [RowGather(a, W, H, rank, world) for a in accs] if rows and backend != "gloo" else None
-        pr = PipelinedNativeRender(ctxs, accs, rank, world, gathers=gathers)
+        pr = PipelinedNativeRender(ctxs[:nif], accs, rank, world, gathers=gathers)
+    # a context allocates its path pool in its first trace: the line's extra contexts trace one
+    # untimed frame of its size now, so no allocation falls into a timed step
+    for c in ctxs[1:nif]:
+        c.trace_accumulate(spp_step, 0)
     rbuf = np.empty(npix * 4, dtype=np.uint8)  # Scene.Render's byte[w*h*4]
 
     def barrier():
@@ -506,7 +523,6 @@ def main():
         po = pr
         if pr is not None:  # the other job's frames in flight, by its own frame size
             pr.drain()
-            o_nif = frames_in_flight(W, H, o_spp, world, rows)
             po = PipelinedNativeRender(ctxs[:o_nif], accs, rank, world, gathers=gathers)
 
         def other_step(k):
@@ -518,6 +534,8 @@ def main():
                 ctx.trace_accumulate(o_spp, base)
                 ctx.accum_reduce()
         other_step(0)
+        for c in ctxs[1:o_nif]:  # (the other job's extra contexts: their pools, untimed)
+            c.trace_accumulate(o_spp, 0)
         if po is not None:
             po.drain()
         barrier()
@@ -768,7 +786,10 @@ def main():
             rapi["without_render_ahead"] = plain
             sapi = sample_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
             sapi["vs_batch"] = round(sapi["value"] / value, 4)
-            share = strong_share(arrays, DEFAULT_SEED, args.spp, value, elapsed / args.steps * 1e3, flags=cf)
+            # each rank's share timed over the line's own step count (its frames-in-flight pipeline
+            # fills and drains between the barriers, as an N-GPU run of these steps does)
+            share = strong_share(arrays, DEFAULT_SEED, args.spp, value, elapsed / args.steps * 1e3,
+                                 steps=args.steps, flags=cf)
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)

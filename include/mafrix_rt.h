@@ -136,6 +136,10 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
                                == part_index) instead of the samples: a rank traces every sample of its rows,
                                its accumulator is +0.0 elsewhere, and a sum-reduce over the ranks is an exact
                                merge (the multi-process image partition; mfx_trace_accumulate)       */
+#define MFX_F_IN_FLIGHT 128 /* the caller keeps frames in flight on several contexts of this device (each its
+                               own pool and stream, frames alternating): the wavefront launches fetch larger
+                               chunks of paths, since another frame's launches fill each launch's tail.
+                               Scheduling only: the same images and ray counts (ABI 6, additive)     */
 
 /* One entry of an instanced scene (mfx_create_instanced; an extension: the reference has no
  * instancing, its scenes are flat lists). The world primitive list — the index space Bvh.Build

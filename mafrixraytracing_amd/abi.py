@@ -24,6 +24,7 @@ MFX_F_WAVEFRONT = 8
 MFX_F_FLATTEN = 16
 MFX_F_TWO_LEVEL = 32
 MFX_F_ROW_PARTITION = 64
+MFX_F_IN_FLIGHT = 128
 MFX_INSTANCE_VERBATIM = 1
 MFX_MAX_DEVICES = 64
 MFX_ABI_VERSION = 6

@@ -168,6 +168,7 @@ struct mfx_ctx {
     int wf_ext_grid = 0, wf_shd_grid = 0;
     int wf_cam_grid = 0;  // > 0: camera rays as packets (k_camera; MFX_CAMERA_PACKETS=0 turns it off)
     int wf_chunk = 256;  // slots per chunk fetch (a multiple of 64; r04j: 256 against 1024, C2 64 spp +1 %, 8 spp +6 %)
+    bool wf_shd_half = true;  // k_shadow takes half chunks in place on frames of at most 2^25 paths (MFX_SHD_HALF)
     int mega_chunk = 0;   // megakernel: paths a wave takes per atomic (0: by the call's size)
     int mega_waves = 1;   // megakernel instance: 4 (128-VGPR budget) or 1 (mfx_kernels.hip)
     int wf_stack_lds_ext = 1, wf_stack_lds_shd = 1;  // traversal stack entries per lane in LDS (the rest spill)
@@ -196,7 +197,9 @@ struct mfx_ctx {
     int64_t dfilm_n = 0;
     unsigned long long* d_counters_aux = nullptr;  // ray counters of a film-only re-trace (not reported)
     hipEvent_t aux_ev0 = nullptr, aux_ev1 = nullptr;
-    hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace)
+    hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace); created
+                                        // at the first render-ahead call, so a batch-only context holds one
+                                        // stream (one of the process's GPU_MAX_HW_QUEUES hardware queues)
     unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
     uint8_t* h_stage = nullptr;         // page-locked staging of large readbacks (host_readback)
     hipEvent_t stage_ev[kStageChunks] = {};  // host_readback: piece i is in h_stage
@@ -306,7 +309,6 @@ static int ctx_setup(mfx_ctx* c) {
     } while (0)
     CK(hipSetDevice(c->device));
     CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    CK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
     CK(hipHostMalloc((void**)&c->h_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
@@ -350,6 +352,14 @@ static int ctx_setup(mfx_ctx* c) {
         if (atoi(rq) == 0) c->wf_queue_from = -1;
     }
     if (const char* ck = getenv("MFX_MEGA_CHUNK")) c->mega_chunk = std::max(1, atoi(ck));
+    // MFX_F_IN_FLIGHT: the caller alternates frames over several contexts of this device, so each
+    // launch's ramp-down runs beside another frame's launches: larger chunk fetches and whole ones
+    // for k_shadow (r05s, C2's 1/8 share over 3 contexts: 4.44 -> 4.37 ms, the 1/4 share 8.78 -> 8.63)
+    if (c->flags & MFX_F_IN_FLIGHT) {
+        c->wf_chunk = 512;
+        c->wf_shd_half = false;
+    }
+    if (const char* e = getenv("MFX_SHD_HALF")) c->wf_shd_half = atoi(e) != 0;
     if (const char* ck = getenv("MFX_CHUNK")) {
         c->wf_chunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(ck) / 64 * 64));
     }
@@ -681,6 +691,12 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     const int nv = c->host.max_depth + 1;  // vertices per path
     const size_t per_slot = WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4 - (queues ? 0 : WF_QUEUE_BYTES_PER_SLOT);
     const size_t bytes = P * per_slot + 64 * 256;
+    // leave the runtime its headroom (kernel scratch is allocated at launch): a pool that would take
+    // the device's last 512 MiB counts as out of memory, and wf_trace retries with smaller generations
+    size_t mfree = 0, mtotal = 0;
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0 && bytes + ((size_t)512 << 20) > mfree)
+        return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB with " +
+                                     std::to_string(mfree >> 20) + " MiB free");
     hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
@@ -787,10 +803,19 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     const int64_t total = per_sample * ns;
     if (total == 0) return fail(MFX_E_STATE, "wf_trace: empty band");
     // generations of whole 64-path windows (one 8x8 tile of one sample each: the camera-ray packets)
-    const int64_t gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
-    const int32_t pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
     const int qf = c->wf_queue_from == -2 ? c->wf_queue_auto : c->wf_queue_from;  // the ray-queue start
-    int rc = wf_ensure_pool(c, pool, qf >= 0);
+    int64_t gen_max = 0;
+    int32_t pool = 0;
+    int rc = MFX_OK;
+    while (true) {
+        gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
+        pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
+        rc = wf_ensure_pool(c, pool, qf >= 0);
+        // the device is short of memory (other contexts or processes on it): smaller generations,
+        // the same images (a generation only bounds how many paths are in flight)
+        if (rc != MFX_E_NOMEM || c->wf_pool_max <= (1 << 20)) break;
+        c->wf_pool_max = std::max<int64_t>(1 << 20, gen_max / 2);
+    }
     if (rc) return rc;
     WfParams P = c->wf;
     fill_scene_params(c, P);
@@ -872,7 +897,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
             // in place on a small frame (the strong-scaling shares), k_shadow takes half chunks: the
             // first vertex's last chunks are its launch's tail (r04u: C2 at 8 spp +2.4 %; at 64 spp
             // the same halving costs 1.5 %, so frames of more than 2^25 paths keep whole chunks)
-            P.chunk_shd = (!P.qcount && total <= ((int64_t)1 << 25)) ? std::max(64, P.chunk / 2) : P.chunk;
+            P.chunk_shd = (c->wf_shd_half && !P.qcount && total <= ((int64_t)1 << 25)) ? std::max(64, P.chunk / 2) : P.chunk;
             if (!own_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;
@@ -1523,6 +1548,7 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     const size_t frame = 4 * (size_t)c->npix;
     for (mfx_ctx* d : ds) {
         HIPCHECK(hipSetDevice(d->device));
+        if (!d->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&d->copy_stream, hipStreamNonBlocking));
         HIPCHECK(hipStreamWaitEvent(d->copy_stream, d->ab[xi].ready, 0));
         if (rgba) {
             const int rb = copy_band_rgba(d, rgba, d->ab[xi].frames + k * frame, d->copy_stream);

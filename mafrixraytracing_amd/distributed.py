@@ -177,47 +177,50 @@ def native_partitioned_render(ctx, acc, rank: int, world: int, exchange: Callabl
 
 
 def frames_in_flight(width: int, height: int, spp: int, world: int, rows: bool = True) -> int:
-    """Contexts a rank alternates frames over: 2 when its frame is at most 2^25 paths (one rank's
-    image-partition share at 4 or more GPUs), else 1. Every persistent launch fills the GPU, so a
-    second context's launches (its own pool and stream) take CUs as the first one's blocks retire:
-    the next frame's dense launches fill the previous frame's tails. Measured on C2
-    (profiles/r05/r05i_frames_in_flight.json): a 1/8 share +8.5 %, 1/4 +2.3 %, 1/2 -2 %, the whole
-    film -4 % (two frames' working sets in one L2)."""
+    """Contexts a rank alternates frames over: 3 when its frame is at most 2^25 paths (one rank's
+    image-partition share at 4 or more GPUs), else 1. Every persistent launch fills the GPU, so
+    another context's launches (its own pool and stream) take CUs as the first one's blocks retire:
+    the next frames' dense launches fill the previous frame's tails. The contexts are created with
+    MFX_F_IN_FLIGHT (larger chunk fetches: the tails are covered). Measured on C2: two contexts, a 1/8
+    share +8.5 %, 1/4 +2.3 %, 1/2 -2 %, the whole film -4 % (profiles/r05/r05i_frames_in_flight.json:
+    two frames' working sets in one L2); three with MFX_F_IN_FLIGHT, the 1/8 share 4.55 -> 4.37 ms and
+    the 1/4 share 8.82 -> 8.63 ms against two (profiles/r05/r05s_sweep_small_frames.txt)."""
     tr = (height + 7) // 8
     rows_per_rank = -(-tr // world) if rows else tr
     paths = ((width + 7) // 8) * rows_per_rank * 64 * spp
-    return 2 if paths <= (1 << 25) else 1
+    return 3 if paths <= (1 << 25) else 1
 
 
 class PipelinedNativeRender:
-    """Frames over two attached accumulators, so a frame's exchange overlaps the next frame's trace:
-    frame k traces into accs[k % 2] on the HIP stream of context ctxs[k % len(ctxs)]; torch's stream
-    waits for that trace (an event on the context stream, no host sync) and runs the exchange — a
-    RowGather per buffer (image partition) or the sum-reduce; frame k + 2 reuses the buffer only
-    after that exchange has finished (an event on torch's stream, waited on the host just before the
-    buffer is cleared, while the GPU is still tracing frame k + 1). With two contexts (two pools, two
-    streams: frames_in_flight) frame k + 1's trace runs beside frame k's. Each frame is the same
-    clear / trace / exchange as PartitionedRender.frame; only the waits move. drain() waits for every
-    outstanding exchange; `buffer(k)` is where frame k's merged accumulator lands (on rank 0)."""
+    """Frames over B >= 2 attached accumulators, so a frame's exchange overlaps the next frames'
+    traces: frame k traces into accs[k % B] on the HIP stream of context ctxs[k % len(ctxs)]
+    (len(ctxs) <= B); torch's stream waits for that trace (an event on the context stream, no host
+    sync) and runs the exchange — a RowGather per buffer (image partition) or the sum-reduce; frame
+    k + B reuses the buffer only after that exchange has finished (an event on torch's stream, waited
+    on the host just before the buffer is cleared, while the GPU is still tracing the frames between).
+    With several contexts (their own pools and streams: frames_in_flight) the next frames' traces run
+    beside frame k's. Each frame is the same clear / trace / exchange as PartitionedRender.frame;
+    only the waits move. drain() waits for every outstanding exchange; `buffer(k)` is where frame k's
+    merged accumulator lands (on rank 0)."""
 
     def __init__(self, ctx, accs, rank: int, world: int, gathers: list | None = None):
         import torch
         self.ctxs = list(ctx) if isinstance(ctx, (list, tuple)) else [ctx]
-        assert len(self.ctxs) in (1, 2)
         self.ctx = self.ctxs[0]
         self.accs = list(accs)
-        assert len(self.accs) == 2 and all(a.is_cuda for a in self.accs)
+        self.nbuf = len(self.accs)
+        assert self.nbuf >= max(2, len(self.ctxs)) and all(a.is_cuda for a in self.accs)
         self.gathers = gathers
-        assert gathers is None or len(gathers) == 2
+        assert gathers is None or len(gathers) == self.nbuf
         self.rank, self.world = rank, world
         self.multi = len(getattr(self.ctx, "devices", [0])) > 1
         self.device = self.accs[0].device
         self.ctx_streams = [torch.cuda.ExternalStream(c.stream(), device=self.device) for c in self.ctxs]
-        self.pending = [None, None]
+        self.pending = [None] * self.nbuf
         self.k = 0
 
     def buffer(self, k: int):
-        return self.accs[k % 2]
+        return self.accs[k % self.nbuf]
 
     def _wait(self, i: int):
         if self.pending[i] is not None:
@@ -227,12 +230,12 @@ class PipelinedNativeRender:
     def frame(self, spp: int, sample_base: int, all_ranks: bool = False):
         import torch
         import torch.distributed as dist
-        i = self.k % 2
+        i = self.k % self.nbuf
         ci = self.k % len(self.ctxs)
         self.k += 1
         acc = self.accs[i]
         ctx = self.ctxs[ci]
-        self._wait(i)  # frame k - 2's exchange has read this buffer
+        self._wait(i)  # frame k - B's exchange has read this buffer
         ctx.accum_attach(acc.data_ptr(), acc.numel() * acc.element_size())
         ctx.accum_clear()
         ctx.trace_accumulate(spp, sample_base)
@@ -258,7 +261,7 @@ class PipelinedNativeRender:
         return acc
 
     def drain(self):
-        for i in (0, 1):
+        for i in range(self.nbuf):
             self._wait(i)
         for c in self.ctxs:
             c.sync()

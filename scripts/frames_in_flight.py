@@ -40,17 +40,23 @@ def main():
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "spot.xml"))
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--parts", default="1,2,4,8")
+    ap.add_argument("--modes", default="1,2", help="contexts in flight per run, comma-separated")
     a = ap.parse_args()
-    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.abi import MFX_F_IN_FLIGHT, MFX_F_ROW_PARTITION
     from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
     arr = load_scene_file(a.scene)
     out = {"scene": os.path.basename(a.scene), "spp": a.spp, "steps": a.steps}
-    for parts in (1, 2, 4, 8):
+    modes = [int(m) for m in a.modes.split(",")]
+    for parts in (int(p) for p in a.parts.split(",")):
         kw = dict(flags=MFX_F_ROW_PARTITION, part_index=0, part_count=parts) if parts > 1 else {}
         row = {}
-        for inflight in (1, 2, 1, 2):  # interleaved
-            ctxs = [NativeContext(arr, seed=DEFAULT_SEED, **kw) for _ in range(inflight)]
+        for inflight in modes + modes:  # interleaved
+            k2 = dict(kw)
+            if inflight > 1:  # what bench.py's ranks create (MFX_F_IN_FLIGHT)
+                k2["flags"] = k2.get("flags", 0) | MFX_F_IN_FLIGHT
+            ctxs = [NativeContext(arr, seed=DEFAULT_SEED, **k2) for _ in range(inflight)]
             ms, rays = run(ctxs, a.spp, a.steps * max(1, parts // 2))
             for c in ctxs:
                 c.close()

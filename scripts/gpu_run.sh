@@ -68,7 +68,7 @@ for step in "$@"; do
         --no-stats --steps 5 --warmup 1 > $O/rehearse_$a1.json 2> $O/rehearse_$a1.err
       python3 -c "import json; d=json.load(open('$O/rehearse_$a1.json')); print('rehearse', d['n_gpus'], d['scaling'], d['value'], d['config']['global_spp_per_step'], d['config']['frames_in_flight'])" ;;
     inflight)
-      timeout -k 10 300 python3 scripts/frames_in_flight.py > $O/inflight.json 2> $O/inflight.err
+      timeout -k 10 300 python3 scripts/frames_in_flight.py --modes 1,2,3 > $O/inflight.json 2> $O/inflight.err
       cat $O/inflight.json ;;
     subpk)
       D=$R/$O/subpk_$a1

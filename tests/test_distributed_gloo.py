@@ -142,6 +142,6 @@ def test_frames_in_flight_policy():
     share at 4 and 8 GPUs (profiles/r05/r05i_frames_in_flight.json: +2.3 %, +8.5 %), one context for
     the whole film and the half share (-4 %, -2 %)."""
     from mafrixraytracing_amd.distributed import frames_in_flight
-    assert [frames_in_flight(1920, 1080, 64, n) for n in (1, 2, 4, 8)] == [1, 1, 2, 2]
+    assert [frames_in_flight(1920, 1080, 64, n) for n in (1, 2, 4, 8)] == [1, 1, 3, 3]
     assert frames_in_flight(1920, 1080, 512, 8) == 1  # the weak job's share: 8x the paths
     assert frames_in_flight(1920, 1080, 64, 8, rows=False) == 1  # a sample partition keeps the whole film

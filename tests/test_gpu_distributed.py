@@ -52,14 +52,14 @@ def _plain_accumulators(name, frames, part_index=0, part_count=1):
 
 
 def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False,
-                 two_ctx=False):
+                 nctx=1):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import torch
     import torch.distributed as dist
 
     from conftest import scene
-    from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.abi import MFX_F_IN_FLIGHT, MFX_F_ROW_PARTITION
     from mafrixraytracing_amd.distributed import PipelinedNativeRender, RowGather, native_partitioned_render
     from mafrixraytracing_amd.native import NativeContext
 
@@ -68,19 +68,20 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
     a = scene(name, W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
     gather = rows and backend == "nccl"  # (gloo has no CUDA gather: rows merge by all_reduce there)
-    with NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world,
-                       flags=MFX_F_ROW_PARTITION if rows else 0) as ctx, \
-            NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world,
-                          flags=MFX_F_ROW_PARTITION if rows else 0) as ctx2:
+    flags = (MFX_F_ROW_PARTITION if rows else 0) | (MFX_F_IN_FLIGHT if nctx > 1 else 0)
+    ctxs = [NativeContext(a, seed=SEED, device=0, part_index=rank, part_count=world, flags=flags)
+            for _ in range(nctx)]
+    ctx = ctxs[0]
+    try:
         got = []
-        if pipelined:  # back to back, no waits between frames; the last two buffers checked after drain
-            acc1 = torch.zeros_like(acc)
-            gs = [RowGather(b, W, H, rank, world) for b in (acc, acc1)] if gather else None
-            pr = PipelinedNativeRender([ctx, ctx2] if two_ctx else ctx, [acc, acc1], rank, world, gathers=gs)
+        if pipelined:  # back to back, no waits between frames; the last B buffers checked after drain
+            accs = [acc] + [torch.zeros_like(acc) for _ in range(max(2, nctx) - 1)]
+            gs = [RowGather(b, W, H, rank, world) for b in accs] if gather else None
+            pr = PipelinedNativeRender(ctxs if nctx > 1 else ctx, accs, rank, world, gathers=gs)
             for spp, base in frames:
                 pr.frame(spp, base, all_ranks=all_ranks)
             pr.drain()
-            got = [pr.buffer(k).cpu().numpy().copy() for k in range(len(frames) - 2, len(frames))]
+            got = [pr.buffer(k).cpu().numpy().copy() for k in range(len(frames) - len(accs), len(frames))]
             pr.close()
         else:
             pr = native_partitioned_render(ctx, acc, rank, world,
@@ -89,16 +90,19 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
                 pr.frame(spp, base, all_ranks=all_ranks)
                 got.append(acc.cpu().numpy().copy())
             ctx.accum_attach(None)
+    finally:
+        for c in ctxs:
+            c.close()
     if rank == 0:
         np.save(os.path.join(outdir, "frames.npy"), np.stack(got))
     dist.barrier()
     dist.destroy_process_group()
 
 
-def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False, two_ctx=False):
+def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False, nctx=1):
     import torch.multiprocessing as mp
     mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks,
-                                           pipelined, rows, two_ctx),
+                                           pipelined, rows, nctx),
                        nprocs=world, join=True, start_method="spawn")
     return np.load(os.path.join(outdir, "frames.npy"))
 
@@ -137,12 +141,15 @@ def test_world1_nccl_row_gather_bit_identical(gpu, tmp_path, pipelined):
         assert np.array_equal(got[i], want[k]), k
 
 
-def test_world1_nccl_two_frames_in_flight(gpu, tmp_path):
-    """Frames alternating over two contexts (two pools, two streams: frames_in_flight), row gather,
-    pipelined: the last two buffers equal the plain context's accumulators bit for bit."""
-    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False, pipelined=True, rows=True, two_ctx=True)
+@pytest.mark.parametrize("nctx", [2, 3])
+def test_world1_nccl_frames_in_flight(gpu, tmp_path, nctx):
+    """Frames alternating over two or three contexts (their own pools and streams, MFX_F_IN_FLIGHT's
+    larger chunks: frames_in_flight), one buffer per context, row gather, pipelined: the last
+    buffers equal the plain context's accumulators bit for bit."""
+    got = _spawn(1, "nccl", "spot", FRAMES, tmp_path, False, pipelined=True, rows=True, nctx=nctx)
     want = _plain_accumulators("spot", FRAMES)
-    for i, k in enumerate(range(len(FRAMES) - 2, len(FRAMES))):
+    nb = max(2, nctx)
+    for i, k in enumerate(range(len(FRAMES) - nb, len(FRAMES))):
         assert np.array_equal(got[i], want[k]), k
 
 

@@ -118,3 +118,33 @@ def test_full_size_render_ahead_device_list(gpu):
         for k in range(10):
             assert np.array_equal(c1.render_rgba8(1), c2.render_rgba8(1)), k
         assert np.array_equal(c1.film_mean(), c2.film_mean())
+
+
+def test_pool_shrinks_when_the_device_is_short_of_memory(gpu):
+    """A context created while the device had room, traced after other allocations left it short:
+    the wavefront pool's allocation fails, the trace retries with half-size generations until it
+    fits (wf_trace), and the accumulator and ray counts equal an unconstrained context's bit for bit.
+    C2 at 64 spp: 132.7 M paths, a ~23 GB pool in one generation; 8 GB are left free (the pool fits
+    at a quarter of the generation, with room for the runtime's own allocations)."""
+    import torch
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("spot")  # 1920 x 1080
+    with NativeContext(a, seed=SEED) as ref_ctx:
+        ref_ctx.trace_accumulate(64, 0)
+        want = ref_ctx.accum_read_mean(1.0)
+        want_counts = ref_ctx.ray_counts()[:3]
+    ctx = NativeContext(a, seed=SEED)
+    try:
+        free, _ = torch.cuda.mem_get_info()
+        hog = torch.empty(max(0, free - (8 << 30)), dtype=torch.uint8, device="cuda")
+        try:
+            ctx.trace_accumulate(64, 0)
+            got = ctx.accum_read_mean(1.0)
+            counts = ctx.ray_counts()[:3]
+        finally:
+            del hog
+            torch.cuda.empty_cache()
+    finally:
+        ctx.close()
+    assert np.array_equal(got, want)
+    assert np.array_equal(counts, want_counts)
