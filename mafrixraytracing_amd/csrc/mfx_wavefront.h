@@ -96,7 +96,9 @@ struct WfParams {
     const uint8_t* ref_blob;
     const MfxShade* shade;
     const MfxInstance* inst;  // two-level scenes: instances (null for a flat scene)
-    MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers
+    MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers (k_resolve)
+    const MfxLight* light_dev;  // the same in device memory: k_shadow copies it into LDS, so its 52
+                                // dwords are not held in scalar registers through the kernel's loops
     MfxCamera cam;
     double* accum;  // [3][w*h]
     // render-ahead (k_resolve's frames mode): film != null makes the call's samples one-sample render

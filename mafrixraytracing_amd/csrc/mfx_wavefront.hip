@@ -412,7 +412,8 @@ struct VertexSample {
     double ei, dist, cs, solid;
     bool lightable;
 };
-__device__ __forceinline__ VertexSample sample_vertex(const WfParams& P, bool own, DV hp, DV nm, uint64_t key,
+// LT: the light (k_shadow's LDS copy).
+__device__ __forceinline__ VertexSample sample_vertex(const MfxLight& LT, bool own, DV hp, DV nm, uint64_t key,
                                                       uint32_t& rn, int* scratch) {
     VertexSample V{};
 #if defined(MFX_DIAG_ONE_TRIAL)  // timing experiment only: the first trial, mirrored into the hemisphere
@@ -424,7 +425,6 @@ __device__ __forceinline__ VertexSample sample_vertex(const WfParams& P, bool ow
     if (!own) return V;
     V.wi = vnormalize(p);
     V.ei = vdot(nm, V.wi);
-    const MfxLight& LT = P.light;
     const double sel = rng_next(key, rn);
     const int lt = sel < 0.5 ? 0 : 1;
     const double tu = rng_next(key, rn);
@@ -458,7 +458,10 @@ __device__ __forceinline__ VertexSample sample_vertex(const WfParams& P, bool ow
 // SK: the scene kind (WF_SK_FLAT, WF_SK_INST: two-level, WF_SK_SLDS: a small flat scene whose whole
 // slot array sits in LDS); only a small scene's instances carry the LDS slot reads (r04c: the runtime
 // branch in every leaf test cost C2 1.8 % and C4 4 %)
-template <bool STATS, bool SPILL, int SK, bool Q>
+// START: the instance for a generation's first iteration when k_camera does not take its camera
+// rays (two-level scenes, MFX_CAMERA_PACKETS=0); only it carries the camera-ray code (GetRay, the
+// path key, the camera's fields), so the bounce instances hold fewer live scalar registers
+template <bool STATS, bool SPILL, int SK, bool Q, bool START = false>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
@@ -503,7 +506,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     auto start_ray = [&](int e) {
         se = e;
         const int s = e & WF_ENTRY_SLOT;
-        const bool fresh = e < 0;
+        const bool fresh = START && e < 0;
         DV o, d;
         if (fresh) {
             // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
@@ -532,7 +535,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     // the lane's ray is finished: its closest hit (hit point, shade index) or its miss
     auto finish_ray = [&]() {
         const int s = se & WF_ENTRY_SLOT;
-        const bool fresh = se < 0;
+        const bool fresh = START && se < 0;
         const int fl = fresh ? WF_FRESH : 0;
         if (T.B.found) {
             const DV hp = vadd(T.o, vmul(T.d, T.B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
@@ -561,7 +564,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
                     bool take = (sj & WF_STATE_MASK) == WF_NEED_EXT;
-                    if (P.start && sj == WF_FREE && j < P.total) {
+                    if (START && sj == WF_FREE && j < P.total) {
                         int x, y;
                         int64_t smp;
                         // edge-tile padding starts no path (none when 8 divides the film size)
@@ -571,7 +574,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
                     // entry: slot | camera-ray flag << 31, or slot | lit mask << 28 (lit_in_entry)
                     if (take)
                         pend[n + __popcll(tm & lanes_below())] =
-                            sj == WF_FREE ? (j | (int)0x80000000)
+                            (START && sj == WF_FREE) ? (j | (int)0x80000000)
                                           : (lit_in_entry ? j | (((unsigned)sj >> WF_SHADE_SHIFT) & 7) << 28 : j);
                     n += __popcll(tm);
                     sc.advance(P.state);
@@ -709,20 +712,25 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
-    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
-    if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int nslot = SLDS ? P.nslot_shd : 0;
-    if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
     int* lds = (int*)(slot_lds + 5 * nslot);
+    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
+    uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
+    // the light, after the four waves' shade lists (8-B aligned): copied before load_top_nodes' barrier
+    MfxLight* light_lds = (MfxLight*)((int*)(red + 16) + 4 * 2 * WF_SHD_LIST);
+    if (threadIdx.x < sizeof(MfxLight) / 8)
+        ((double*)light_lds)[threadIdx.x] = ((const double*)P.light_dev)[threadIdx.x];
+    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
+    if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
+    if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
+    const MfxLight& LT = *light_lds;
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_shd * 64 + lane, P, P.stack_lds_shd);
-    uint8_t* pend_base = (uint8_t*)(lds + 4 * P.stack_lds_shd * 64);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
-    uint32_t* red = (uint32_t*)(pend_base + 4 * PendShd::BYTES);
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, nslot};
     const int shard_size = P.pool / WF_SHARDS;
 
@@ -836,7 +844,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     }
                 }
                 wave_lds_sync();  // every owner has read its shl entries: shl[0, 64) is the sampler's scratch
-                const VertexSample V = sample_vertex(P, own, hp, nm, key, rn, shl);
+                const VertexSample V = sample_vertex(LT, own, hp, nm, key, rn, shl);
                 if (own) {
                     const DV wi = V.wi, unit = V.unit;
                     const double dist = V.dist, cs = V.cs, solid = V.solid;
@@ -862,7 +870,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     pd.v[3 * 64 + lane] = dist - 1e-6;
                     // a gray light: the direct term itself, (cs * (solid * I)) / pdf_li (Integrators.fs:52,
                     // Light.fs:52-53), the expression k_resolve evaluates per channel otherwise
-                    pd.v[4 * 64 + lane] = P.gray_light ? (cs * (solid * P.light.color[0])) / P.light.pdf : cs;
+                    pd.v[4 * 64 + lane] = P.gray_light ? (cs * (solid * LT.color[0])) / LT.pdf : cs;
                     pd.v[5 * 64 + lane] = solid;
                     c_shadow++;
                 }
@@ -1163,7 +1171,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst, int nslot = 0) {
     const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
                           (size_t)4 * stack_size * 64 * sizeof(int);
-    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int)
+    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int) + sizeof(MfxLight)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
@@ -1183,7 +1191,8 @@ template <int SK>
 static const void* occ_kernel(bool shadow, bool spill) {
     if (shadow)
         return spill ? (const void*)k_shadow<false, true, 4, SK, false> : (const void*)k_shadow<false, false, 4, SK, false>;
-    return spill ? (const void*)k_extend<false, true, SK, false> : (const void*)k_extend<false, false, SK, false>;
+    // (the START instance: a superset of the bounce instance's code)
+    return spill ? (const void*)k_extend<false, true, SK, false, true> : (const void*)k_extend<false, false, SK, false, true>;
 }
 
 hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int ntop, int ninst, int* blocks_per_cu,
@@ -1197,16 +1206,17 @@ hipError_t mfx_wf_kernel_occupancy(bool shadow, int stack_lds, bool spill, int n
     return e;
 }
 
-template <bool SPILL, int SK, bool Q>
+template <bool SPILL, int SK, bool Q, bool START = false>
 static void launch_extend_q(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (stats)
-        hipLaunchKernelGGL((k_extend<true, SPILL, SK, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_extend<true, SPILL, SK, Q, START>), dim3(grid), dim3(256), lds, st, P);
     else
-        hipLaunchKernelGGL((k_extend<false, SPILL, SK, Q>), dim3(grid), dim3(256), lds, st, P);
+        hipLaunchKernelGGL((k_extend<false, SPILL, SK, Q, START>), dim3(grid), dim3(256), lds, st, P);
 }
 template <bool SPILL, int SK>
 static void launch_extend(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
     if (P.qcount) launch_extend_q<SPILL, SK, true>(P, grid, stats, st, lds);
+    else if (P.start) launch_extend_q<SPILL, SK, false, true>(P, grid, stats, st, lds);
     else launch_extend_q<SPILL, SK, false>(P, grid, stats, st, lds);
 }
 template <bool SPILL, int WAVES, int SK, bool Q>
