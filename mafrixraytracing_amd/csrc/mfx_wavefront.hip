@@ -283,7 +283,9 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
 // tile-coherent. False for the padding indices of edge tiles (no path). A banded
 // trace (image partition) numbers only its own tile rows: its k-th tile row is film tile row
 // band_index + k * band_count, so pixels, keys and samples are the whole-film trace's.
-__device__ __forceinline__ bool path_pixel(const WfParams& P, int64_t p, int& x, int& y, int64_t& smp) {
+// PP: WfParams, or k_shadow's LDS copy of the fields it needs (PixParams)
+template <typename PP>
+__device__ __forceinline__ bool path_pixel(const PP& P, int64_t p, int& x, int& y, int64_t& smp) {
     // p = path_base + s: the 64-bit split of path_base is done once per generation on the host
     // (base_smp, base_q), so only 32-bit divisions remain here (base_q + s < 2^32)
     const unsigned tiles_x = (unsigned)(P.width + 7) >> 3;
@@ -649,6 +651,10 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     uint64_t* stm = (uint64_t*)lds_all + wave * P.stack_size;  // per wave: stack masks, then nodes
     int* stk = (int*)((uint64_t*)lds_all + 4 * P.stack_size) + wave * P.stack_size;
     uint32_t* red = (uint32_t*)((int*)((uint64_t*)lds_all + 4 * P.stack_size) + 4 * P.stack_size);
+    // the camera in LDS (read per window), not held in scalar registers through the packet walk
+    MfxCamera* cam_lds = (MfxCamera*)(red + 16);
+    if (threadIdx.x < sizeof(MfxCamera) / 8) ((double*)cam_lds)[threadIdx.x] = ((const double*)P.cam_dev)[threadIdx.x];
+    __syncthreads();
     const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
@@ -673,7 +679,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
             uint32_t rn = 0;
             const double u = ((double)x + rng_next(key, rn)) / (double)P.width;
             const double v = ((double)y + rng_next(key, rn)) / (double)P.height;
-            const MfxCamera& CAM = P.cam;
+            const MfxCamera& CAM = *cam_lds;
             const DV target = vadd(vadd(ld3(CAM.topleft), vmul(ld3(CAM.right), u)), vmul(ld3(CAM.down), v));
             o = ld3(CAM.position);
             d = vnormalize(vsub(target, o));
@@ -703,6 +709,29 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     }
 }
 
+// the fields path_pixel and path_key read, in k_shadow's LDS (after its array pointers): a shading
+// vertex derives its path's key from the slot, and these are not held in scalar registers through
+// the traversal loop
+struct PixParams {
+    int64_t path_base, base_q, base_smp, sample_base;
+    uint64_t seed;
+    int32_t width, height, band_index, band_count, band_rows, part_index, part_count, pad;
+};
+// k_shadow's array pointers in its LDS (after the light)
+struct ShdPtrs {
+    double *ox, *oy, *oz, *dx, *dy, *dz, *vei, *vls;
+    WfMat* vmat;
+    uint32_t* rn;
+    int32_t* depth;
+    const MfxShade* shade;
+    int32_t* fstate;
+    const int32_t* qslot;
+    double *nox, *noy, *noz, *ndx, *ndy, *ndz;
+    uint32_t* nrn;
+    int32_t *ndepth, *nstate, *nslot;
+    unsigned long long* ncount;
+};
+
 // ------------------------------------------------------------------------------------------------
 // k_shadow: shade HIT slots (listed at scan time), trace the vertex's shadow ray, continue or finish
 // ------------------------------------------------------------------------------------------------
@@ -722,10 +751,22 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     MfxLight* light_lds = (MfxLight*)((int*)(red + 16) + 4 * 2 * WF_SHD_LIST);
     if (threadIdx.x < sizeof(MfxLight) / 8)
         ((double*)light_lds)[threadIdx.x] = ((const double*)P.light_dev)[threadIdx.x];
+    if (threadIdx.x == 0)
+        *(ShdPtrs*)(light_lds + 1) = ShdPtrs{P.ox, P.oy, P.oz, P.dx, P.dy, P.dz, P.vei, P.vls, P.vmat, P.rn, P.depth,
+                                            P.shade, P.fstate, P.qslot, P.nox, P.noy, P.noz, P.ndx, P.ndy, P.ndz,
+                                            P.nrn, P.ndepth, P.nstate, P.nslot, P.ncount};
+    if (threadIdx.x == 1)
+        *(PixParams*)((ShdPtrs*)(light_lds + 1) + 1) =
+            PixParams{P.path_base, P.base_q, P.base_smp, P.sample_base, P.seed, P.width, P.height, P.band_index,
+                      P.band_count, P.band_rows, P.part_index, P.part_count, 0};
     load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
     const MfxLight& LT = *light_lds;
+    // the pool's and the queues' array pointers, read from LDS where they are used (the shading batch,
+    // the records) instead of held in scalar registers through the traversal loop
+    const ShdPtrs& C = *(const ShdPtrs*)(light_lds + 1);
+    const PixParams& PX = *(const PixParams*)((const ShdPtrs*)(light_lds + 1) + 1);
     const int lane = lane_id();
     const int wave = threadIdx.x >> 6;
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
@@ -770,15 +811,15 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const bool hit = (sv & ~WF_FRESH) == WF_HIT;
                     // a pool slot's miss stays as k_extend wrote it: k_resolve takes MISS as finished
                     // (its state word holds the lit vertices) and a camera ray's MISS | FRESH as black
-                    if (Q && P.qslot && sv == WF_MISS) {  // a queue entry: its slot finishes (no lit vertex: stays unfinished)
-                        const int dw = P.depth[j];
-                        if (dw >> WF_LIT_SHIFT) P.fstate[P.qslot[j]] = WF_DONE | ((dw >> WF_LIT_SHIFT) << WF_SHADE_SHIFT);
+                    if (Q && C.qslot && sv == WF_MISS) {  // a queue entry: its slot finishes (no lit vertex: stays unfinished)
+                        const int dw = C.depth[j];
+                        if (dw >> WF_LIT_SHIFT) C.fstate[C.qslot[j]] = WF_DONE | ((dw >> WF_LIT_SHIFT) << WF_SHADE_SHIFT);
                     }
                     const uint64_t hm = __ballot(hit);
                     if (hit) {
                         const int r = nshade + __popcll(hm & lanes_below());
                         // sign bit: first vertex; lit_in_hit: the lit mask in bits 28..30 (slots < 2^28)
-                        const bool lh = P.lit_in_hit && !(Q && P.qslot);
+                        const bool lh = P.lit_in_hit && !(Q && C.qslot);
                         shl[r] = (sv & WF_FRESH) ? (j | (int)0x80000000) : (lh ? j | (int)(((unsigned)sj >> 29) << 28) : j);
                         shl[WF_SHD_LIST + r] = (int)(((unsigned)sj >> WF_SHADE_SHIFT) & (lh ? 0x1ffffffu : 0x0fffffffu));
                     }
@@ -801,15 +842,15 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     j = shl[lane] & WF_ENTRY_SLOT;
                     first = shl[lane] < 0;  // draws 2, depth max_depth, no lit vertex: implicit
                     const int slot = shl[WF_SHD_LIST + lane];
-                    jr = (Q && P.qslot) ? P.qslot[j] : j;
+                    jr = (Q && C.qslot) ? C.qslot[j] : j;
                     // remaining depth | lit mask << 8: in place with lit_in_hit, the iteration's and
                     // the mask the state word carried; otherwise the depth word
                     dw = first ? P.max_depth
-                               : ((P.lit_in_hit && !(Q && P.qslot))
+                               : ((P.lit_in_hit && !(Q && C.qslot))
                                       ? (P.max_depth - P.iter) | ((((unsigned)shl[lane] >> 28) & 7) << WF_LIT_SHIFT)
-                                      : P.depth[j]);
-                    hp = dv(P.ox[j], P.oy[j], P.oz[j]);
-                    const MfxShade sh = P.shade[slot];
+                                      : C.depth[j]);
+                    hp = dv(C.ox[j], C.oy[j], C.oz[j]);
+                    const MfxShade sh = C.shade[slot];
                     if ((sh.prim_kind & 3) == MFX_KIND_SPHERE) nm = vnormalize(vsub(hp, ld3(sh.n)));  // Sphere.fs:39-43
                     else nm = ld3(sh.n);
                     mat = sh.material;
@@ -819,25 +860,25 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     {
                         int x, y;
                         int64_t smp;
-                        path_pixel(P, P.path_base + jr, x, y, smp);
-                        const int64_t pixel = (int64_t)x * P.height + y;
-                        key = path_key(P.seed, (uint64_t)pixel, (uint64_t)(P.sample_base + P.part_index + smp * P.part_count));
+                        path_pixel(PX, PX.path_base + jr, x, y, smp);
+                        const int64_t pixel = (int64_t)x * PX.height + y;
+                        key = path_key(PX.seed, (uint64_t)pixel, (uint64_t)(PX.sample_base + PX.part_index + smp * PX.part_count));
                     }
-                    rn = first ? 2u : P.rn[j];  // the camera ray drew u, v
+                    rn = first ? 2u : C.rn[j];  // the camera ray drew u, v
                 }
                 // the depth -1 query's result is discarded (Integrators.fs:109): never traced
                 const bool cn = own && (dw & 0xff) - 1 >= 0;
                 // MFX_RAY_QUEUE: a continuing path's entry in the next queue, in the range of its
                 // source shard (capacity: that shard's size), one atomic per shard in the batch
                 int qi = 0;
-                if (Q && P.ncount) {
+                if (Q && C.ncount) {
                     const int g = cn ? j / shard_size : 0;
                     uint64_t rem = __ballot(cn);
                     while (rem) {
                         const int gl = __shfl(g, __builtin_ctzll(rem));
                         const uint64_t gm = __ballot(cn && g == gl);
                         unsigned long long base = 0;
-                        if (lane == __builtin_ctzll(gm)) base = atomicAdd(P.ncount + gl * WF_HS, (unsigned long long)__popcll(gm));
+                        if (lane == __builtin_ctzll(gm)) base = atomicAdd(C.ncount + gl * WF_HS, (unsigned long long)__popcll(gm));
                         base = __shfl(base, __builtin_ctzll(gm));
                         if (cn && g == gl) qi = gl * shard_size + (int)base + __popcll(gm & lanes_below());
                         rem &= ~gm;
@@ -851,20 +892,20 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                     const bool lightable = V.lightable;
                     const int v = P.max_depth - (dw & 0xff);          // this vertex's index
                     // the operands of col = INVPI * a * ei * TwoPi (Material.fs:36), c_v (k_resolve)
-                    P.vei[v * P.vstride + jr] = V.ei;
-                    P.vmat[v * P.vstride + jr] = (WfMat)mat;
-                    if (Q && cn && P.ncount) {  // the next vertex's ray in the next queue (its depth word and
+                    C.vei[v * P.vstride + jr] = V.ei;
+                    C.vmat[v * P.vstride + jr] = (WfMat)mat;
+                    if (Q && cn && C.ncount) {  // the next vertex's ray in the next queue (its depth word and
                                            // state are written after the shadow ray)
-                        P.nox[qi] = hp.x; P.noy[qi] = hp.y; P.noz[qi] = hp.z;
-                        P.ndx[qi] = wi.x; P.ndy[qi] = wi.y; P.ndz[qi] = wi.z;
-                        P.nrn[qi] = rn;
-                        P.nslot[qi] = jr;
+                        C.nox[qi] = hp.x; C.noy[qi] = hp.y; C.noz[qi] = hp.z;
+                        C.ndx[qi] = wi.x; C.ndy[qi] = wi.y; C.ndz[qi] = wi.z;
+                        C.nrn[qi] = rn;
+                        C.nslot[qi] = jr;
                     } else if (cn) {  // what the next vertex reads, in place
-                        P.rn[j] = rn;
-                        P.dx[j] = wi.x; P.dy[j] = wi.y; P.dz[j] = wi.z;
+                        C.rn[j] = rn;
+                        C.dx[j] = wi.x; C.dy[j] = wi.y; C.dz[j] = wi.z;
                     }
                     // shadow bvh.Hit(Ray(hit.point, unit), 1e-6, dist - 1e-6) (Integrators.fs:44)
-                    pd.slot[lane] = (Q && cn && P.ncount) ? qi : j;
+                    pd.slot[lane] = (Q && cn && C.ncount) ? qi : j;
                     pd.flag[lane] = (cn ? 1 : 0) | (lightable ? 2 : 0) | (v << 2) | (dw & ~0xff);
                     pd.v[0 * 64 + lane] = unit.x; pd.v[1 * 64 + lane] = unit.y; pd.v[2 * 64 + lane] = unit.z;
                     pd.v[3 * 64 + lane] = dist - 1e-6;
@@ -901,10 +942,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // read is ordered after that store by the wave_lds_sync() calls that end the shading
                 // batch (release / acquire fences at wavefront scope cover global memory as well as
                 // LDS), and one wave's vector memory operations reach its L1 in order.
-                const bool nq = Q && (vflag & 1) && P.ncount;
-                const double* hx = nq ? P.nox : P.ox;
-                const double* hy = nq ? P.noy : P.oy;
-                const double* hz = nq ? P.noz : P.oz;
+                const bool nq = Q && (vflag & 1) && C.ncount;
+                const double* hx = nq ? C.nox : C.ox;
+                const double* hy = nq ? C.noy : C.oy;
+                const double* hz = nq ? C.noz : C.oz;
                 trav_begin(T, S, dv(hx[s], hy[s], hz[s]), dv(pd.v[0 * 64 + e], pd.v[1 * 64 + e], pd.v[2 * 64 + e]),
                            pd.v[3 * 64 + e]);
 
@@ -944,10 +985,10 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             int mask = (vflag >> WF_LIT_SHIFT) & 0xffff;
             // MFX_RAY_QUEUE: s is the path's next-queue entry (it continues) or its entry in this
             // iteration's queue; its slot is read back where the slot's records are written
-            const bool nq = Q && cont0(vflag) && P.ncount;
+            const bool nq = Q && cont0(vflag) && C.ncount;
             if (!T.B.found && (vflag & 2)) {  // unoccluded: record the operands of its direct term a_v
-                const int jr = nq ? P.nslot[s] : ((Q && P.qslot) ? P.qslot[s] : s);
-                double* vl = P.vls + (int64_t)(2 * v) * P.vstride + jr;
+                const int jr = nq ? C.nslot[s] : ((Q && C.qslot) ? C.qslot[s] : s);
+                double* vl = C.vls + (int64_t)(2 * v) * P.vstride + jr;
                 vl[0] = scs;
                 if (!P.gray_light) vl[P.vstride] = ssolid;
                 mask |= 1 << v;
@@ -959,12 +1000,12 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
             // in place, NEED_EXT carries the lit mask for k_extend's pending entries (lit_in_entry)
             const int need = WF_NEED_EXT | (nq ? 0 : mask << WF_SHADE_SHIFT);
             if (nq) {
-                P.ndepth[s] = dwn;
-                P.nstate[s] = need;
-            } else if (Q && (P.ncount || P.qslot)) {  // finished; the pool's slot keeps its final words
-                if (mask) P.fstate[P.qslot ? P.qslot[s] : s] = WF_DONE | (mask << WF_SHADE_SHIFT);
+                C.ndepth[s] = dwn;
+                C.nstate[s] = need;
+            } else if (Q && (C.ncount || C.qslot)) {  // finished; the pool's slot keeps its final words
+                if (mask) C.fstate[C.qslot ? C.qslot[s] : s] = WF_DONE | (mask << WF_SHADE_SHIFT);
             } else {
-                if (cont && !P.lit_in_hit) P.depth[s] = dwn;
+                if (cont && !P.lit_in_hit) C.depth[s] = dwn;
                 P.state[s] = cont ? need : (mask ? WF_DONE | (mask << WF_SHADE_SHIFT) : WF_FREE);
             }
             active = false;
@@ -1171,7 +1212,8 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
 static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst, int nslot = 0) {
     const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
                           (size_t)4 * stack_size * 64 * sizeof(int);
-    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int) + sizeof(MfxLight)
+    return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int) + sizeof(MfxLight) + sizeof(ShdPtrs) +
+                        sizeof(PixParams)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
@@ -1247,7 +1289,9 @@ static void launch_extend_sk(const WfParams& P, int grid, bool stats, hipStream_
     else launch_extend<false, SK>(P, grid, stats, st, lds);
 }
 
-static size_t cam_lds_bytes(int stack_size) { return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64; }
+static size_t cam_lds_bytes(int stack_size) {
+    return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64 + sizeof(MfxCamera);
+}
 
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
     const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, (const void*)k_camera<false>, 256,
