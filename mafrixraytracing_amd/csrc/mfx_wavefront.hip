@@ -730,6 +730,9 @@ struct ShdPtrs {
     uint32_t* nrn;
     int32_t *ndepth, *nstate, *nslot;
     unsigned long long* ncount;
+    unsigned long long *ctl, *counters;
+    int32_t* state;
+    const unsigned long long* qcount;
 };
 
 // ------------------------------------------------------------------------------------------------
@@ -754,7 +757,8 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     if (threadIdx.x == 0)
         *(ShdPtrs*)(light_lds + 1) = ShdPtrs{P.ox, P.oy, P.oz, P.dx, P.dy, P.dz, P.vei, P.vls, P.vmat, P.rn, P.depth,
                                             P.shade, P.fstate, P.qslot, P.nox, P.noy, P.noz, P.ndx, P.ndy, P.ndz,
-                                            P.nrn, P.ndepth, P.nstate, P.nslot, P.ncount};
+                                            P.nrn, P.ndepth, P.nstate, P.nslot, P.ncount, P.ctl, P.counters, P.state,
+                                            P.qcount};
     if (threadIdx.x == 1)
         *(PixParams*)((ShdPtrs*)(light_lds + 1) + 1) =
             PixParams{P.path_base, P.base_q, P.base_smp, P.sample_base, P.seed, P.width, P.height, P.band_index,
@@ -803,7 +807,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 // list hits from as many windows as it takes (state words only): a camera ray's miss
                 // frees its slot (TraceRay returns black, Integrators.fs:137), a later miss finishes
                 // its path with the radiance already in the slot
-                while (nshade < 64 && sc.window(P.ctl + WF_CTL_SHD, P.chunk_shd, shard_size, P.state, Q ? P.qcount : nullptr, P.ctl + WF_CTL_CLOSED_SHD)) {
+                while (nshade < 64 && sc.window(C.ctl + WF_CTL_SHD, P.chunk_shd, shard_size, C.state, Q ? C.qcount : nullptr, C.ctl + WF_CTL_CLOSED_SHD)) {
                     if (DG) dg.windows++;
                     const int j = sc.win_next + lane;
                     const int sj = sc.word();
@@ -824,7 +828,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                         shl[WF_SHD_LIST + r] = (int)(((unsigned)sj >> WF_SHADE_SHIFT) & (lh ? 0x1ffffffu : 0x0fffffffu));
                     }
                     nshade += __popcll(hm);
-                    sc.advance(P.state);
+                    sc.advance(C.state);
                 }
                 wave_lds_sync();
                 DIAG_MARK(dg, scan, DG);
@@ -1006,13 +1010,13 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                 if (mask) C.fstate[C.qslot ? C.qslot[s] : s] = WF_DONE | (mask << WF_SHADE_SHIFT);
             } else {
                 if (cont && !P.lit_in_hit) C.depth[s] = dwn;
-                P.state[s] = cont ? need : (mask ? WF_DONE | (mask << WF_SHADE_SHIFT) : WF_FREE);
+                C.state[s] = cont ? need : (mask ? WF_DONE | (mask << WF_SHADE_SHIFT) : WF_FREE);
             }
             active = false;
         }
         DIAG_MARK(dg, fin, DG);
     }
-    unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
+    unsigned long long* cnt = C.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 2, c_shadow, red);
     if (DG) block_add<4>(cnt + 15, dg.node_iters, red);
     if (DG && lane == 0) {
