@@ -180,6 +180,7 @@ struct mfx_ctx {
     double* d_albedo = nullptr;      // [nmat][3]
     MfxLight* d_light = nullptr;     // the light (k_shadow reads it into LDS)
     MfxCamera* d_cam = nullptr;      // the camera (k_camera reads it into LDS)
+    const void** d_refs = nullptr;   // {d_slot_ref, d_ref_blob} (k_shadow reads them into LDS)
     // render-ahead (mfx_options.render_ahead; see the section above mfx_render_rgba8): one-sample
     // render calls take their frame from batches of the next render_ahead samples, traced and
     // post-processed ahead of the calls, the next batch in the background while the current one is
@@ -266,7 +267,7 @@ static void free_ctx(mfx_ctx* c) {
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     if (c->d_merge) (void)hipFree(c->d_merge);
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_light, c->d_cam};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_light, c->d_cam, (void*)c->d_refs};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     ahead_free(c);
@@ -322,6 +323,7 @@ static int ctx_setup(mfx_ctx* c) {
     CK(upload(&c->d_albedo, c->host.albedo));
     CK(upload(&c->d_light, std::vector<MfxLight>{c->host.light}));
     CK(upload(&c->d_cam, std::vector<MfxCamera>{c->host.camera}));
+    CK(upload(&c->d_refs, std::vector<const void*>{c->d_slot_ref, c->d_ref_blob}));
     const bool inst = !c->host.inst.empty();
     const int ninst = (int)c->host.inst.size();
     if (inst) {
@@ -779,6 +781,7 @@ static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.light = c->host.light;
     P.light_dev = c->d_light;
     P.cam_dev = c->d_cam;
+    P.refs_dev = c->d_refs;
     P.cam = c->host.camera;
     // a gray light (bitwise equal intensities): k_shadow records a lit vertex's direct term itself
     P.gray_light = std::memcmp(&P.light.color[0], &P.light.color[1], sizeof(double)) == 0 &&

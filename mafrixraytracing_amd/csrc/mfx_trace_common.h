@@ -228,6 +228,12 @@ __device__ __forceinline__ bool sphere_hit64(const MfxSlot& s, DV o, DV d, doubl
     return false;
 }
 
+// a reference leaf's arrays, read where a candidate needs its whole reference leaf (rare: a hit at
+// t >= tMax); k_shadow keeps them in LDS instead of in scalar registers (SceneView::refs)
+struct SceneRefs {
+    const int32_t* slot_ref;
+    const uint8_t* ref_blob;
+};
 struct SceneView {
     const MfxNode* __restrict__ nodes;
     const MfxSlot* __restrict__ slots;     // traversal leaves: runs of MfxSlot records
@@ -240,6 +246,7 @@ struct SceneView {
     // per slot; wavefront kernels), or none: nslot_lds is the slot count or 0
     const int4* slots_lds;
     int nslot_lds;
+    const SceneRefs* refs = nullptr;  // non-null: slot_ref / ref_blob are read from here (LDS)
 };
 
 // An instance's record: from the kernel's LDS copy when it holds it, else from global memory
@@ -578,7 +585,9 @@ __device__ __forceinline__ bool leaf_hit(const SceneView& S, int code, DV o, DV 
         if (t >= tMax) {
             double t2;
             int info2, first2;
-            if (ref_leaf_hit(S.ref_blob, S.slot_ref[s0 + hs], o, d, tMin, tMax, t2, info2, first2, shd)) {
+            const int32_t* sref = S.refs ? S.refs->slot_ref : S.slot_ref;
+            const uint8_t* rblob = S.refs ? S.refs->ref_blob : S.ref_blob;
+            if (ref_leaf_hit(rblob, sref[s0 + hs], o, d, tMin, tMax, t2, info2, first2, shd)) {
                 if (shd) return true;
                 if (beats(B, t2, first2, info2)) {
                     B = Best{t2, info2, first2, true};

@@ -654,8 +654,11 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     // the camera in LDS (read per window), not held in scalar registers through the packet walk
     MfxCamera* cam_lds = (MfxCamera*)(red + 16);
     if (threadIdx.x < sizeof(MfxCamera) / 8) ((double*)cam_lds)[threadIdx.x] = ((const double*)P.cam_dev)[threadIdx.x];
+    // the reference-leaf arrays too (as k_shadow): `nodes` and `slots` alone stay in scalar registers
+    SceneRefs* refs_lds = (SceneRefs*)(cam_lds + 1);
+    if (threadIdx.x == 64) *refs_lds = SceneRefs{(const int32_t*)P.refs_dev[0], (const uint8_t*)P.refs_dev[1]};
     __syncthreads();
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, nullptr, 0};
+    const SceneView S{P.nodes, P.slots, nullptr, nullptr, P.inst, nullptr, 0, nullptr, 0, refs_lds};
     const int shard_size = P.pool / WF_SHARDS;
     Scanner sc{};
     sc.shard = blockIdx.x & (WF_SHARDS - 1);
@@ -759,6 +762,9 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
                                             P.shade, P.fstate, P.qslot, P.nox, P.noy, P.noz, P.ndx, P.ndy, P.ndz,
                                             P.nrn, P.ndepth, P.nstate, P.nslot, P.ncount, P.ctl, P.counters, P.state,
                                             P.qcount};
+    SceneRefs* refs_lds = (SceneRefs*)((PixParams*)((ShdPtrs*)(light_lds + 1) + 1) + 1);
+    if (threadIdx.x == 2)  // (from device memory: kernel arguments beside `nodes` would be loaded with it)
+        *refs_lds = SceneRefs{(const int32_t*)P.refs_dev[0], (const uint8_t*)P.refs_dev[1]};
     if (threadIdx.x == 1)
         *(PixParams*)((ShdPtrs*)(light_lds + 1) + 1) =
             PixParams{P.path_base, P.base_q, P.base_smp, P.sample_base, P.seed, P.width, P.height, P.band_index,
@@ -776,7 +782,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     using Stack = typename std::conditional<SPILL, SpillStack, LdsStack>::type;
     const Stack stack = make_stack<SPILL>(lds + wave * P.stack_lds_shd * 64 + lane, P, P.stack_lds_shd);
     const PendShd pd(pend_base + wave * PendShd::BYTES);
-    const SceneView S{P.nodes, P.slots, P.slot_ref, P.ref_blob, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, nslot};
+    const SceneView S{P.nodes, P.slots, nullptr, nullptr, P.inst, inst_lds, INST ? P.ninst_lds : 0, slot_lds, nslot, refs_lds};
     const int shard_size = P.pool / WF_SHARDS;
 
     int* shl = (int*)(red + 16) + wave * 2 * WF_SHD_LIST;  // shade list: [0,128) path slots, [128,256) shade indices
@@ -1217,7 +1223,7 @@ static size_t wf_lds_bytes(int stack_size, bool shadow, int ntop, int ninst, int
     const size_t stacks = (size_t)ntop * sizeof(MfxNode) + (size_t)ninst * sizeof(MfxInstance) + (size_t)nslot * 80 +
                           (size_t)4 * stack_size * 64 * sizeof(int);
     return shadow ? stacks + 4 * PendShd::BYTES + 64 + 4 * 2 * WF_SHD_LIST * sizeof(int) + sizeof(MfxLight) + sizeof(ShdPtrs) +
-                        sizeof(PixParams)
+                        sizeof(PixParams) + sizeof(SceneRefs)
                   : stacks + 4 * WF_EXT_PEND * sizeof(int) + 64;
 }
 
@@ -1294,7 +1300,7 @@ static void launch_extend_sk(const WfParams& P, int grid, bool stats, hipStream_
 }
 
 static size_t cam_lds_bytes(int stack_size) {
-    return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64 + sizeof(MfxCamera);
+    return (size_t)4 * stack_size * (sizeof(int) + sizeof(uint64_t)) + 64 + sizeof(MfxCamera) + sizeof(SceneRefs);
 }
 
 hipError_t mfx_cam_occupancy(int stack_size, int* blocks_per_cu) {
