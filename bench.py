@@ -47,11 +47,23 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-# Hardware queues per process, read by the HIP runtime when it initializes (before any GPU call
-# here). A rank keeps up to three contexts' streams in flight (distributed.frames_in_flight) beside
-# torch's and RCCL's; with HIP's default of 4 queues two of them share one and serialize, and C2's
-# 1/8 share runs 5.03 instead of 4.70 ms per step (profiles/r05/r05w_*). An explicit setting wins.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+# Hardware queues per process. A rank keeps up to three contexts' streams in flight
+# (distributed.frames_in_flight) beside torch's and RCCL's; with HIP's default of 4 queues two of
+# them share one and serialize: C2's 1/8 share 4.59 instead of 4.26 ms per step in bench.py's
+# strong_share (profiles/r05/r05zm_*, r05zo_*). The HIP runtime takes GPU_MAX_HW_QUEUES from the
+# environment the process starts with (setting os.environ here is too late), so without it bench.py
+# runs itself as a child process with GPU_MAX_HW_QUEUES=8 and exits with the child's code, before
+# anything here touches the GPU (signals are forwarded). An explicit setting wins.
+HW_QUEUES = "8"
+
+
+def _relaunch_with_hw_queues():
+    import signal
+    env = dict(os.environ, GPU_MAX_HW_QUEUES=HW_QUEUES)
+    child = subprocess.Popen([sys.executable] + sys.argv, env=env)
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, lambda s, f: child.send_signal(s))
+    sys.exit(child.wait())
 
 METRIC = "Mrays/s (primary+secondary) at 1080p/64spp; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
@@ -97,6 +109,8 @@ def parse():
     ap.add_argument("--api", default="batch", choices=["batch", "render"],
                     help="batch: mfx_trace_accumulate of the frame's spp; render: spp x mfx_render_rgba8(1)")
     ap.add_argument("--no-render-api", action="store_true", help="skip the render_api sub-measurement")
+    # internal: measure strong_share in this (fresh) process for the parent run's VALUE_1GPU, MS_1GPU
+    ap.add_argument("--strong-share-child", nargs=2, type=float, default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
 
 
@@ -340,7 +354,8 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
                            (ms_1gpu / n) / (t_rank * max(1.0, ov["trace_ms_beside_it"] / ov["trace_ms_alone"]) +
                                             (0.0 if ov["exchange_completion_ms"] < t_rank else t_ex)), 4)}
     return {"shares": out, "partition": "image: tile rows r mod N per rank (MFX_F_ROW_PARTITION), RowGather to rank 0",
-            "note": "every rank's share of --scaling strong at N GPUs, measured on one GPU one after another; "
+            "note": "every rank's share of --scaling strong at N GPUs, measured on one GPU one after another, in a fresh "
+                    "process (bench.py --strong-share-child); "
                     "the exchange's pack/unpack measured here, its transfer modeled at one xGMI link "
                     f"({XGMI_LINK_GBS:.0f} GB/s) per sending rank; predicted_efficiency counts the exchange in full "
                     "(not overlapped); predicted_efficiency_pipelined uses overlap_measured (rank 0's pack + unpack "
@@ -360,6 +375,13 @@ def main():
     if args.spp is None:
         args.spp = cfg_spp
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.strong_share_child is not None:  # a fresh process, as a rank's own process runs its share
+        from mafrixraytracing_amd.native import DEFAULT_SEED
+        from mafrixraytracing_amd.scene_io import load_scene_file
+        share = strong_share(load_scene_file(args.scene), DEFAULT_SEED, args.spp, args.strong_share_child[0],
+                             args.strong_share_child[1], steps=args.steps, flags=CONFIG_FLAGS.get(args.config, 0))
+        print(json.dumps(share), file=json_out, flush=True)
+        return
     if args.gpus > 1 and not args.single_process and "RANK" not in os.environ:
         sys.exit(relaunch_distributed(args))
     rank = int(os.environ.get("RANK", "0"))
@@ -787,9 +809,16 @@ def main():
             sapi = sample_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
             sapi["vs_batch"] = round(sapi["value"] / value, 4)
             # each rank's share timed over the line's own step count (its frames-in-flight pipeline
-            # fills and drains between the barriers, as an N-GPU run of these steps does)
-            share = strong_share(arrays, DEFAULT_SEED, args.spp, value, elapsed / args.steps * 1e3,
-                                 steps=args.steps, flags=cf)
+            # fills and drains between the barriers, as an N-GPU run of these steps does), in a fresh
+            # process as a rank's own process runs it: this process's earlier contexts and streams
+            # (render_api, sample_api) slowed the 1/8 share by ~8 % (profiles/r05/r05zm_*, r05zo_*)
+            cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--spp", str(args.spp),
+                   "--scene", args.scene, "--steps", str(args.steps),
+                   "--strong-share-child", repr(float(value)), repr(float(elapsed / args.steps * 1e3))]
+            pc = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+            if pc.returncode != 0:
+                raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
+            share = json.loads(pc.stdout.strip().splitlines()[-1])
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
@@ -841,4 +870,6 @@ def main():
 
 
 if __name__ == "__main__":
+    if os.environ.get("GPU_MAX_HW_QUEUES") is None:
+        _relaunch_with_hw_queues()
     main()

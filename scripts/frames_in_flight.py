@@ -42,7 +42,12 @@ def main():
     ap.add_argument("--steps", type=int, default=12)
     ap.add_argument("--parts", default="1,2,4,8")
     ap.add_argument("--modes", default="1,2", help="contexts in flight per run, comma-separated")
+    ap.add_argument("--torch", default="", help="'import' or 'cuda': import torch (and initialize its HIP context) first")
     a = ap.parse_args()
+    if a.torch:
+        import torch
+        if a.torch == "cuda":
+            torch.zeros(1, device="cuda")
     from mafrixraytracing_amd.abi import MFX_F_IN_FLIGHT, MFX_F_ROW_PARTITION
     from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file

@@ -21,6 +21,8 @@
 #   diagab:SCENE:SPP     per-iteration stage times of every build_variants/*.so (with its .env), 2 rounds
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
 set -e
+# the hardware queues bench.py would relaunch itself with (so rocprofv3 sees one process)
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd $R
 TAG=$1
