@@ -34,6 +34,15 @@ Extra objects on the JSON line:
                 workload's paths (rank 0, N = 1 only): "strict" (the FP64 restatement of the
                 reference algorithm; `value`) and "fast" (SAH BVH2, tMax culling, any-hit
                 shadows), with the thread count, nproc and CPU model
+  sample_api    (N = 1) mfx_sample: the trace, the mean kernel and the FP64 frame's readback
+  strong_share  (N = 1) every rank's share of the strong job at N = 2, 4, 8 timed on this GPU in a
+                fresh process (--strong-share-child), frames in flight as the N-GPU ranks keep
+                them, the exchange's pack/unpack measured and its transfer modeled, and the
+                predicted efficiency with and without the measured overlap
+
+A rank whose frame is small rotates frames over three contexts (distributed.frames_in_flight,
+MFX_F_IN_FLIGHT); their streams need hardware queues of their own, so bench.py runs with
+GPU_MAX_HW_QUEUES=8 (relaunching itself as a child when the environment lacks it).
 """
 from __future__ import annotations
 
