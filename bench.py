@@ -42,7 +42,8 @@ Extra objects on the JSON line:
 
 A rank whose frame is small rotates frames over three contexts (distributed.frames_in_flight,
 MFX_F_IN_FLIGHT); their streams need hardware queues of their own, so bench.py runs with
-GPU_MAX_HW_QUEUES=8 (relaunching itself as a child when the environment lacks it).
+GPU_MAX_HW_QUEUES=8 (relaunching itself as a child when the environment lacks it; under a profiler,
+which has initialised the GPU before bench.py starts, it refuses instead: set it in the environment).
 """
 from __future__ import annotations
 
@@ -821,13 +822,18 @@ def main():
             # fills and drains between the barriers, as an N-GPU run of these steps does), in a fresh
             # process as a rank's own process runs it: this process's earlier contexts and streams
             # (render_api, sample_api) slowed the 1/8 share by ~8 % (profiles/r05/r05zm_*, r05zo_*)
-            cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--spp", str(args.spp),
-                   "--scene", args.scene, "--steps", str(args.steps),
-                   "--strong-share-child", repr(float(value)), repr(float(elapsed / args.steps * 1e3))]
-            pc = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-            if pc.returncode != 0:
-                raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
-            share = json.loads(pc.stdout.strip().splitlines()[-1])
+            # (never from a profiled process: the profiler initialised the GPU before this one started)
+            cmd = None if _under_profiler() else \
+                [sys.executable, os.path.abspath(__file__), "--config", args.config, "--spp", str(args.spp),
+                 "--scene", args.scene, "--steps", str(args.steps),
+                 "--strong-share-child", repr(float(value)), repr(float(elapsed / args.steps * 1e3))]
+            if cmd is None:
+                share = {"skipped": "under a profiler"}
+            else:
+                pc = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+                if pc.returncode != 0:
+                    raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
+                share = json.loads(pc.stdout.strip().splitlines()[-1])
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
@@ -878,7 +884,19 @@ def main():
     return result
 
 
+def _under_profiler():
+    """rocprofv3 (or another ROCm profiler) preloads a library that initialises the GPU before this
+    script starts: a process it started must not start bench.py again."""
+    if any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ):
+        return True
+    return "rocprof" in os.environ.get("LD_PRELOAD", "")
+
+
 if __name__ == "__main__":
     if os.environ.get("GPU_MAX_HW_QUEUES") is None:
+        if _under_profiler():
+            sys.exit("bench.py: under a profiler GPU_MAX_HW_QUEUES must be set in the environment "
+                     "(e.g. GPU_MAX_HW_QUEUES=8 rocprofv3 ... -- python3 bench.py); bench.py does not start "
+                     "a copy of itself from a profiled process")
         _relaunch_with_hw_queues()
     main()

@@ -2,6 +2,8 @@
 # Bench lines for every BASELINE.json GPU config at N = 1 (C2 the metric's; C4/C5 one GPU's share
 # of their 8-GPU workloads) plus the per-iteration diagnostic of C2. Run on the GPU box from the
 # repo root: scripts/bench_configs.sh TAG
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}

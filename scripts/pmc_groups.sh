@@ -1,6 +1,8 @@
 #!/bin/bash
 # One rocprofv3 --pmc pass per counter group on the bench workload; summary per kernel.
 # Usage: scripts/pmc_groups.sh TAG "GROUP1" "GROUP2" ...
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
 OUT=$R/gpurun_out/pmc_$TAG

@@ -1,5 +1,7 @@
 #!/bin/bash
 # SQ / TCP / TCC counter passes for the trace kernel (one rocprofv3 --pmc pass per group).
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/pmc_${1:-r01}
 mkdir -p $OUT

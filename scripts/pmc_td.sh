@@ -2,6 +2,8 @@
 # TD / TCP / SQ memory-pipeline counters of the wavefront kernels, the groups of round 1's
 # profiles/r01b_pmc_td_tcp_utcl1.txt (one rocprofv3 --pmc pass per group), on the C2 bench step.
 # Usage: scripts/pmc_td.sh TAG [extra bench args...]
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-td}
 shift || true

@@ -8,6 +8,8 @@
 # reads its nodes and slots through the scalar cache: its roof). scripts/summarize_td.py writes
 # profiles/td_<scene>.json, which bench.py reads for roofline.td / roofline.smem.
 # Usage: scripts/pmc_td_roof.sh TAG [extra bench args...]
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-td}

@@ -1,6 +1,8 @@
 #!/bin/bash
 # VALU / FP64 instruction mix and wave activity of the trace kernels on the C2 bench step (two
 # rocprofv3 --pmc passes of 8 counters each, kernel trace on) -> gpurun_out/r04y/summary.txt
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/r04y

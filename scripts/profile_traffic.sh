@@ -4,6 +4,8 @@
 # passes: the two counters do not fit one TCC pass on gfx950). Then summarise into
 # $OUT/traffic.json (per-kernel HBM bytes per launch, gfx950 FETCH_SIZE correction applied).
 # Usage: scripts/profile_traffic.sh TAG [extra bench args...]
+# bench.py refuses to relaunch itself under rocprofv3: the hardware queues come from here
+export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-r01}
