@@ -119,6 +119,10 @@ def parse():
     ap.add_argument("--api", default="batch", choices=["batch", "render"],
                     help="batch: mfx_trace_accumulate of the frame's spp; render: spp x mfx_render_rgba8(1)")
     ap.add_argument("--no-render-api", action="store_true", help="skip the render_api sub-measurement")
+    ap.add_argument("--sample-base", type=int, default=0,
+                    help="global sample index of the first warmup step's first sample (steps follow on)")
+    ap.add_argument("--no-verify", action="store_true",
+                    help="N > 1: skip the merged-frame check against one GPU (merged_equals_1gpu)")
     # internal: measure strong_share in this (fresh) process for the parent run's VALUE_1GPU, MS_1GPU
     ap.add_argument("--strong-share-child", nargs=2, type=float, default=None, help=argparse.SUPPRESS)
     return ap.parse_args()
@@ -372,6 +376,94 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
                     "on a second stream 1 ms into its trace: its completion time and the trace's time beside it)"}
 
 
+def topology(ctx, use_dist, dist, backend, local, world, single_process):
+    """Where the job ran: the process group (world, backend) and every rank's device (ordinal, and
+    the device's UUID where torch reports one), or for one process the library context's device list
+    and the RCCL communicators it created (mfx_device_info). One process per GPU must use distinct
+    devices unless the one-GPU rehearsal (MFX_BENCH_DEVICE) pins them all to one: anything else fails."""
+    out = {}
+    if use_dist:
+        import torch
+        uid = None
+        try:
+            uid = str(torch.cuda.get_device_properties(local).uuid)
+        except Exception:
+            pass
+        mine = {"device": local, "uuid": uid}
+        allv = [None] * world
+        dist.all_gather_object(allv, mine)
+        devs = [(v["device"], v["uuid"]) for v in allv]
+        distinct = len(set(devs)) == len(devs)
+        pinned = os.environ.get("MFX_BENCH_DEVICE") is not None
+        if not distinct and not pinned:
+            raise RuntimeError(f"ranks share a device: {devs}")
+        out.update({"rccl_world": dist.get_world_size(), "backend": dist.get_backend(), "requested_backend": backend,
+                    "rank_devices": [d for d, _ in devs], "rank_device_uuids": [u for _, u in devs],
+                    "distinct_devices": distinct, "pinned_one_device": pinned})
+    info = ctx.device_info()
+    out["library_context"] = info
+    if single_process:
+        out["single_process_devices"] = info["devices"]
+        out["communicators"] = info["communicators"]
+    return out
+
+
+def verify_merge(arrays, ctx, ctxs, pr, accs, gathers, rank, world, local, backend, spp, mode, rows, single_process,
+                 devices, npix):
+    """One more frame of the line's job, untimed: traced as the timed steps trace it (every rank its
+    partition, merged to rank 0 by the line's exchange; or the one-process context over its device
+    list and the library's merge), then the same samples traced whole on one GPU by a fresh context.
+    merged_equals_1gpu: the two FP64 accumulators are equal bit for bit (the image partition's claim).
+    A sample partition merges sums in another order: exact equality is not expected there, and its
+    max_abs_diff is reported. Every rank joins (collectives); rank 0 returns the result."""
+    import hashlib
+    import time as _t
+    import torch
+    from mafrixraytracing_amd.distributed import PipelinedNativeRender
+    from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
+    vbase = 1 << 30  # a sample range no timed step used
+    dev = devices[0] if single_process else local
+    nbytes = 3 * npix * 8
+    if pr is not None:
+        pr.drain()
+        pv = PipelinedNativeRender(ctxs[:1], accs[:2], rank, world, gathers=gathers[:2] if gathers else None)
+        pv.frame(spp, vbase, all_ranks=backend == "gloo")
+        pv.drain()
+        merged = pv.buffer(0)
+        import torch.distributed as dist
+        dist.barrier()
+    else:
+        merged = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{dev}")
+        ctx.accum_attach(merged.data_ptr(), nbytes)
+        ctx.accum_clear()
+        ctx.trace_accumulate(spp, vbase)
+        ctx.accum_reduce()
+        ctx.sync()
+        ctx.accum_attach(None)
+    if rank != 0:
+        return None
+    ref = torch.zeros(3 * npix, dtype=torch.float64, device=f"cuda:{dev}")
+    t0 = _t.perf_counter()
+    with NativeContext(arrays, seed=DEFAULT_SEED, device=dev, flags=mode) as rc:  # whole film, every sample
+        rc.accum_attach(ref.data_ptr(), nbytes)
+        rc.accum_clear()
+        rc.trace_accumulate(spp, vbase)
+        rc.sync()
+        rc.accum_attach(None)
+    ms = (_t.perf_counter() - t0) * 1e3
+    torch.cuda.synchronize(dev)
+    exact = bool(torch.equal(merged, ref))
+    diff = float((merged - ref).abs().max().item())
+    dig = lambda t: hashlib.blake2b(t.cpu().numpy().tobytes(), digest_size=8).hexdigest()
+    image_part = rows or single_process
+    return {"merged_equals_1gpu": exact, "exact_expected": bool(image_part), "max_abs_diff": diff,
+            "digest_merged": dig(merged), "digest_1gpu": dig(ref), "spp": spp, "sample_base": vbase,
+            "nonzero_pixels_1gpu": int((ref[:npix] != 0).sum().item()), "ms_1gpu_check": round(ms, 2),
+            "note": "one more frame of the line's job after the timed steps (untimed), merged as the steps merge it, "
+                    "against a fresh one-GPU context tracing the same samples of the whole film; FP64 accumulators "
+                    "compared bit for bit (digest: blake2b-64 of their bytes)"}
+
+
 def main():
     args = parse()
     # the JSON line is the only thing on stdout: libraries that print banners there (RCCL prints
@@ -449,9 +541,12 @@ def main():
     nctx = max(nif, o_nif)
     if nctx > 1:
         rank_mode |= MFX_F_IN_FLIGHT
-    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank, part_count=world,
+    # MFX_BENCH_FAULT=partition (tests only): rank r > 0 traces rank r - 1's partition, so one partition
+    # is traced twice and one not at all: the merged-frame check must catch it
+    part = max(0, rank - 1) if os.environ.get("MFX_BENCH_FAULT") == "partition" else rank
+    ctx = NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=part, part_count=world,
                         devices=devices, render_ahead=args.render_ahead if args.api == "render" else 0)
-    ctxs = [ctx] + [NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=rank,
+    ctxs = [ctx] + [NativeContext(arrays, seed=DEFAULT_SEED, device=local, flags=rank_mode, part_index=part,
                                   part_count=world) for _ in range(nctx - 1)]
 
     def totals():  # the timed steps' rays, summed on the device over this rank's contexts
@@ -484,7 +579,7 @@ def main():
             c.sync()
 
     def step(k):
-        base = k * spp_step
+        base = args.sample_base + k * spp_step
         if args.api == "render":  # Scene.Render x spp: 1 spp per call, film + post + readback
             for _ in range(spp_step):
                 ctx.render_rgba8(1, out=rbuf)
@@ -558,7 +653,7 @@ def main():
             po = PipelinedNativeRender(ctxs[:o_nif], accs, rank, world, gathers=gathers)
 
         def other_step(k):
-            base = (args.warmup + args.steps) * spp_step + k * o_spp
+            base = args.sample_base + (args.warmup + args.steps) * spp_step + k * o_spp
             if po is not None:
                 po.frame(o_spp, base, all_ranks=backend == "gloo")
             else:
@@ -581,12 +676,21 @@ def main():
         c = totals()
         o_el, o_rays = job_max_sum(time.perf_counter() - ts, c[0] + c[1] + c[2])
         other = {"scaling": o_scaling, "global_spp_per_step": o_spp,
+                 "first_timed_sample": args.sample_base + (args.warmup + args.steps) * spp_step + o_spp,
                  "frames_in_flight": frames_in_flight(W, H, o_spp, world, rows) if use_dist else 1,
                  "spp_per_gpu": o_spp if rows else o_spp / ngpu,
                  "film_share_per_gpu": round(1.0 / ngpu, 6) if rows else 1.0,
                  "value": round(o_rays / o_el / 1e6, 2), "unit": "Mrays/s", "steps": args.steps,
                  "ms_per_step": round(o_el / args.steps * 1e3, 3), "rays_per_step": o_rays / args.steps,
                  "note": f"the same job {o_scaling}-scaled (whole-job Mrays/s), measured after the line's steps"}
+    # N > 1 (and the forced multi-process path): the job's merged frame against the same samples traced
+    # whole on one GPU, after every timed measurement (VERDICT r05 Next #2), and the topology it ran on
+    verify = topo = None
+    if ngpu > 1 or use_dist:
+        topo = topology(ctx, use_dist, dist, backend, local, world, args.single_process)
+        if args.api == "batch" and not args.no_verify:
+            verify = verify_merge(arrays, ctx, ctxs, pr, accs if use_dist else None, gathers if use_dist else None,
+                                  rank, world, local, backend, spp_step, mode, rows, args.single_process, devices, npix)
     stage_ms = {k: float(np.mean([t[k] for t in timings]))
                 for k in ("total_ms", "camera_ms", "extend_ms", "camera_launches", "shadow_ms", "iterations", "launches",
                           "generations")}
@@ -873,6 +977,11 @@ def main():
                        "parallelism": par},
             "roofline": roofline, "render_api": rapi, "sample_api": sapi, "strong_share": share, "cpu_baseline": cpu,
         }
+        if topo is not None:
+            result["topology"] = topo
+        if verify is not None:
+            result["verify"] = verify
+            result["merged_equals_1gpu"] = verify["merged_equals_1gpu"]
         if other is not None:
             result[other["scaling"]] = other
         print(json.dumps(result), file=json_out, flush=True)

@@ -242,7 +242,8 @@ int mfx_film_mean(mfx_ctx* ctx, double* frame_xmajor_rgba);
 int mfx_trace_accumulate(mfx_ctx* ctx, int32_t spp, int64_t sample_base);
 /* Multi-device context: sum every device's accumulator into the primary's (RCCL reduce, root
  * devices[0]), ordered after each device's trace: after a clear and a trace, an exact merge of
- * the devices' tile rows. No-op on a single-device context. mfx_sample calls it itself.       */
+ * the devices' tile rows. No-op on a single-device context, and on an accumulator already merged
+ * since the last trace, clear or attach. mfx_sample calls it itself.                             */
 int mfx_accum_reduce(mfx_ctx* ctx);
 int mfx_accum_clear(mfx_ctx* ctx);
 /* Device pointer + byte size of the (primary device's) FP64 accumulator (for an RCCL reduce
@@ -253,7 +254,9 @@ int mfx_accum_device_ptr(mfx_ctx* ctx, void** dptr, int64_t* nbytes);
  * context's own buffer. The caller keeps it alive until detached or mfx_destroy.            */
 int mfx_accum_attach(mfx_ctx* ctx, void* dptr, int64_t nbytes);
 /* Copy accumulator / count to host as x-major RGBA doubles (alpha = 1): the division by the
- * sample count itself, as `color / float n` (Integrators.fs:171). count must be > 0.         */
+ * sample count itself, as `color / float n` (Integrators.fs:171). count must be > 0. On a device
+ * list it reads the merged accumulator: a trace not merged since (mfx_trace_accumulate, or the
+ * trace of an mfx_render_rgba8 call without render-ahead) is merged first (mfx_accum_reduce).   */
 int mfx_accum_read_mean(mfx_ctx* ctx, double count, double* frame_xmajor_rgba);
 int mfx_sync(mfx_ctx* ctx);
 /* The HIP stream (hipStream_t) the context launches on, for event timing by the caller.   */
@@ -338,6 +341,13 @@ int mfx_fp64_selftest(int32_t device, int64_t n, const double* a, const double* 
  * left to the FP64 test) and the vertex-box proof's (1 proved to pass, 0 not proved). Wherever a
  * shortcut decides it must agree with the FP64 answer.                                         */
 int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out);
+
+/* How a context's work is laid over devices (ABI 6, additive): out[0] = devices G, out[1] = RCCL
+ * communicators the context created (G for a list of distinct devices, else 0), out[2] = how
+ * mfx_accum_reduce merges (0 one device, 1 RCCL reduce, 2 device-ordered adds: a repeated device),
+ * out[3] / out[4] = the primary's tile-row band (band_index, band_count: rows r % band_count ==
+ * band_index), out[5 + g] = device g's HIP ordinal. cap = entries of out (>= 5 + G).          */
+int mfx_device_info(mfx_ctx* ctx, int32_t* out, int32_t cap);
 
 /* ---- misc -------------------------------------------------------------------------------- */
 const char* mfx_last_error(void);

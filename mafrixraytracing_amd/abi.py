@@ -173,6 +173,7 @@ def _bind(lib):
         "mfx_aabb_selftest": (C.c_int, [C.c_int32, C.c_int64, _dp, _ip]),
         "mfx_build_leaves": (C.c_int, [_P(MfxSceneDesc), _ip, _ip, _ip, _ip, _ip]),
         "mfx_build_info": (C.c_int, [C.c_void_p, _dp, _P(C.c_uint64)]),
+        "mfx_device_info": (C.c_int, [C.c_void_p, _ip, C.c_int32]),
         "mfx_last_error": (C.c_char_p, []),
         "mfx_abi_version": (C.c_int, []),
         "mfx_device_count": (C.c_int, []),
@@ -189,7 +190,7 @@ EXPORTED_SYMBOLS = [
     "mfx_film_mean", "mfx_stats",
     "mfx_trace_accumulate", "mfx_accum_clear", "mfx_accum_reduce", "mfx_accum_device_ptr", "mfx_accum_attach", "mfx_accum_read_mean",
     "mfx_sync", "mfx_stream", "mfx_ray_counts", "mfx_last_trace_ms", "mfx_trace_timing", "mfx_ray_counts_total", "mfx_closest_hit", "mfx_any_hit", "mfx_ref_leaves",
-    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
+    "mfx_fp64_selftest", "mfx_aabb_selftest", "mfx_build_leaves", "mfx_build_info", "mfx_device_info", "mfx_last_error", "mfx_abi_version", "mfx_device_count",
 ]
 
 _lib = None

@@ -141,6 +141,7 @@ struct mfx_ctx {
     WfParams wf{};
     void* wf_mem = nullptr;
     int32_t wf_pool = 0;
+    size_t wf_pool_bytes = 0;  // bytes of wf_mem
     bool wf_pool_q = false;  // the pool holds the ray queues' arrays too (allocated only for a trace that uses them)
     // MFX_RAY_QUEUE: the ray queues, and the first iteration (0-based) whose k_shadow moves the
     // continuing paths to one (-1: every iteration in place; MFX_RAY_QUEUE=0 / MFX_QUEUE_FROM=d)
@@ -217,6 +218,8 @@ struct mfx_ctx {
     std::vector<mfx_ctx*> peers;         // devices[1..G) of the device list, same host scene
     std::vector<ncclComm_t> comms;       // [G] one RCCL communicator per device, rank g = device g
     double* d_merge = nullptr;           // [3][npix] the devices' films merged (mfx_film_mean), allocated on first use
+    bool accum_merged = true;            // the primary's accumulator holds every device's rows (mfx_accum_reduce
+                                         // since the last trace or clear)
     double* d_reduce_stage = nullptr;    // repeated-device list: a peer's accumulator copied here
     std::vector<hipEvent_t> peer_done;   // repeated-device list: per peer, its trace has finished
     hipEvent_t reduce_done = nullptr;    // repeated-device list: the primary has read every peer's buffer
@@ -690,19 +693,26 @@ void mfx_destroy(mfx_ctx* ctx) { free_ctx(ctx); }
 // (MFX_RAY_QUEUE), whose arrays (6 doubles and 7 words per slot) are allocated only then.
 static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     if (pool <= c->wf_pool && (!queues || c->wf_pool_q)) return MFX_OK;
-    if (c->wf_mem) (void)hipFree(c->wf_mem);
-    c->wf_mem = nullptr;
-    c->wf_pool = 0;
     const size_t P = (size_t)pool;
     const int nv = c->host.max_depth + 1;  // vertices per path
     const size_t per_slot = WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4 - (queues ? 0 : WF_QUEUE_BYTES_PER_SLOT);
     const size_t bytes = P * per_slot + 64 * 256;
     // leave the runtime its headroom (kernel scratch is allocated at launch): a pool that would take
-    // the device's last 512 MiB counts as out of memory, and wf_trace retries with smaller generations
+    // the device's last min(512 MiB, a quarter of what is free) counts as out of memory, and wf_trace
+    // retries with smaller generations. The check runs before the current pool is freed (its bytes
+    // count as free), so a refused growth keeps it: a smaller generation may fit in it.
     size_t mfree = 0, mtotal = 0;
-    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0 && bytes + ((size_t)512 << 20) > mfree)
-        return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB with " +
-                                     std::to_string(mfree >> 20) + " MiB free");
+    if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
+        const size_t avail = mfree + (c->wf_mem ? c->wf_pool_bytes : 0);
+        const size_t headroom = std::min<size_t>((size_t)512 << 20, avail / 4);
+        if (bytes + headroom > avail)
+            return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB with " +
+                                         std::to_string(avail >> 20) + " MiB free");
+    }
+    if (c->wf_mem) (void)hipFree(c->wf_mem);
+    c->wf_mem = nullptr;
+    c->wf_pool = 0;
+    c->wf_pool_bytes = 0;
     hipError_t e = hipMalloc(&c->wf_mem, bytes);
     if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
                                      std::string("wavefront pool: ") + hipGetErrorString(e));
@@ -740,6 +750,7 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
 #endif
     c->wf_pool = pool;
     c->wf_pool_q = queues;
+    c->wf_pool_bytes = bytes;
     return MFX_OK;
 }
 
@@ -816,14 +827,16 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     int64_t gen_max = 0;
     int32_t pool = 0;
     int rc = MFX_OK;
+    // the device short of memory (other contexts or processes on it): smaller generations for this
+    // call only, the same images (a generation only bounds how many paths are in flight); the next
+    // call tries the configured maximum again
+    int64_t cap = c->wf_pool_max;
     while (true) {
-        gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, c->wf_pool_max / 4096 * 4096));
+        gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, cap / 4096 * 4096));
         pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
         rc = wf_ensure_pool(c, pool, qf >= 0);
-        // the device is short of memory (other contexts or processes on it): smaller generations,
-        // the same images (a generation only bounds how many paths are in flight)
-        if (rc != MFX_E_NOMEM || c->wf_pool_max <= (1 << 20)) break;
-        c->wf_pool_max = std::max<int64_t>(1 << 20, gen_max / 2);
+        if (rc != MFX_E_NOMEM || cap <= (1 << 20)) break;
+        cap = std::max<int64_t>(1 << 20, gen_max / 2);
     }
     if (rc) return rc;
     WfParams P = c->wf;
@@ -883,9 +896,9 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
         for (int q = WF_CTR_ITER + 1; q < WF_CTR_ITER + WF_ITER_CTRS; ++q) r[1] += r[q];
         fprintf(stderr, "gen %lld %s %d: cumulative primary %.0f ext %.0f shadow %.0f; extend %.3f ms shadow %.3f ms;"
                 " stamps %.4g %.4g %.4g %.4g outer %.4g node %.4g; cumulative traversal closest %.0f %.0f %.0f"
-                " shadow %.0f %.0f %.0f; scan %.4g shade %.4g\n", (long long)g, what, d,
+                " shadow %.0f %.0f %.0f; scan %.4g shade %.4g lat %.4g\n", (long long)g, what, d,
                 r[0], r[1], r[2], fe, fs, r[10], r[11], r[12], r[13], r[14], r[15], r[4], r[5], r[6], r[7], r[8], r[9],
-                r[16], r[17]);
+                r[16], r[17], r[3]);
         return MFX_OK;
     };
     HIPCHECK(hipEventRecord(own_events ? c->ev0 : e0, c->stream));
@@ -1038,6 +1051,7 @@ int mfx_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
     c->rep_valid = false;  // the stats now describe this trace
+    c->accum_merged = false;
     for (mfx_ctx* d : devs_of(c)) {
         const int rc = dev_trace_accumulate(d, spp, sample_base);
         if (rc) return rc;
@@ -1097,7 +1111,10 @@ static int reduce_planes(mfx_ctx* c, double* (*buf)(mfx_ctx*), double* dst, cons
 int mfx_accum_reduce(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
     if (c->peers.empty() && c->comms.empty()) return MFX_OK;
-    return reduce_planes(c, [](mfx_ctx* d) { return d->d_accum; }, c->d_accum, "mfx_accum_reduce");
+    if (c->accum_merged) return MFX_OK;  // merged since the last trace or clear: a second sum would add the peers twice
+    const int rc = reduce_planes(c, [](mfx_ctx* d) { return d->d_accum; }, c->d_accum, "mfx_accum_reduce");
+    if (rc == MFX_OK) c->accum_merged = true;
+    return rc;
 }
 
 int mfx_trace_timing(mfx_ctx* c, double out[8]) {
@@ -1161,6 +1178,7 @@ int mfx_last_trace_ms(mfx_ctx* c, double* ms) {
 
 int mfx_accum_clear(mfx_ctx* c) {
     if (!c) return fail(MFX_E_STATE, "null context");
+    c->accum_merged = false;
     for (mfx_ctx* d : devs_of(c)) {
         HIPCHECK(hipSetDevice(d->device));
         HIPCHECK(hipMemsetAsync(d->d_accum, 0, 3 * sizeof(double) * (size_t)d->npix, d->stream));
@@ -1183,6 +1201,7 @@ int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
     }
     if (nbytes < 3 * (int64_t)sizeof(double) * c->npix) return fail(MFX_E_INVALID, "attached accumulator too small");
     c->d_accum = (double*)dptr;
+    c->accum_merged = false;
     return MFX_OK;
 }
 
@@ -1237,6 +1256,12 @@ static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, h
 int mfx_accum_read_mean(mfx_ctx* c, double count, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     if (!(count > 0.0)) return fail(MFX_E_INVALID, "mfx_accum_read_mean: count must be > 0");
+    // a device list whose last trace (a render call's included) has not been merged: merge it first,
+    // so the mean covers every device's rows; a merged accumulator is not merged twice
+    if (!c->accum_merged && (!c->peers.empty() || !c->comms.empty())) {
+        const int rc = mfx_accum_reduce(c);
+        if (rc) return rc;
+    }
     HIPCHECK(hipSetDevice(c->device));
     // texture[i,j] <- color / float n (Integrators.fs:171): divided by the count itself
     HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, count, c->d_frame, c->stream));
@@ -1827,6 +1852,19 @@ int mfx_build_info(mfx_ctx* c, double out[8], uint64_t* digest) {
         mix(h.inst.data(), h.inst.size() * sizeof(MfxInstance));
         *digest = x;
     }
+    return MFX_OK;
+}
+
+int mfx_device_info(mfx_ctx* c, int32_t* out, int32_t cap) {
+    if (!c || !out) return fail(MFX_E_INVALID, "null argument");
+    const std::vector<mfx_ctx*> ds = devs_of(c);
+    if (cap < 5 + (int32_t)ds.size()) return fail(MFX_E_INVALID, "mfx_device_info: cap < 5 + devices");
+    out[0] = (int32_t)ds.size();
+    out[1] = (int32_t)c->comms.size();
+    out[2] = !c->comms.empty() ? 1 : (c->peers.empty() ? 0 : 2);
+    out[3] = c->band_index;
+    out[4] = c->band_count;
+    for (size_t g = 0; g < ds.size(); ++g) out[5 + g] = ds[g]->device;
     return MFX_OK;
 }
 

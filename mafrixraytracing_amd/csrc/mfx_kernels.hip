@@ -291,6 +291,11 @@ __global__ void __launch_bounds__(256) anyhit_kernel(QueryParams Q) {
     Q.occ_out[k] = traverse<true, false, INST>(S, o, d, Q.tmin, Q.tmax_per_ray[k], stack, B, st) ? 1 : 0;
 }
 
+#ifndef MFX_EXPERIMENT_PACKET16
+#define MFX_EXPERIMENT_PACKET16 0  // the variant build only (Makefile `experiments`: build_variants/pk16.so)
+#endif
+#if MFX_EXPERIMENT_PACKET16
+// Measured and lost (2.9x slower than one ray per lane), so not in the shipped library:
 // Experiment (VERDICT r04 Next #4a; MFX_ANYHIT_PACKET=16 switches mfx_any_hit to it): the any-hit
 // query traced as four 16-lane sub-packets per wave. A sub-packet walks the BVH4 together: its
 // lanes load the same node (per-lane loads of one address), each tests the four children with its
@@ -407,6 +412,7 @@ __global__ void __launch_bounds__(256) anyhit_packet16_kernel(QueryParams Q, uns
         atomicAdd(steps + 3, (unsigned long long)st.clusters);
     }
 }
+#endif  // MFX_EXPERIMENT_PACKET16
 
 // ----------------------------------------------------------------------------------------------
 // Film + post (FP64, reference order)
@@ -533,11 +539,14 @@ hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st) {
     const size_t lds = (size_t)4 * Q.stack_size * 64 * sizeof(int);
     const dim3 g(grid_for(Q.n, 256));
     if (shadow) {
+#if MFX_EXPERIMENT_PACKET16
         const char* pk = getenv("MFX_ANYHIT_PACKET");  // the sub-packet experiment (flat scenes)
         if (pk && atoi(pk) == 16 && !Q.inst)
             hipLaunchKernelGGL(anyhit_packet16_kernel<false>, g, dim3(256), (size_t)16 * Q.stack_size * 3 * sizeof(int),
                                st, Q, nullptr);
-        else if (Q.inst) hipLaunchKernelGGL(anyhit_kernel<true>, g, dim3(256), lds, st, Q);
+        else
+#endif
+        if (Q.inst) hipLaunchKernelGGL(anyhit_kernel<true>, g, dim3(256), lds, st, Q);
         else hipLaunchKernelGGL(anyhit_kernel<false>, g, dim3(256), lds, st, Q);
     } else {
         if (Q.inst) hipLaunchKernelGGL(closest_kernel<true>, g, dim3(256), lds, st, Q);

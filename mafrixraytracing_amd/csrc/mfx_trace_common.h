@@ -775,11 +775,22 @@ __device__ __forceinline__ void slab4(const float4& lx, const float4& hx, const 
     }
 }
 
+// Diagnostic builds (-DMFX_DIAG_STAMPS, scripts/latency_roof.py): `lat` != null accumulates the wave's
+// cycles from the node loads' issue to their first use (the slab tests), the step's round trip.
+__device__ __forceinline__ uint64_t diag_clock() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
 template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
-                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0}) {
+                                         const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0},
+                                         uint64_t* lat = nullptr) {
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
+    const uint64_t t_issue = lat ? diag_clock() : 0;
     // Lanes at a top-level node read LDS, the others global memory. In a wave with both, the two
     // reads land in the same registers, so the LDS reads wait for the global loads (measured
     // alternatives: LDS only when the whole wave is at top nodes, -0.5 to -2 %; both reads by every
@@ -802,6 +813,7 @@ __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int 
     int nh = 0;
     Slab4 SL;
     slab4(lx, hx, ly, hy, lz, hz, r, SL);
+    if (lat) *lat += diag_clock() - t_issue;
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];

@@ -54,7 +54,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow
 #endif
 struct DiagAcc {
-    uint64_t fetch, node, leaf, fin, last, scan, shade;
+    uint64_t fetch, node, leaf, fin, last, scan, shade, lat;  // lat: node loads' issue-to-use cycles (node_step)
     uint32_t outer, node_iters, windows;
 };
 __device__ __forceinline__ uint64_t stamp() {
@@ -228,8 +228,8 @@ __device__ __forceinline__ void trav_begin(Trav& T, const SceneView& S, DV o, DV
 // one node step of the per-lane traversal (BVH4; shadow rays far-first)
 template <bool SHADOW, typename ST>
 __device__ __forceinline__ int trav_node_step(const SceneView& S, int node, const RayF& rf, float tlim, const ST& stack,
-                                              int& sp, TopNodes tn) {
-    return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn);
+                                              int& sp, TopNodes tn, uint64_t* lat) {
+    return node_step<true, SHADOW && MFX_SHADOW_ORDER == 1>(S.nodes, node, rf, tlim, stack, sp, tn, lat);
 }
 
 // Internal nodes until this lane reaches a leaf (while-while), then that one reference leaf in
@@ -253,7 +253,7 @@ __device__ __forceinline__ bool trav_step(Trav& T, const SceneView& S, const ST&
         if (STATS && !SHADOW && T.B.found) st.after_nodes++;
 #endif
         if (diag && lane_id() == __builtin_amdgcn_readfirstlane(lane_id())) dg.node_iters++;  // once per wave iteration
-        T.node = trav_node_step<SHADOW>(S, T.node, rf, tlim, stack, T.sp, tn);
+        T.node = trav_node_step<SHADOW>(S, T.node, rf, tlim, stack, T.sp, tn, diag ? &dg.lat : nullptr);
         if (INST) T.node = inst_frame(S, T.node, T.inst, T.inst_sp, T.sp, T.o, T.d, rf);
         // leave the node loop once few lanes still step: the rest resume next round, after the
         // leaf tests and a refill of the idle lanes
@@ -621,6 +621,7 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
         atomicAdd(cnt + 12, (unsigned long long)dg.leaf);
         atomicAdd(cnt + 13, (unsigned long long)dg.fin);
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
+        atomicAdd(cnt + 3, (unsigned long long)dg.lat);  // (counter 3: unused by the shipped kernels)
     }
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
@@ -1033,6 +1034,7 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
         atomicAdd(cnt + 14, (unsigned long long)dg.outer);
         atomicAdd(cnt + 16, (unsigned long long)dg.scan);
         atomicAdd(cnt + 17, (unsigned long long)dg.shade);
+        atomicAdd(cnt + 3, (unsigned long long)dg.lat);
     }
     if (STATS) {
         block_add<4>(cnt + 7, st.nodes, red);

@@ -185,6 +185,16 @@ class NativeContext:
                 "nodes4": int(out[4]), "slots": int(out[5]), "nodes2": int(out[6]), "levels": int(out[7]),
                 "digest": dig.value}
 
+    def device_info(self) -> dict:
+        """How the context's work lies over devices (mfx_device_info): the HIP ordinals, the RCCL
+        communicators it created, how mfx_accum_reduce merges, and the primary's tile-row band."""
+        out = np.zeros(5 + len(self.devices), dtype=np.int32)
+        check(self.lib.mfx_device_info(self._h, iptr(out), len(out)), "mfx_device_info")
+        g = int(out[0])
+        return {"devices": [int(d) for d in out[5:5 + g]], "communicators": int(out[1]),
+                "merge": {0: "none", 1: "rccl_reduce", 2: "ordered_adds"}[int(out[2])],
+                "band_index": int(out[3]), "band_count": int(out[4])}
+
     def instancing_info(self) -> dict:
         """How instances are traced (mfx_instancing_info): two-level shape and image bytes."""
         out = np.zeros(8)

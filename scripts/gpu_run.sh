@@ -20,6 +20,10 @@
 #                        WRITE_SIZE passes, scripts/per_dispatch.py) -> dispatch_CFG.txt
 #   diagab:SCENE:SPP     per-iteration stage times of every build_variants/*.so (with its .env), 2 rounds
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
+#   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
+#                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
+#   latroof:SCENE:SPP    latency roof of k_extend / k_shadow from the stamp builds build_variants/st1.so,
+#                        st2.so (scripts/latency_roof.py) -> latency_SCENE.json
 set -e
 # the hardware queues bench.py would relaunch itself with (so rocprofv3 sees one process)
 export GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES:-8}
@@ -110,6 +114,18 @@ for step in "$@"; do
       cat $O/diagab_summary.txt ;;
     iterstats)
       timeout -k 10 300 python3 scripts/iter_stats.py scenes/$a1 $a2 | tee $O/iterstats_$a1.txt ;;
+    sharetrace)
+      D=$R/$O/sharetrace_${a1}_$(echo $a2 | tr , _)
+      mkdir -p $D
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $D/trace -o run -- \
+         python3 $R/scripts/share_trace.py --parts $a1 --nif $a2 --steps 20 > $D/run.json 2> $D/run.err)
+      cat $D/run.json
+      python3 scripts/share_timeline.py $D/trace | tee $D/timeline.txt ;;
+    latroof)
+      timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a1 --spp ${a2:-64} \
+        --out $O/latency_$(basename $a1 .xml).json > $O/latroof.log 2>&1
+      tail -5 $O/latroof.log ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -74,7 +74,11 @@ def main():
     ap.add_argument("--scene", default=os.path.join(ROOT, "scenes", "spot.xml"))
     ap.add_argument("--spp", type=int, default=4)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--lib", default=os.path.join(ROOT, "build_variants", "pk16.so"),
+                    help="the experiment build that carries anyhit_packet16_kernel (Makefile `experiments`)")
     a = ap.parse_args()
+    import mafrixraytracing_amd.abi as abi
+    abi._lib = abi.load_library(a.lib)
     from mafrixraytracing_amd.native import DEFAULT_SEED, NativeContext
     from mafrixraytracing_amd.scene_io import load_scene_file
     arr = load_scene_file(a.scene)

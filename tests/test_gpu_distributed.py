@@ -211,6 +211,9 @@ def test_bench_multiprocess_path_under_torchrun(gpu, tmp_path):
     plain = json.loads(r1.stdout.strip().splitlines()[-1])
     assert line["metric"] == plain["metric"] and line["n_gpus"] == 1
     assert "process group" in line["config"]["parallelism"]
+    # the forced multi-process path checks its merged frame too (world 1 over RCCL)
+    assert line["merged_equals_1gpu"] is True and line["verify"]["exact_expected"] is True
+    assert line["topology"]["rccl_world"] == 1 and line["topology"]["backend"] == "nccl"
     # rays per step are a property of the sample set: equal whichever path traced it
     assert line["rays_per_step"] == plain["rays_per_step"] > 0
 
@@ -241,12 +244,30 @@ def test_bench_two_ranks_rehearsal_under_torchrun(gpu):
     assert "image partition" in line["config"]["parallelism"]
     one = _bench(["--spp", "2"] + common)
     assert line["rays_per_step"] == one["rays_per_step"] > 0
+    # the line proves its own merge: the 2-rank frame is the 1-GPU frame bit for bit
+    assert line["merged_equals_1gpu"] is True and line["verify"]["max_abs_diff"] == 0.0
+    assert line["verify"]["digest_merged"] == line["verify"]["digest_1gpu"]
+    topo = line["topology"]
+    assert topo["rccl_world"] == 2 and topo["backend"] == "gloo" and topo["rank_devices"] == [0, 0]
+    assert topo["pinned_one_device"] is True
     wk = line["weak"]
     assert wk["scaling"] == "weak" and wk["global_spp_per_step"] == 4
-    # (the sub-object continues the sample sequence after the line's steps: other samples of the same
-    # 4-spp-per-step job, so its rays per step agree with a 1-rank run's to sampling noise)
-    four = _bench(["--spp", "4"] + common)
-    assert abs(wk["rays_per_step"] / four["rays_per_step"] - 1) < 2e-3 and wk["value"] > 0
+    # the sub-object continues the sample sequence after the line's steps: a 1-rank run of the same
+    # 4-spp-per-step job over the same samples (its first timed step at the same global sample) has
+    # exactly its rays
+    first = wk["first_timed_sample"]
+    four = _bench(["--spp", "4", "--sample-base", str(first - 4 * 1)] + common)  # warmup 1 step of 4 spp
+    assert wk["rays_per_step"] == four["rays_per_step"] > 0 and wk["value"] > 0
+
+
+def test_bench_merge_check_catches_a_wrong_partition(gpu):
+    """The merged-frame check is not vacuous: with rank 1 tracing rank 0's rows instead of its own
+    (MFX_BENCH_FAULT=partition), the 2-rank line reports merged_equals_1gpu false."""
+    common = ["--steps", "1", "--warmup", "1", "--spp", "2", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    env = dict(os.environ, MFX_BENCH_DEVICE="0", MFX_BENCH_BACKEND="gloo", MFX_BENCH_FAULT="partition")
+    line = _bench(common, env=env, torchrun=2)
+    assert line["merged_equals_1gpu"] is False and line["verify"]["max_abs_diff"] > 0
+    assert line["verify"]["digest_merged"] != line["verify"]["digest_1gpu"]
 
 
 def test_bench_single_process_device_list_rehearsal(gpu):
@@ -259,6 +280,11 @@ def test_bench_single_process_device_list_rehearsal(gpu):
     line = _bench(["--spp", "4", "--single-process", "--gpus", "2"] + common, env=env)
     one = _bench(["--spp", "4"] + common)
     assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["rays_per_step"] == one["rays_per_step"]
+    assert line["merged_equals_1gpu"] is True
+    topo = line["topology"]
+    # a repeated device cannot form a communicator: the library merges by device-ordered adds
+    assert topo["single_process_devices"] == [0, 0] and topo["communicators"] == 0
+    assert topo["library_context"]["merge"] == "ordered_adds"
     ra = ["--spp", "8", "--api", "render", "--render-ahead", "4"]
     rl = _bench(ra + ["--single-process", "--gpus", "2"] + common, env=env)
     r1 = _bench(ra + common)

@@ -141,10 +141,19 @@ def test_pool_shrinks_when_the_device_is_short_of_memory(gpu):
             ctx.trace_accumulate(64, 0)
             got = ctx.accum_read_mean(1.0)
             counts = ctx.ray_counts()[:3]
+            gens_short = ctx.trace_timing()["generations"]
         finally:
             del hog
             torch.cuda.empty_cache()
+        # the shrink holds for that call only: with the memory back, the next trace of the same context
+        # runs the frame as one generation again
+        ctx.accum_clear()
+        ctx.trace_accumulate(64, 0)
+        again = ctx.accum_read_mean(1.0)
+        gens_after = ctx.trace_timing()["generations"]
     finally:
         ctx.close()
     assert np.array_equal(got, want)
     assert np.array_equal(counts, want_counts)
+    assert gens_short > 1 and gens_after == 1
+    assert np.array_equal(again, want)

@@ -201,3 +201,22 @@ def test_ray_counts_total_sums_back_to_back_traces(gpu, devices):
         got = c.ray_counts_total(reset=True)
         assert np.array_equal(got[:3], want[:3]) and got[3] == got[0]
         assert not np.any(c.ray_counts_total(reset=False)[:3])
+
+
+@pytest.mark.parametrize("devices", [[0], [0, 0], [0, 0, 0]])
+def test_accum_read_mean_after_render_merges_the_device_list(gpu, devices):
+    """ADVICE r05: a render call on a device list leaves each device's rows in its own accumulator;
+    mfx_accum_read_mean merges them before reading (and only once: a second read, or a read after an
+    explicit mfx_accum_reduce, is the same), so it equals the one-device context's accumulator."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("cube_cornell", 48, 27)
+    with NativeContext(a, seed=SEED) as s:
+        s.render_rgba8(3)
+        want = s.accum_read_mean(3.0)
+    with NativeContext(a, seed=SEED, devices=devices) as m:
+        m.render_rgba8(3)
+        got = m.accum_read_mean(3.0)
+        again = m.accum_read_mean(3.0)
+        m.accum_reduce()
+        third = m.accum_read_mean(3.0)
+    assert np.array_equal(got, want) and np.array_equal(again, want) and np.array_equal(third, want)
