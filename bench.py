@@ -265,7 +265,7 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
                         "to pageable host memory, synchronize"}
 
 
-def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
+def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repeats=3):
     """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
     measured on this GPU: rank r traces all `spp` samples of the film's tile rows r mod N
     (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
@@ -274,7 +274,10 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
     (torch index kernels on this accumulator); the transfer is modeled as the largest sending rank's
     bytes over one xGMI link (every rank sends to rank 0 over its own link, in parallel).
     predicted_efficiency = (t_1GPU / N) / (t_slowest_rank + t_pack + t_transfer + t_unpack): the
-    exchange not overlapped (the bench overlaps it with the next frame's trace; not counted here)."""
+    exchange not overlapped (the bench overlaps it with the next frame's trace; not counted here).
+    Each rank's share is timed `repeats` times (its contexts kept, the steps run again) and its median
+    taken (one run's 1/8 share varied by 7 % between runs); `spread` = (max - min) / median
+    of the slowest rank's repeats, and the predictions from each repeat's slowest rank beside them."""
     import torch
     from mafrixraytracing_amd.abi import MFX_F_IN_FLIGHT, MFX_F_ROW_PARTITION
     from mafrixraytracing_amd.distributed import RowGather, frames_in_flight
@@ -316,7 +319,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
 
     out = {}
     for n in (2, 4, 8):
-        rank_ms, rank_rays = [], []
+        rank_ms, rank_rays, rank_reps = [], [], []
         ov = None
         nif = frames_in_flight(W, H, spp, n)  # the bench's rank alternates its frames over nif contexts
         for r in range(n):
@@ -327,19 +330,22 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
             for c in cs:
                 c.sync()
                 c.ray_counts_total(reset=True)
-            t0 = time.perf_counter()
-            for k in range(steps):  # back to back, as the bench's steps run
-                c = cs[k % nif]
-                c.accum_clear()
-                c.trace_accumulate(spp, (k + 1) * spp)
-            for c in cs:
-                c.sync()
-            rank_ms.append((time.perf_counter() - t0) / steps * 1e3)
-            rays = 0.0
-            for c in cs:
-                t = c.ray_counts_total(reset=True)
-                rays += t[0] + t[1] + t[2]
-            rank_rays.append(rays / steps)
+            reps, rays = [], 0.0
+            for rp in range(repeats):
+                t0 = time.perf_counter()
+                for k in range(steps):  # back to back, as the bench's steps run
+                    c = cs[k % nif]
+                    c.accum_clear()
+                    c.trace_accumulate(spp, (rp * steps + k + 1) * spp)
+                for c in cs:
+                    c.sync()
+                reps.append((time.perf_counter() - t0) / steps * 1e3)
+                for c in cs:
+                    t = c.ray_counts_total(reset=True)
+                    rays += t[0] + t[1] + t[2]
+            rank_reps.append(reps)
+            rank_ms.append(sorted(reps)[len(reps) // 2])
+            rank_rays.append(rays / steps / repeats)
             if r == 0:
                 ov = overlap(cs[0], RowGather(acc, W, H, 0, n))
             for c in cs:
@@ -351,9 +357,14 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0):
         t_rank = max(rank_ms)
         t_ex = t_pack + t_xfer + t_unpack
         job_rays = sum(rank_rays)
+        slow = rank_reps[rank_ms.index(t_rank)]
+        per_rep_slowest = [max(r[i] for r in rank_reps) for i in range(repeats)]
         out[str(n)] = {"film_share_per_gpu": round(1.0 / n, 6), "spp_per_gpu": spp, "frames_in_flight": nif,
                        "rank_ms_per_step": [round(t, 3) for t in rank_ms],
-                       "slowest_rank_ms": round(t_rank, 3),
+                       "slowest_rank_ms": round(t_rank, 3), "repeats": repeats,
+                       "slowest_rank_repeats_ms": [round(t, 3) for t in slow],
+                       "spread": round((max(slow) - min(slow)) / t_rank, 4),
+                       "predicted_efficiency_per_repeat": [round((ms_1gpu / n) / (t + t_ex), 4) for t in per_rep_slowest],
                        "imbalance": round(t_rank / (sum(rank_ms) / n), 4),
                        "mrays_per_s_per_gpu": round(job_rays / n / (t_rank / 1e3) / 1e6, 2),
                        "vs_full_step_rate": round(job_rays / n / (t_rank / 1e3) / 1e6 / value_1gpu, 4),
@@ -801,6 +812,34 @@ def main():
                         "peak_case": tdroof["peak"]["case"],
                         "source": os.path.relpath(tdfile, ROOT) + " (scripts/pmc_td_roof.sh)"}
 
+            latf = os.path.join(ROOT, "profiles", f"latency_{sname}.json")  # scripts/latency_roof.py
+            lat = None
+            if os.path.exists(latf) and ngpu == 1 and args.api == "batch" and not CONFIG_FLAGS.get(args.config):
+                with open(latf) as f:
+                    lat = json.load(f)
+                if lat.get("spp", args.spp) != args.spp:
+                    lat = None
+
+            def latency_roofline(kname, kms, launches):
+                """The per-lane kernels' latency roof (VERDICT r05 Next #3): the node steps per launch and
+                the loaded round trip of a node step (L_step, s_memtime around the node loads) from the
+                stamp builds' pass; achieved = node steps per resident wave per second over this run's
+                HIP-event launch time, peak = clock / L_step (every wave waiting one round trip per
+                step): frac = the share of the launch its node chain's round trips explain."""
+                if not lat or kname.split("<")[0] not in lat["kernels"]:
+                    return None
+                kv = lat["kernels"][kname.split("<")[0]]
+                waves = kv["waves_per_simd"] * 1024  # 256 CUs x 4 SIMDs
+                ach = kv["node_steps_per_launch"] / waves / (kms / launches / 1e3) / 1e6
+                return {"bound": "latency", "achieved": round(ach, 4), "peak": kv["peak"], "unit": kv["unit"],
+                        "frac": round(ach / kv["peak"], 4), "frac_profile_run": kv["frac"],
+                        "L_step_cycles": kv["L_step_cycles"], "L_idle_cycles": kv["L_idle_cycles"],
+                        "loaded_over_idle": kv["loaded_over_idle"], "clock_mhz": kv["clock_mhz"],
+                        "waves_per_simd": kv["waves_per_simd"], "node_steps_per_wave_launch":
+                            round(kv["node_steps_per_launch"] / waves, 1),
+                        "lat_share_stamp_build": kv["lat_share_stamp_build"],
+                        "source": os.path.relpath(latf, ROOT) + " (scripts/latency_roof.py)"}
+
             def smem_roofline(kname, kms, launches):
                 """k_camera's roof: scalar-memory instructions (SQ_INSTS_SMEM, the PMC pass of
                 scripts/pmc_td_roof.sh) per launch over this run's HIP-event launch time, against
@@ -837,6 +876,7 @@ def main():
                                         "correction measured for wide streaming reads) is applied to these gathers "
                                         "too, and MALL hits count as fabric traffic" if traffic else None,
                         "td": td_roofline(kname, kms, launches),
+                        "latency": latency_roofline(kname, kms, launches),
                         "kernel": kname, "launches_per_step": launches,
                         "avg_launch_ms": round(kms / launches, 4),
                         "bytes_per_ray": round(bray, 1), "bytes_per_ray_source":
@@ -872,6 +912,7 @@ def main():
                     kc["bytes_per_ray_source"] = ("packet fetch counters (mfx_ray_counts out[10], out[11], "
                                                   "MFX_F_COUNT_STATS pass)" if pkc else kc["bytes_per_ray_source"])
                     kc["td"] = None  # its nodes and slots do not pass the TD: the scalar-load roof is kc["smem"]
+                    kc["latency"] = None  # (a packet walk: one wave-uniform chain, VALU-bound; the smem roof)
                     kc["smem"] = smem_roofline("k_camera", stage_ms["camera_ms"], cl)
                     kc["note"] = ("HBM index priced at the bytes the packets fetch (each node and slot once per wave, "
                                   "through the scalar cache); its binding roof is the scalar-load rate (smem)")
@@ -904,6 +945,10 @@ def main():
                     "note": "32 B per node or leaf-cluster visit + 36 B per primitive test + 64 B per ray (SURVEY.md "
                             "§8d) on this run's MFX_F_COUNT_STATS counters (the kernels' BVH4 visits), not the "
                             "frozen BVH2 fixture"}
+            roofline["note"] = ("the hbm entry is a speed index: SURVEY §8(d)'s algorithmic bytes of a frozen BVH2 walk "
+                                "(profiles/bray_fixture.json) over the HIP-event launch time, kept comparable across rounds; "
+                                "the bytes the kernels move are `traffic` (PMC) and live_bytes_per_ray; the roof that binds "
+                                "the per-lane kernels is `latency` (their node chain's round trips; DESIGN.md §7)")
             roofline["stage_ms"] = {k: round(v, 3) for k, v in stage_ms.items()}
             roofline["counters"] = {g: ({k: round(v, 3) for k, v in d.items()} if isinstance(d, dict)
                                         else round(d, 4)) for g, d in stats.items()}

@@ -103,7 +103,7 @@ struct FrameMode {
     double count0;    // frameCount before the first sample
 };
 
-constexpr int kStageChunks = 4;  // host_readback's pipelined pieces
+constexpr int kStageChunks = 8;  // host_readback's pipelined pieces (at most)
 
 struct mfx_ctx {
     int device = 0;
@@ -212,6 +212,7 @@ struct mfx_ctx {
     double rep_counts[16] = {0};
     double rep_ms = 0.0;
     bool diag_iter = false;
+    bool iter_events = true;  // per-iteration HIP events around each launch (mfx_trace_timing's stage split)
 
     // ---- multi-device (primary context only) ----
     int api_part_count = 1;              // the caller's partition count (mfx_options.part_count)
@@ -355,6 +356,7 @@ static int ctx_setup(mfx_ctx* c) {
     // (at most 2^28 slots: k_extend's pending entries keep a slot index in 28 bits)
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, std::min<int64_t>(1 << 28, atoll(pm)));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
+    if (const char* e = getenv("MFX_ITER_EVENTS")) c->iter_events = atoi(e) != 0 || c->diag_iter;
     if (const char* qf = getenv("MFX_QUEUE_FROM")) c->wf_queue_from = MFX_RAY_QUEUE ? std::max(-2, atoi(qf)) : -1;
     if (const char* qc = getenv("MFX_QCHUNK")) c->wf_qchunk = std::max(64, std::min(WF_CHUNK_MAX, atoi(qc) / 64 * 64));
     if (const char* rq = getenv("MFX_RAY_QUEUE")) {
@@ -844,6 +846,8 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     P.ctl = c->d_wfctl - WF_CTL_Q0;
     P.counters = counters ? counters : c->d_counters;
     const bool own_events = e0 == nullptr;
+    // per-iteration stage events (mfx_trace_timing's split): off with MFX_ITER_EVENTS=0 (A/B of their cost)
+    const bool iter_events = own_events && c->iter_events;
     P.seed = c->seed;
     P.sample_base = sample_base;
     P.part_index = c->part_index;
@@ -880,7 +884,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     const int64_t ngen = (total + gen_max - 1) / gen_max;
     const int per_gen = P.max_depth + 1;  // bounce-synchronous iterations per generation
     const int iters = (int)ngen * per_gen;
-    while (own_events && (int)c->it_ev.size() < 3 * iters) {
+    while (iter_events && (int)c->it_ev.size() < 3 * iters) {
         hipEvent_t e;
         HIPCHECK(hipEventCreate(&e));
         c->it_ev.push_back(e);
@@ -920,7 +924,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
             // first vertex's last chunks are its launch's tail (r04u: C2 at 8 spp +2.4 %; at 64 spp
             // the same halving costs 1.5 %, so frames of more than 2^25 paths keep whole chunks)
             P.chunk_shd = (c->wf_shd_half && !P.qcount && total <= ((int64_t)1 << 25)) ? std::max(64, P.chunk / 2) : P.chunk;
-            if (!own_events) {
+            if (!iter_events) {
                 HIPCHECK(mfx_wf_iteration(P, c->wf_ext_grid, c->wf_shd_grid, stats, c->stream, nullptr));
                 continue;
             }
@@ -950,7 +954,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     // the context's first wavefront trace (settle_queue_auto, once every device has been
     // enqueued), so a caller that never polls the counters gets the same kernels as one that does
     if (c->wf_queue_from == -2 && !c->wf_auto_read) c->wf_auto_pending = true;
-    c->it_recorded = iters;
+    c->it_recorded = iter_events ? iters : 0;
     c->it_per_gen = per_gen;
     c->generations = (int)ngen;
     return MFX_OK;
@@ -1207,8 +1211,11 @@ int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
 
 // Device -> caller's (pageable) host memory, stream-ordered, complete on return. A pageable
 // destination is slow for large copies (mfx_sample's 66 MB FP64 frame at 1080p: ~10 ms, r03b), so a
-// large readback goes to a page-locked staging buffer by DMA and from there to the caller's buffer
-// by host threads; a small one (or with no staging memory) is a plain copy.
+// large readback goes to a page-locked staging buffer by DMA, in pieces, and from there to the
+// caller's buffer by host threads, each copying its slice of every piece as soon as that piece has
+// landed: the copy trails the DMA by one piece. r06a (readback_probe.py): the DMA alone moves 66 MB
+// in 1.17 ms, one thread copies it on in 2.07 ms; 4 pieces copied by threads spawned per piece took
+// 2.56 ms with the mean kernel. A small readback (or with no staging memory) is a plain copy.
 static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
     const size_t kLarge = 16u << 20;
     if (bytes >= kLarge && bytes > c->h_stage_bytes) {
@@ -1223,33 +1230,41 @@ static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, h
         HIPCHECK(hipStreamSynchronize(st));
         return MFX_OK;
     }
-    // in kStageChunks pieces: the host threads copy piece i while the DMA engine brings piece i + 1
-    for (hipEvent_t& e : c->stage_ev)
-        if (!e) HIPCHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    const size_t piece = (bytes / kStageChunks + 4095) & ~(size_t)4095;
-    for (int i = 0; i < kStageChunks; ++i) {
+    int npiece = kStageChunks, nt = 8;  // MFX_READBACK_PIECES / MFX_READBACK_THREADS: A/B knobs
+    if (const char* e = getenv("MFX_READBACK_PIECES")) npiece = std::max(1, std::min(kStageChunks, atoi(e)));
+    if (const char* e = getenv("MFX_READBACK_THREADS")) nt = std::max(1, std::min(32, atoi(e)));
+    for (int i = 0; i < npiece; ++i)
+        if (!c->stage_ev[i]) HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+    const size_t piece = (bytes / npiece + 4095) & ~(size_t)4095;
+    int used = 0;
+    for (int i = 0; i < npiece; ++i) {
         const size_t off = piece * i;
         if (off >= bytes) break;
         HIPCHECK(hipMemcpyAsync(c->h_stage + off, (const uint8_t*)src + off, std::min(piece, bytes - off),
                                 hipMemcpyDeviceToHost, st));
         HIPCHECK(hipEventRecord(c->stage_ev[i], st));
+        used = i + 1;
     }
-    const int nt = 4;
-    for (int i = 0; i < kStageChunks; ++i) {
-        const size_t off0 = piece * i;
-        if (off0 >= bytes) break;
-        HIPCHECK(hipEventSynchronize(c->stage_ev[i]));
-        const size_t len = std::min(piece, bytes - off0);
-        const size_t part = (len / nt + 4095) & ~(size_t)4095;
-        std::vector<std::thread> th;
-        for (int t = 1; t < nt; ++t) {
+    // thread t copies slice t of every piece, in piece order, once the piece's DMA has finished
+    auto work = [&](int t) -> hipError_t {
+        for (int i = 0; i < used; ++i) {
+            const hipError_t e = hipEventSynchronize(c->stage_ev[i]);
+            if (e != hipSuccess) return e;
+            const size_t off0 = piece * i, len = std::min(piece, bytes - off0);
+            const size_t part = (len / nt + 4095) & ~(size_t)4095;
+            if (part * t >= len) continue;
             const size_t off = off0 + part * t;
-            if (part * t >= len) break;
-            th.emplace_back([=] { std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, len - part * t)); });
+            std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, len - part * t));
         }
-        std::memcpy((uint8_t*)dst + off0, c->h_stage + off0, std::min(part, len));
-        for (auto& t : th) t.join();
-    }
+        return hipSuccess;
+    };
+    std::vector<hipError_t> err(nt, hipSuccess);
+    std::vector<std::thread> th;
+    for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { err[t] = work(t); });
+    err[0] = work(0);
+    for (auto& t : th) t.join();
+    for (hipError_t e : err)
+        if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("host_readback: ") + hipGetErrorString(e));
     return MFX_OK;
 }
 

@@ -22,6 +22,7 @@
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
 #   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
 #                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
+#   py:SCRIPT[:ARGS]     scripts/SCRIPT.py ARGS (comma-separated) -> SCRIPT.json
 #   latroof:SCENE:SPP    latency roof of k_extend / k_shadow from the stamp builds build_variants/st1.so,
 #                        st2.so (scripts/latency_roof.py) -> latency_SCENE.json
 set -e
@@ -126,6 +127,11 @@ for step in "$@"; do
       timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a1 --spp ${a2:-64} \
         --out $O/latency_$(basename $a1 .xml).json > $O/latroof.log 2>&1
       tail -5 $O/latroof.log ;;
+    py)
+      # py:SCRIPT[:ARGS] -- scripts/SCRIPT.py with comma-separated ARGS -> SCRIPT.json / SCRIPT.err
+      X=(); [ -n "$a2" ] && IFS=, read -ra X <<< "$a2"
+      timeout -k 10 300 python3 scripts/$a1.py "${X[@]}" > $O/$a1.json 2> $O/$a1.err
+      tail -3 $O/$a1.json ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
