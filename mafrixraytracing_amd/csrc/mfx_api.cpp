@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <functional>
 #include <cstdlib>
 #include <cstring>
 #include <string>
@@ -104,6 +105,15 @@ struct FrameMode {
 };
 
 constexpr int kStageChunks = 8;  // host_readback's pipelined pieces (at most)
+
+// mfx_sample's banded resolve (one device): the last generation's k_resolve runs in nbands column bands
+// of tiles, and after each band `after(k, tx0, ntx)` enqueues that band's mean and readback, so the
+// frame's copy to the host overlaps the rest of the resolve. used: wf_trace ran it (not the megakernel).
+struct ResolveSplit {
+    int nbands = 0;
+    std::function<int(int, int, int)> after;
+    bool used = false;
+};
 
 struct mfx_ctx {
     int device = 0;
@@ -207,6 +217,7 @@ struct mfx_ctx {
     unsigned long long* h_counters = nullptr;  // page-locked [WF_SHARDS][WF_NCTR]: a batch's ray counters
     uint8_t* h_stage = nullptr;         // page-locked staging of large readbacks (host_readback)
     hipEvent_t stage_ev[kStageChunks] = {};  // host_readback: piece i is in h_stage
+    hipEvent_t band_ev[kStageChunks] = {};   // mfx_sample's banded readback: band i's mean is computed
     size_t h_stage_bytes = 0;
     bool rep_valid = false;          // the last call was served from held frames: its stats are rep_*
     double rep_counts[16] = {0};
@@ -279,6 +290,8 @@ static void free_ctx(mfx_ctx* c) {
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->stage_ev)
+        if (e) (void)hipEventDestroy(e);
+    for (hipEvent_t e : c->band_ev)
         if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : c->it_ev)
         if (e) (void)hipEventDestroy(e);
@@ -817,8 +830,10 @@ static void note_live(mfx_ctx* c, const unsigned long long* h);
 // (k_resolve's frames mode), the ray counters go to `counters` and the trace is bracketed by the
 // events e0 / e1 instead of the context's (no per-iteration events), so a batch traced in the
 // background leaves the last call's timing records alone.
+// split != null (mfx_sample, one device): the last generation's resolve in column bands (ResolveSplit).
 static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode* fm = nullptr,
-                    unsigned long long* counters = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr) {
+                    unsigned long long* counters = nullptr, hipEvent_t e0 = nullptr, hipEvent_t e1 = nullptr,
+                    ResolveSplit* split = nullptr) {
     const int W = c->host.width, H = c->host.height;
     const int brows = band_rows(c);
     const int64_t per_sample = (int64_t)((W + 7) / 8) * brows * 64;  // the device's band of the film
@@ -942,7 +957,23 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
             }
         }
         wf_queue_views(c, P, -1);  // k_resolve reads the pool's final state and depth words
-        HIPCHECK(mfx_wf_resolve(P, c->stream));
+        if (split && g == ngen - 1) {
+            // a pixel's sum is its own thread's whatever the launch: the same bits as one launch
+            const int tiles_x = (W + 7) / 8;
+            for (int k = 0; k < split->nbands; ++k) {
+                const int tx0 = (int)((int64_t)k * tiles_x / split->nbands);
+                const int tx1 = (int)((int64_t)(k + 1) * tiles_x / split->nbands);
+                P.res_tx0 = tx0;
+                P.res_ntx = tx1 - tx0;
+                if (P.res_ntx > 0) HIPCHECK(mfx_wf_resolve(P, c->stream));
+                const int rc = split->after(k, tx0, tx1 - tx0);
+                if (rc) return rc;
+            }
+            P.res_tx0 = P.res_ntx = 0;
+            split->used = true;
+        } else {
+            HIPCHECK(mfx_wf_resolve(P, c->stream));
+        }
     }
     if (!own_events) {
         HIPCHECK(hipEventRecord(e1, c->stream));
@@ -961,7 +992,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
 }
 
 // one device's share of mfx_trace_accumulate (its sample partition), enqueued on its stream
-static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
+static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base, ResolveSplit* split = nullptr) {
     HIPCHECK(hipSetDevice(c->device));
     int64_t ns = spp > c->part_index ? (spp - c->part_index + c->part_count - 1) / c->part_count : 0;
     if (band_rows(c) == 0) ns = 0;  // a film too small to give this device a tile row
@@ -981,7 +1012,7 @@ static int dev_trace_accumulate(mfx_ctx* c, int32_t spp, int64_t sample_base) {
         return MFX_OK;
     }
     if (!c->mega_last) {
-        const int rc = wf_trace(c, ns, sample_base);
+        const int rc = wf_trace(c, ns, sample_base, nullptr, nullptr, nullptr, nullptr, split);
         if (rc) return rc;
         HIPCHECK(mfx_launch_counters_add(c->d_counters_total, c->d_counters, WF_NCTR * WF_SHARDS, c->stream));
         return MFX_OK;
@@ -1209,52 +1240,39 @@ int mfx_accum_attach(mfx_ctx* c, void* dptr, int64_t nbytes) {
     return MFX_OK;
 }
 
-// Device -> caller's (pageable) host memory, stream-ordered, complete on return. A pageable
-// destination is slow for large copies (mfx_sample's 66 MB FP64 frame at 1080p: ~10 ms, r03b), so a
-// large readback goes to a page-locked staging buffer by DMA, in pieces, and from there to the
-// caller's buffer by host threads, each copying its slice of every piece as soon as that piece has
-// landed: the copy trails the DMA by one piece. r06a (readback_probe.py): the DMA alone moves 66 MB
-// in 1.17 ms, one thread copies it on in 2.07 ms; 4 pieces copied by threads spawned per piece took
-// 2.56 ms with the mean kernel. A small readback (or with no staging memory) is a plain copy.
-static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
-    const size_t kLarge = 16u << 20;
-    if (bytes >= kLarge && bytes > c->h_stage_bytes) {
+// Device -> caller's (pageable) host memory. A pageable destination is slow for large copies
+// (mfx_sample's 66 MB FP64 frame at 1080p: ~10 ms, r03b), so a large readback goes to a page-locked
+// staging buffer by DMA, in pieces, and from there to the caller's buffer by host threads, each
+// copying its slice of every piece as soon as that piece has landed: the copy trails the DMA by one
+// piece. r06a (scripts/readback_probe.py): the DMA alone moves 66 MB in 1.17 ms, one thread copies
+// it on in 2.07 ms; 4 pieces copied by threads spawned per piece took 2.56 ms with the mean kernel.
+
+// the page-locked staging buffer, at least `bytes` (false: none could be allocated)
+static bool ensure_stage(mfx_ctx* c, size_t bytes) {
+    if (bytes > c->h_stage_bytes) {
         if (c->h_stage) (void)hipHostFree(c->h_stage);
         c->h_stage = nullptr;
         c->h_stage_bytes = 0;
         if (hipHostMalloc((void**)&c->h_stage, bytes, hipHostMallocDefault) == hipSuccess) c->h_stage_bytes = bytes;
         else (void)hipGetLastError();
     }
-    if (bytes < kLarge || !c->h_stage) {
-        HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipStreamSynchronize(st));
-        return MFX_OK;
-    }
-    int npiece = kStageChunks, nt = 8;  // MFX_READBACK_PIECES / MFX_READBACK_THREADS: A/B knobs
-    if (const char* e = getenv("MFX_READBACK_PIECES")) npiece = std::max(1, std::min(kStageChunks, atoi(e)));
+    return c->h_stage != nullptr;
+}
+
+// Pieces [off[i], off[i] + len[i]) of h_stage, each complete once stage_ev[i] has fired, copied to
+// dst at the same offsets by nt host threads (MFX_READBACK_THREADS; thread t takes slice t of every
+// piece, in piece order). Returns when every piece is in dst.
+static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* len, int npiece) {
+    int nt = 8;
     if (const char* e = getenv("MFX_READBACK_THREADS")) nt = std::max(1, std::min(32, atoi(e)));
-    for (int i = 0; i < npiece; ++i)
-        if (!c->stage_ev[i]) HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
-    const size_t piece = (bytes / npiece + 4095) & ~(size_t)4095;
-    int used = 0;
-    for (int i = 0; i < npiece; ++i) {
-        const size_t off = piece * i;
-        if (off >= bytes) break;
-        HIPCHECK(hipMemcpyAsync(c->h_stage + off, (const uint8_t*)src + off, std::min(piece, bytes - off),
-                                hipMemcpyDeviceToHost, st));
-        HIPCHECK(hipEventRecord(c->stage_ev[i], st));
-        used = i + 1;
-    }
-    // thread t copies slice t of every piece, in piece order, once the piece's DMA has finished
     auto work = [&](int t) -> hipError_t {
-        for (int i = 0; i < used; ++i) {
+        for (int i = 0; i < npiece; ++i) {
             const hipError_t e = hipEventSynchronize(c->stage_ev[i]);
             if (e != hipSuccess) return e;
-            const size_t off0 = piece * i, len = std::min(piece, bytes - off0);
-            const size_t part = (len / nt + 4095) & ~(size_t)4095;
-            if (part * t >= len) continue;
-            const size_t off = off0 + part * t;
-            std::memcpy((uint8_t*)dst + off, c->h_stage + off, std::min(part, len - part * t));
+            const size_t part = (len[i] / nt + 4095) & ~(size_t)4095;
+            if (part * t >= len[i]) continue;
+            const size_t o = off[i] + part * t;
+            std::memcpy((uint8_t*)dst + o, c->h_stage + o, std::min(part, len[i] - part * t));
         }
         return hipSuccess;
     };
@@ -1264,8 +1282,41 @@ static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, h
     err[0] = work(0);
     for (auto& t : th) t.join();
     for (hipError_t e : err)
-        if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("host_readback: ") + hipGetErrorString(e));
+        if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("readback: ") + hipGetErrorString(e));
     return MFX_OK;
+}
+
+static int stage_events(mfx_ctx* c) {
+    for (int i = 0; i < kStageChunks; ++i) {
+        if (!c->stage_ev[i]) HIPCHECK(hipEventCreateWithFlags(&c->stage_ev[i], hipEventDisableTiming));
+        if (!c->band_ev[i]) HIPCHECK(hipEventCreateWithFlags(&c->band_ev[i], hipEventDisableTiming));
+    }
+    return MFX_OK;
+}
+
+// stream-ordered after what `st` has enqueued, complete on return; a small readback (or with no
+// staging memory) is a plain copy
+static int host_readback(mfx_ctx* c, void* dst, const void* src, size_t bytes, hipStream_t st) {
+    const size_t kLarge = 16u << 20;
+    if (bytes < kLarge || !ensure_stage(c, bytes)) {
+        HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipStreamSynchronize(st));
+        return MFX_OK;
+    }
+    int npiece = kStageChunks;  // MFX_READBACK_PIECES: A/B knob
+    if (const char* e = getenv("MFX_READBACK_PIECES")) npiece = std::max(1, std::min(kStageChunks, atoi(e)));
+    int rc = stage_events(c);
+    if (rc) return rc;
+    const size_t piece = (bytes / npiece + 4095) & ~(size_t)4095;
+    size_t off[kStageChunks], len[kStageChunks];
+    int used = 0;
+    for (int i = 0; i < npiece && piece * i < bytes; ++i, ++used) {
+        off[i] = piece * i;
+        len[i] = std::min(piece, bytes - off[i]);
+        HIPCHECK(hipMemcpyAsync(c->h_stage + off[i], (const uint8_t*)src + off[i], len[i], hipMemcpyDeviceToHost, st));
+        HIPCHECK(hipEventRecord(c->stage_ev[i], st));
+    }
+    return copy_staged(c, dst, off, len, used);
 }
 
 int mfx_accum_read_mean(mfx_ctx* c, double count, double* frame) {
@@ -1656,15 +1707,65 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
     return MFX_OK;
 }
 
+// mfx_sample on one device: the trace with its last resolve in column bands of tiles (ResolveSplit),
+// each band's mean enqueued right behind its resolve and its readback on the copy stream, so the
+// frame's DMA and the host copy overlap the rest of the resolve. A band of tile columns is a contiguous
+// range of the x-major frame (pixel = x * h + y). The bits are the unbanded path's: a pixel's sum is
+// its own thread's, and the mean is the same division. MFX_SAMPLE_BANDS=0: the unbanded path.
+// Returns 1 (nothing done) when the call is not for it (a device list, no staging memory).
+static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
+    int nb = kStageChunks;
+    if (const char* e = getenv("MFX_SAMPLE_BANDS")) nb = std::min(kStageChunks, atoi(e));
+    const int W = c->host.width, H = c->host.height;
+    nb = std::min(nb, (W + 7) / 8);
+    const size_t bytes = 4 * sizeof(double) * (size_t)c->npix;
+    if (nb < 1 || !c->peers.empty() || !c->comms.empty() || !ensure_stage(c, bytes)) return 1;
+    HIPCHECK(hipSetDevice(c->device));
+    int rc = stage_events(c);
+    if (rc) return rc;
+    if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    size_t off[kStageChunks] = {0}, len[kStageChunks] = {0};
+    ResolveSplit S;
+    S.nbands = nb;
+    S.after = [&](int k, int tx0, int ntx) -> int {
+        const int64_t p0 = (int64_t)tx0 * 8 * H, p1 = (int64_t)std::min(W, (tx0 + ntx) * 8) * H;
+        off[k] = (size_t)p0 * 4 * sizeof(double);
+        len[k] = (size_t)(p1 - p0) * 4 * sizeof(double);
+        HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, c->d_frame, c->stream, p0, p1));
+        HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
+        HIPCHECK(hipStreamWaitEvent(c->copy_stream, c->band_ev[k], 0));
+        if (len[k]) HIPCHECK(hipMemcpyAsync(c->h_stage + off[k], (const uint8_t*)c->d_frame + off[k], len[k],
+                                            hipMemcpyDeviceToHost, c->copy_stream));
+        HIPCHECK(hipEventRecord(c->stage_ev[k], c->copy_stream));
+        return MFX_OK;
+    };
+    c->rep_valid = false;
+    c->accum_merged = false;
+    rc = dev_trace_accumulate(c, spp, c->next_sample, &S);
+    if (rc) return rc;
+    rc = settle_queue_auto(c);
+    if (rc) return rc;
+    c->next_sample += spp;
+    if (!S.used) {  // (one sample per pixel: the megakernel ran, no banded resolve)
+        rc = mfx_accum_read_mean(c, (double)spp, frame);
+        return rc ? rc : mfx_sync(c);
+    }
+    rc = copy_staged(c, frame, off, len, nb);
+    return rc ? rc : mfx_sync(c);
+}
+
 int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {
     if (!c || !frame) return fail(MFX_E_INVALID, "null argument");
     if (c->api_part_count != 1)
         return fail(MFX_E_STATE, "mfx_sample needs the whole film and sample set (part_count == 1); "
                                  "partitioned contexts compose with mfx_trace_accumulate + a reduce");
+    if (spp < 1) return fail(MFX_E_INVALID, "spp must be >= 1");
     int rc = ahead_break(c);  // it moves the sample sequence past held frames
     if (rc) return rc;
     rc = mfx_accum_clear(c);
     if (rc) return rc;
+    rc = sample_banded(c, spp, frame);
+    if (rc != 1) return rc;
     rc = mfx_trace_accumulate(c, spp, c->next_sample);
     if (rc) return rc;
     c->next_sample += spp;

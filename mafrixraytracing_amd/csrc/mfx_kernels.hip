@@ -418,9 +418,11 @@ __global__ void __launch_bounds__(256) anyhit_packet16_kernel(QueryParams Q, uns
 // Film + post (FP64, reference order)
 // ----------------------------------------------------------------------------------------------
 // mean of this call's samples -> x-major RGBA doubles (texture[i,j] <- color / float n)
-__global__ void mean_kernel(const double* __restrict__ accum, int64_t npix, double n, double* __restrict__ out) {
-    const int64_t q = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (q >= npix) return;
+// (pixels [p0, p1) only: mfx_sample's banded readback)
+__global__ void mean_kernel(const double* __restrict__ accum, int64_t npix, double n, double* __restrict__ out,
+                            int64_t p0, int64_t p1) {
+    const int64_t q = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p1) return;
     out[4 * q + 0] = accum[q] / n;
     out[4 * q + 1] = accum[npix + q] / n;
     out[4 * q + 2] = accum[2 * npix + q] / n;
@@ -555,8 +557,11 @@ hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st) {
-    hipLaunchKernelGGL(mean_kernel, dim3(grid_for(npix, 256)), dim3(256), 0, st, accum, npix, n, out);
+hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st, int64_t p0,
+                           int64_t p1) {
+    if (p1 < 0) p1 = npix;
+    if (p1 <= p0) return hipSuccess;
+    hipLaunchKernelGGL(mean_kernel, dim3(grid_for(p1 - p0, 256)), dim3(256), 0, st, accum, npix, n, out, p0, p1);
     return hipGetLastError();
 }
 

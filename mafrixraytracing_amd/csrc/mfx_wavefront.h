@@ -169,6 +169,7 @@ struct WfParams {
     int32_t ninst_lds;                    // two-level scenes: instances each trace kernel keeps in LDS
     int32_t cam_grid;                     // > 0: a generation's camera rays run k_camera (packets) on this grid
     int32_t iter;                         // the iteration (0 = camera rays); k_extend counts its rays per iteration
+    int32_t res_tx0, res_ntx;             // k_resolve: only tile columns [res_tx0, res_tx0 + res_ntx) (0: every column)
 };
 
 #ifndef MFX_RAY_QUEUE

@@ -1154,7 +1154,12 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     __syncthreads();
     const int tiles_x = (P.width + 7) >> 3;
     const int64_t per_sample = (int64_t)tiles_x * P.band_rows * 64;
-    const int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    int64_t q = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (P.res_ntx > 0) {  // a band of tile columns (mfx_sample's banded resolve): thread -> its tile's q
+        const int64_t tl = q >> 6;
+        if (tl >= (int64_t)P.res_ntx * P.band_rows) return;
+        q = ((tl / P.res_ntx) * tiles_x + P.res_tx0 + tl % P.res_ntx) * 64 + (q & 63);
+    }
     if (q >= per_sample) return;
     const int64_t tile = q >> 6;
     const int within = (int)(q & 63);
@@ -1356,7 +1361,7 @@ hipError_t mfx_wf_iteration(const WfParams& P, int ext_grid, int shd_grid, bool 
 }
 
 hipError_t mfx_wf_resolve(const WfParams& P, hipStream_t st) {
-    const int64_t per_sample = (int64_t)((P.width + 7) >> 3) * P.band_rows * 64;
+    const int64_t per_sample = (int64_t)(P.res_ntx > 0 ? P.res_ntx : (P.width + 7) >> 3) * P.band_rows * 64;
     if (P.film) hipLaunchKernelGGL(k_resolve<true>, dim3((unsigned)((per_sample + 255) / 256)), dim3(256), 0, st, P);
     else hipLaunchKernelGGL(k_resolve<false>, dim3((unsigned)((per_sample + 255) / 256)), dim3(256), 0, st, P);
     return hipGetLastError();

@@ -41,6 +41,9 @@ def main():
         fp = frame.ctypes.data_as(C.POINTER(C.c_double))
         out["accum_read_mean_ms"] = best(lambda: ctx.lib.mfx_accum_read_mean(ctx._h, float(spp), fp))
         out["sample_ms"] = best(lambda: ctx.sample(spp, out=frame), 3)
+        os.environ["MFX_SAMPLE_BANDS"] = "0"  # the unbanded path: trace, then mean + staged readback
+        out["sample_ms_unbanded"] = best(lambda: ctx.sample(spp, out=frame), 3)
+        os.environ.pop("MFX_SAMPLE_BANDS")
         # host_readback's pieces x copy threads (read per call from the environment)
         sweep = {}
         for pieces, threads in ((4, 4), (8, 4), (8, 8), (8, 12), (4, 8), (8, 16)):
