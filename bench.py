@@ -361,6 +361,7 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repea
         per_rep_slowest = [max(r[i] for r in rank_reps) for i in range(repeats)]
         out[str(n)] = {"film_share_per_gpu": round(1.0 / n, 6), "spp_per_gpu": spp, "frames_in_flight": nif,
                        "rank_ms_per_step": [round(t, 3) for t in rank_ms],
+                       "rank_rays_rel": [round(r / (job_rays / n), 4) for r in rank_rays],
                        "slowest_rank_ms": round(t_rank, 3), "repeats": repeats,
                        "slowest_rank_repeats_ms": [round(t, 3) for t in slow],
                        "spread": round((max(slow) - min(slow)) / t_rank, 4),

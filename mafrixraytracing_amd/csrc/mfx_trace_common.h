@@ -931,27 +931,41 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
 // Closest hits of the wave's active lanes (act) by packet traversal; B per lane as traverse() gives.
 // STATS: besides the per-lane visits (st), the wave's own fetches: wave-uniform node steps (one
 // 128-B node each) and leaf slots (an 80-B test prefix each), counted on every lane alike.
-template <bool STATS>
+// PH (diagnostic builds, -DMFX_DIAG_STAMPS=3): ph[0] += the wave's cycles in node steps, ph[1] += in
+// leaf tests, ph[2] += node steps, ph[3] += leaf visits
+template <bool STATS, bool PH = false>
 __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
                                                int* stk, uint64_t* stm, Stats& st, uint32_t& pk_nodes,
-                                               uint32_t& pk_slots) {
+                                               uint32_t& pk_slots, uint64_t* ph = nullptr) {
     B = Best{tMax, -1, -1, false};
     const RayF rf = make_rayf(o, d);
     float tlim = f_tlim(tMax);
     uint64_t mask = __ballot(act);
     const int rep = __builtin_ctzll(mask);
     int sp = 0, node = 0;
+    uint64_t t0 = 0;
     while (true) {
+        if (PH) t0 = diag_clock();
         while (node >= 0) {
             if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
             if (STATS) pk_nodes++;
+            if (PH) ph[2]++;
             node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep);
+        }
+        if (PH) {
+            const uint64_t t1 = diag_clock();
+            ph[0] += t1 - t0;
+            t0 = t1;
         }
         if (node == MFX_TRAV_EXIT) return;
         if (STATS) pk_slots += (~node & 7) + 1;
         if ((mask >> __lane_id()) & 1) {  // the lanes whose ray hits the leaf's box
             leaf_hit<false, STATS, true>(S, ~node, o, d, 1e-6, tMax, B, st);
             tlim = f_tlim(B.t);
+        }
+        if (PH) {
+            ph[1] += diag_clock() - t0;
+            ph[3]++;
         }
         if (sp > 0) {
             --sp;

@@ -51,7 +51,7 @@ __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 #endif
 
 #ifndef MFX_DIAG_STAMPS
-#define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow
+#define MFX_DIAG_STAMPS 0  // diagnostic build only: 1 = k_extend phase stamps, 2 = k_shadow, 3 = k_camera
 #endif
 struct DiagAcc {
     uint64_t fetch, node, leaf, fin, last, scan, shade, lat;  // lat: node loads' issue-to-use cycles (node_step)
@@ -666,6 +666,21 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     uint32_t c_primary = 0;
     Stats st{0, 0, 0};
     uint32_t pk_nodes = 0, pk_slots = 0;  // STATS: the wave's own node and slot fetches (every lane counts them)
+#if MFX_DIAG_STAMPS == 3
+    // the wave's cycles per phase (window scan, camera ray, node steps, leaf tests, result writes) and
+    // its node steps and leaf visits (scripts/camera_phases.py); the shipped build has none of it
+    uint64_t ph[4] = {0, 0, 0, 0}, t_scan = 0, t_gen = 0, t_out = 0, t_last = stamp();
+#define CAM_MARK(acc)                  \
+    do {                               \
+        const uint64_t _t = stamp();   \
+        (acc) += _t - t_last;          \
+        t_last = _t;                   \
+    } while (0)
+#else
+#define CAM_MARK(acc) \
+    do {              \
+    } while (0)
+#endif
     while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr, P.ctl + WF_CTL_CLOSED_EXT)) {
         const int j = sc.win_next + lane;
         const int sj = sc.word();
@@ -675,6 +690,7 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
         // edge-tile padding starts no path
         const bool act = sj == WF_FREE && j < P.total && path_pixel(P, P.path_base + j, x, y, smp);
         if (!__any(act)) continue;
+        CAM_MARK(t_scan);
         DV o = dv(0, 0, 0), d = dv(0, 0, 1);
         if (act) {  // PixelIntegrator.Sample (Integrators.fs:167-169) + GetRay (Camera.fs:134-139)
             const int64_t pixel = (int64_t)x * P.height + y;  // Color[w,h] x-major
@@ -690,7 +706,13 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
             c_primary++;
         }
         Best B;
+#if MFX_DIAG_STAMPS == 3
+        CAM_MARK(t_gen);
+        packet_closest<STATS, true>(S, act, o, d, 99999999., B, stk, stm, st, pk_nodes, pk_slots, ph);
+        t_last = stamp();
+#else
         packet_closest<STATS>(S, act, o, d, 99999999., B, stk, stm, st, pk_nodes, pk_slots);  // Integrators.fs:108
+#endif
         if (act) {
             if (B.found) {
                 const DV hp = vadd(o, vmul(d, B.t));  // Ray.PointAtParameter (Ray.fs:8-9)
@@ -700,9 +722,22 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
                 P.state[j] = WF_MISS | WF_FRESH;
             }
         }
+        CAM_MARK(t_out);
     }
+#undef CAM_MARK
     unsigned long long* cnt = P.counters + WF_NCTR * (blockIdx.x & (WF_SHARDS - 1));
     block_add<4>(cnt + 0, c_primary, red);
+#if MFX_DIAG_STAMPS == 3
+    if (lane == 0) {  // (MFX_DIAG_ITER prints counters 10..17 as "stamps ... outer ... node ... scan shade")
+        atomicAdd(cnt + 10, (unsigned long long)t_scan);
+        atomicAdd(cnt + 11, (unsigned long long)t_gen);
+        atomicAdd(cnt + 12, (unsigned long long)ph[0]);
+        atomicAdd(cnt + 13, (unsigned long long)ph[1]);
+        atomicAdd(cnt + 14, (unsigned long long)t_out);
+        atomicAdd(cnt + 15, (unsigned long long)ph[2]);
+        atomicAdd(cnt + 16, (unsigned long long)ph[3]);
+    }
+#endif
     if (STATS) {
         block_add<4>(cnt + 4, st.nodes, red);
         block_add<4>(cnt + 5, st.clusters, red);

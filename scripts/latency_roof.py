@@ -32,6 +32,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
 LINE = re.compile(r"gen (\d+) iter (\d+): .*?extend ([\d.]+) ms shadow ([\d.]+) ms; stamps (\S+) (\S+) (\S+) (\S+) "
                   r"outer (\S+) node (\S+);.*scan (\S+) shade (\S+) lat (\S+)")
 SHAPE = re.compile(r"blocks/CU extend (\d+) shadow (\d+) \((\d)-wave build\)")
@@ -115,7 +116,25 @@ def main():
     st2, _ = parse(run(os.path.join(ROOT, "build_variants", "st2.so"), a.scene, a.spp))
     ebpc, sbpc, _ = shape  # 256-lane blocks per CU = waves per SIMD
     nit = max(r["iter"] for r in prod)
-    res = {"scene": os.path.relpath(a.scene, ROOT), "spp": a.spp, "L_idle": L_IDLE,
+    cam = None
+    st3p = os.path.join(ROOT, "build_variants", "st3.so")
+    if os.path.exists(st3p):  # k_camera's phases (-DMFX_DIAG_STAMPS=3), VERDICT r05 Next #5
+        st3, _ = parse(run(st3p, a.scene, a.spp))
+        r = [x for x in st3 if x["iter"] == 1][0]
+        p = [x for x in prod if x["iter"] == 1][0]
+        ph = {"window_scan": r["fetch"], "camera_ray": r["node"], "node_steps": r["leaf"], "leaf_tests": r["fin"],
+              "result_writes": r["outer"]}
+        tot = sum(ph.values())
+        from mafrixraytracing_amd.scene_io import load_scene_file
+        arr = load_scene_file(a.scene)
+        tiles = (arr.width + 7) // 8 * ((arr.height + 7) // 8) * a.spp
+        cam = {"share": {k: round(v / tot, 4) for k, v in ph.items()},
+               "wave_cycles_per_tile": {k: round(v / tiles, 1) for k, v in ph.items()},
+               "node_steps_per_tile": round(r["node_iters"] / tiles, 3), "leaf_visits_per_tile": round(r["scan"] / tiles, 3),
+               "cycles_per_node_step": round(ph["node_steps"] / max(r["node_iters"], 1), 1),
+               "cycles_per_leaf_visit": round(ph["leaf_tests"] / max(r["scan"], 1), 1),
+               "ms_shipped": p["extend_ms"], "ms_stamp_build": r["extend_ms"], "tiles": tiles}
+    res = {"scene": os.path.relpath(a.scene, ROOT), "spp": a.spp, "L_idle": L_IDLE, "k_camera_phases": cam,
            "kernels": {"k_extend": kernel("k_extend", st1, prod, ebpc, a.simds, range(2, nit + 1)),
                        "k_shadow": kernel("k_shadow", st2, prod, sbpc, a.simds, range(1, nit + 1))},
            "note": "frac = node steps x loaded round trip / (resident waves x clock x shipped HIP-event time): the "
