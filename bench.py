@@ -5,7 +5,7 @@ Workload (BASELINE.json configs[1]; --config C3/C4/C5 for the
 scenes/spot.xml — spot (5,856 triangles)
 on a floor quad under a quad light, 1920x1080, 64 samples per pixel, maxDepth 3.
 A step = one frame: every GPU traces every sample of its disjoint set of the film's 8-pixel tile
-rows (image partition: rows t % N == rank, MFX_F_ROW_PARTITION) into an FP64 accumulator, then
+rows (image partition: one of each N consecutive tile rows, serpentine, MFX_F_ROW_PARTITION) into an FP64 accumulator, then
 (N > 1) the ranks' rows are gathered to GPU 0 (RowGather over RCCL: 1/N of the [3][w*h] buffer per
 rank; the merged frame is the 1-GPU frame bit for bit).
   --scaling strong (default): the job renders the metric's 1080p x 64 spp, each GPU 1/N of the film;
@@ -267,7 +267,7 @@ def sample_api(arrays, seed, spp, calls=2, flags=0):
 
 def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repeats=3):
     """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
-    measured on this GPU: rank r traces all `spp` samples of the film's tile rows r mod N
+    measured on this GPU: rank r traces all `spp` samples of the film's tile rows of band r of N
     (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
     fixed per-generation costs included); the slowest rank is the step's trace. The exchange is
     RowGather: its pack (the largest rank's rows) and rank 0's unpack of the others' are timed here
@@ -379,7 +379,8 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repea
                        "predicted_efficiency_pipelined": round(
                            (ms_1gpu / n) / (t_rank * max(1.0, ov["trace_ms_beside_it"] / ov["trace_ms_alone"]) +
                                             (0.0 if ov["exchange_completion_ms"] < t_rank else t_ex)), 4)}
-    return {"shares": out, "partition": "image: tile rows r mod N per rank (MFX_F_ROW_PARTITION), RowGather to rank 0",
+    return {"shares": out, "partition": "image: serpentine tile-row band r of N per rank (MFX_F_ROW_PARTITION), "
+                                        "RowGather to rank 0",
             "note": "every rank's share of --scaling strong at N GPUs, measured on one GPU one after another, in a fresh "
                     "process (bench.py --strong-share-child); "
                     "the exchange's pack/unpack measured here, its transfer modeled at one xGMI link "
@@ -537,7 +538,7 @@ def main():
     spp_step = step_spp(args.spp, ngpu, args.scaling)
     rows = args.partition == "rows"
     mode = (MFX_F_MEGAKERNEL if args.megakernel else MFX_F_NONE) | CONFIG_FLAGS.get(args.config, 0)
-    # one process per GPU: rank r traces tile rows r mod N (image partition) or samples r mod N
+    # one process per GPU: rank r traces tile-row band r of N (image partition) or samples r mod N
     rank_mode = mode | (MFX_F_ROW_PARTITION if rows else 0)
     devices = None
     if args.single_process:  # one context over the device list (the library's own tile-row partition)
@@ -993,10 +994,10 @@ def main():
         elif ngpu == 1:
             par = "one GPU"
         elif args.single_process:
-            par = (f"image partition x{ngpu} (tile rows t % {ngpu}), one process, the library's RCCL merge "
+            par = (f"image partition x{ngpu} (serpentine tile-row bands), one process, the library's RCCL merge "
                    "(mfx_options.devices)")
         elif rows:
-            par = (f"image partition x{ngpu} (tile rows t % {ngpu} per rank, MFX_F_ROW_PARTITION), one process per GPU, "
+            par = (f"image partition x{ngpu} (a serpentine tile-row band per rank, MFX_F_ROW_PARTITION), one process per GPU, "
                    + ("rows gathered to rank 0 over RCCL (RowGather)" if backend != "gloo" else
                       "rows merged by gloo all_reduce (the one-GPU rehearsal)")
                    + "; frame k's exchange overlapped with frame k+1's trace")

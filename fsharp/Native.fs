@@ -247,7 +247,7 @@ let marshalCamera (camera : ICamera) : MfxPinhole =
 
 /// IPixelIntegrator (IIntegrator.fs:35-40) over one libmafrix_rt context.
 ///   devices = [||]: HIP device 0; devices = [|0..7|]: one context drives all eight GPUs of the
-///   node by an image partition (GPU g traces the 8-pixel tile rows r % 8 = g of every frame and
+///   node by an image partition (GPU g traces one of each 8 consecutive 8-pixel tile rows of every frame and
 ///   batch, and copies its rows of each RGBA8 frame into the buffer): the frames are the one-GPU bytes.
 /// Sample(n) writes the mean of n fresh samples per pixel straight into a pinned Color[w,h]
 /// (Color is a sequential 4 x float struct, Color.fs:3-4; element (i,j) at i*h + j, as

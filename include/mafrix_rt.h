@@ -97,7 +97,8 @@ typedef struct mfx_scene_desc {
  * Devices: with ndevices == 0 the context runs on `device`. With ndevices > 0 it drives
  * devices[0..ndevices) from this one process (the reference's in-process fan-out,
  * Integrators.fs:164, across GPUs) by an image partition: device g of G traces the film's
- * 8-pixel tile rows r with r % G == g, every sample of the context's sample partition, on its own
+ * 8-pixel tile rows of band g of G — one of each G consecutive tile rows, at offset g in even groups
+ * and G - 1 - g in odd ones (serpentine) — every sample of the context's sample partition, on its own
  * stream. Every per-pixel operation (the sample-order sum, Film.AddSample, the post) therefore runs
  * on one device in the one-device order, and every output is bit-identical to a one-device
  * context's. mfx_render_rgba8 (render-ahead included) copies each device's rows of the RGBA8
@@ -111,7 +112,7 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
     int32_t flags;      /* MFX_F_* */
     int32_t part_index; /* this context renders sample partition part_index of part_count */
     int32_t part_count; /* (multi-process: one context per rank; partitions are disjoint sample sets;
-                           with MFX_F_ROW_PARTITION disjoint sets of tile rows r % part_count == part_index) */
+                           with MFX_F_ROW_PARTITION disjoint sets of tile rows: band part_index of part_count) */
     int32_t ndevices;   /* 0: one device (`device`); 1..MFX_MAX_DEVICES: the device list below */
     int32_t render_ahead; /* 0 or 1: off. K in 2..MFX_MAX_RENDER_AHEAD: one-sample mfx_render_rgba8
                              calls (Scene.Render) take their sample from a batch of the next K
@@ -132,8 +133,9 @@ typedef struct mfx_options {  /* ABI 4: the former `reserved` field is render_ah
                                flattened when the flat image fits MFX_FLATTEN_MAX_BYTES (env; default
                                2 GiB at 512 B per traversal slot of the expansion) and a sixteenth of
                                the device's free memory, two-level otherwise. Both flags: MFX_E_INVALID */
-#define MFX_F_ROW_PARTITION 64 /* part_index / part_count partition the film's 8-pixel tile rows (r % part_count
-                               == part_index) instead of the samples: a rank traces every sample of its rows,
+#define MFX_F_ROW_PARTITION 64 /* part_index / part_count partition the film's 8-pixel tile rows (serpentine
+                               band part_index of part_count, as a device list's devices) instead of the
+                               samples: a rank traces every sample of its rows,
                                its accumulator is +0.0 elsewhere, and a sum-reduce over the ranks is an exact
                                merge (the multi-process image partition; mfx_trace_accumulate)       */
 #define MFX_F_IN_FLIGHT 128 /* the caller keeps frames in flight on several contexts of this device (each its
@@ -345,7 +347,7 @@ int mfx_aabb_selftest(int32_t device, int64_t n, const double* rec, int32_t* out
 /* How a context's work is laid over devices (ABI 6, additive): out[0] = devices G, out[1] = RCCL
  * communicators the context created (G for a list of distinct devices, else 0), out[2] = how
  * mfx_accum_reduce merges (0 one device, 1 RCCL reduce, 2 device-ordered adds: a repeated device),
- * out[3] / out[4] = the primary's tile-row band (band_index, band_count: rows r % band_count ==
+ * out[3] / out[4] = the primary's tile-row band (band_index, band_count: the serpentine band
  * band_index), out[5 + g] = device g's HIP ordinal. cap = entries of out (>= 5 + G).          */
 int mfx_device_info(mfx_ctx* ctx, int32_t* out, int32_t cap);
 

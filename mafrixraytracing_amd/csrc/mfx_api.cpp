@@ -136,7 +136,8 @@ struct mfx_ctx {
     uint64_t seed = 0;
     int flags = 0;
     int part_index = 0, part_count = 1;  // sample partition: global samples part_index mod part_count
-    // image partition: this device traces the film's 8-pixel tile rows r = band_index mod band_count
+    // image partition: this device traces the film's 8-pixel tile rows of band band_index of band_count
+    // (band_tile_row, mfx_device.h: one of each band_count consecutive tile rows, serpentine)
     // (device g of a G-device list: g of G; an MFX_F_ROW_PARTITION rank composes with it)
     int band_index = 0, band_count = 1;
     int64_t next_sample = 0;
@@ -247,7 +248,7 @@ static std::vector<mfx_ctx*> devs_of(mfx_ctx* c) {
 // tile rows of the film in a device's band (its image partition)
 static int band_rows(const mfx_ctx* d) {
     const int tr = (d->host.height + 7) / 8;
-    return tr > d->band_index ? (tr - d->band_index + d->band_count - 1) / d->band_count : 0;
+    return band_row_count(d->band_index, d->band_count, tr);
 }
 
 static void ahead_free(mfx_ctx* c) {
@@ -560,7 +561,7 @@ static int create_impl(const mfx_scene_desc* scene, const mfx_instance* instance
         const bool dev = err.rfind("GPU BVH build", 0) == 0;
         return fail(dev ? MFX_E_DEVICE : MFX_E_INVALID, "mfx_create: " + err);
     }
-    // Image partition: device g of G traces the film's tile rows r = g mod G, every sample of the
+    // Image partition: device g of G traces the film's tile rows of band g of G, every sample of the
     // caller's partition, so every per-pixel operation (the sample-order sum, the film add, the post)
     // runs on one device in the one-device order: images are bit-identical to one device's, and the
     // devices' buffers merge exactly (a pixel is non-zero on its own device only). With
@@ -1594,8 +1595,9 @@ static int ahead_launch(mfx_ctx* c, int xi, int64_t base, int src, double count0
 }
 
 // A device's band rows of a y-major RGBA8 frame (device memory) into the caller's frame (host):
-// one copy of the whole frame for a one-device context; on a device list one strided copy of its
-// whole tile rows (8 rows every band_count * 8) plus the film's partial last tile row if it owns it.
+// one copy of the whole frame for a one-device context; on a device list two strided copies of its
+// whole tile rows (band_tile_row: the even groups' rows and the odd groups' rows, each 8 rows every
+// 2 * band_count * 8) plus the film's partial last tile row if it owns it.
 static int copy_band_rgba(const mfx_ctx* d, uint8_t* dst, const uint8_t* src, hipStream_t st) {
     const int W = d->host.width, H = d->host.height;
     const size_t row = 4 * (size_t)W;
@@ -1604,12 +1606,15 @@ static int copy_band_rgba(const mfx_ctx* d, uint8_t* dst, const uint8_t* src, hi
         return MFX_OK;
     }
     const int full = H / 8, tr = (H + 7) / 8, bi = d->band_index, bc = d->band_count;
-    const int nfull = full > bi ? (full - bi + bc - 1) / bc : 0;
-    if (nfull > 0) {
-        const size_t off = (size_t)8 * bi * row, pitch = (size_t)8 * bc * row;
-        HIPCHECK(hipMemcpy2DAsync(dst + off, pitch, src + off, pitch, 8 * row, (size_t)nfull, hipMemcpyDeviceToHost, st));
+    const int nb = band_row_count(bi, bc, tr);
+    for (int k0 = 0; k0 < 2; ++k0) {
+        int n = 0;  // the band's rows of this parity that are whole tile rows (a prefix: rows grow with k)
+        for (int k = k0; k < nb && band_tile_row(bi, bc, k) < full; k += 2) ++n;
+        if (n == 0) continue;
+        const size_t off = (size_t)8 * band_tile_row(bi, bc, k0) * row, pitch = (size_t)16 * bc * row;
+        HIPCHECK(hipMemcpy2DAsync(dst + off, pitch, src + off, pitch, 8 * row, (size_t)n, hipMemcpyDeviceToHost, st));
     }
-    if (full < tr && (tr - 1) % bc == bi) {
+    if (full < tr && nb > 0 && band_tile_row(bi, bc, nb - 1) == tr - 1) {
         const size_t off = (size_t)8 * full * row;
         HIPCHECK(hipMemcpyAsync(dst + off, src + off, (size_t)(H - 8 * full) * row, hipMemcpyDeviceToHost, st));
     }

@@ -7,6 +7,17 @@
 
 #include "mfx_layout.h"
 
+// Image partition (device lists, MFX_F_ROW_PARTITION ranks): band bi of bc owns one 8-pixel tile row
+// of each group of bc consecutive tile rows, at offset bi in even groups and bc - 1 - bi in odd ones
+// (serpentine), so a band's rows sit at every offset within the groups alike and a gradient of work
+// down a group (C2: +4.5 % rays from its top tile row to its bottom one, r06b rank_rays_rel) does
+// not load one band more than another. Its k-th tile row, and how many of the film's tr it owns:
+__host__ __device__ inline int band_tile_row(int bi, int bc, int k) { return k * bc + ((k & 1) ? bc - 1 - bi : bi); }
+__host__ __device__ inline int band_row_count(int bi, int bc, int tr) {
+    const int g = tr / bc, off = (g & 1) ? bc - 1 - bi : bi;
+    return g + (off < tr - g * bc ? 1 : 0);
+}
+
 struct TraceParams {
     const MfxNode* nodes;
     const MfxSlot* slots;
@@ -23,7 +34,7 @@ struct TraceParams {
     int64_t sample_base;             // first global sample index of this call
     int64_t nsamples;                // samples this context renders per pixel in this call
     int32_t part_index, part_count;  // global sample = sample_base + part_index + s * part_count
-    int32_t band_index, band_count, band_rows;  // image partition: tile rows band_index + k * band_count (WfParams)
+    int32_t band_index, band_count, band_rows;  // image partition: tile rows band_tile_row(band_index, band_count, k)
     int32_t width, height, max_depth;
     int32_t stack_size;              // LDS traversal stack entries per lane
     int32_t chunk;                   // path indices a wave takes per atomic

@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256, WAVES) trace_kernel(TraceParams P) {
                 const int64_t tile = q >> 6;
                 const int within = (int)(q & 63);
                 const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-                const int y = (P.band_index + (int)(tile / tiles_x) * P.band_count) * 8 + (within >> 3);
+                const int y = band_tile_row(P.band_index, P.band_count, (int)(tile / tiles_x)) * 8 + (within >> 3);
                 if (x < W && y < H) {
                     // PixelIntegrator.Sample (Integrators.fs:166-169) + PinholeCamera.GetRay (Camera.fs:134-139)
                     pixel = (int64_t)x * H + y;  // Color[w,h] x-major

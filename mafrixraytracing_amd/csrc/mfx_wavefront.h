@@ -151,7 +151,8 @@ struct WfParams {
     int64_t sample_base;
     int32_t part_index, part_count;
     // image partition (a device list's devices, MFX_F_ROW_PARTITION ranks): this trace covers the
-    // 8-pixel tile rows r = band_index + k * band_count, band_rows of them (1 / 0 / all: the whole film)
+    // 8-pixel tile rows band_tile_row(band_index, band_count, k) (mfx_device.h: serpentine), band_rows
+    // of them (1 / 0 / all: the whole film)
     int32_t band_index, band_count, band_rows;
     int32_t pool;                         // slots scanned (>= total, a multiple of 64)
     int32_t width, height, max_depth;

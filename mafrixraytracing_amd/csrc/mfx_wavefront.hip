@@ -296,7 +296,7 @@ __device__ __forceinline__ bool path_pixel(const PP& P, int64_t p, int& x, int& 
     const unsigned q = qs - ds * per_sample;
     const unsigned tile = q >> 6, within = q & 63;
     const unsigned tyl = tile / tiles_x;
-    const unsigned ty = (unsigned)P.band_index + tyl * (unsigned)P.band_count;
+    const unsigned ty = (unsigned)band_tile_row(P.band_index, P.band_count, (int)tyl);
     x = (int)((tile - tyl * tiles_x) * 8 + (within & 7));
     y = (int)(ty * 8 + (within >> 3));
     return x < P.width && y < P.height;
@@ -1199,7 +1199,7 @@ __global__ void __launch_bounds__(256) k_resolve(WfParams P) {
     const int64_t tile = q >> 6;
     const int within = (int)(q & 63);
     const int x = (int)(tile % tiles_x) * 8 + (within & 7);
-    const int y = (P.band_index + (int)(tile / tiles_x) * P.band_count) * 8 + (within >> 3);  // the band's film row
+    const int y = band_tile_row(P.band_index, P.band_count, (int)(tile / tiles_x)) * 8 + (within >> 3);  // the band's film row
     if (x >= P.width || y >= P.height) return;
     const int64_t npix = (int64_t)P.width * P.height;
     const int64_t pixel = (int64_t)x * P.height + y;

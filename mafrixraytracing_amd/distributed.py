@@ -2,7 +2,8 @@
 This is the path `bench.py --gpus N` runs under torch.distributed.run.
 
 Every (pixel, sample) path is independent (Integrators.fs:164-171), so rank r of W traces every
-sample of the film's 8-pixel tile rows t with t % W == r (mfx_options.flags MFX_F_ROW_PARTITION,
+sample of the film's 8-pixel tile rows it owns — one of each W consecutive ones, serpentine
+(tile_row_owner) — (mfx_options.flags MFX_F_ROW_PARTITION,
 part_index / part_count) into an FP64 accumulator it owns, which stays +0.0 outside its rows. Every
 pixel's sample-order sum runs on one rank, so the merged frame is the 1-rank frame bit for bit, and
 the only exchange is moving each rank's rows to rank 0:
@@ -34,11 +35,20 @@ def partition_samples(spp: int, rank: int, world: int) -> np.ndarray:
     return np.arange(rank, spp, world, dtype=np.int64)
 
 
+def tile_row_owner(t, world: int):
+    """The rank that owns 8-pixel tile row t under the image partition (csrc/mfx_device.h
+    band_tile_row): each group of `world` consecutive tile rows gives one row to every rank, in rank
+    order in even groups and in reverse order in odd ones (serpentine, so a gradient of work down a
+    group does not load one rank more than another)."""
+    g, o = np.divmod(np.asarray(t, dtype=np.int64), world)
+    return np.where(g % 2 == 0, o, world - 1 - o)
+
+
 def partition_rows(height: int, rank: int, world: int) -> np.ndarray:
-    """Film rows y that `rank` renders under the image partition: its 8-pixel tile rows
-    (y // 8) % world == rank (MFX_F_ROW_PARTITION; a device list's device g of G likewise)."""
+    """Film rows y that `rank` renders under the image partition: the rows of the 8-pixel tile rows
+    it owns (tile_row_owner; MFX_F_ROW_PARTITION, and a device list's device g of G likewise)."""
     y = np.arange(height, dtype=np.int64)
-    return y[(y // 8) % world == rank]
+    return y[tile_row_owner(y // 8, world) == rank]
 
 
 def step_spp(config_spp: int, world: int, scaling: str) -> int:

@@ -111,13 +111,13 @@ def test_ranks_merge_to_the_single_rank_image(oracle, tmp_path, world, rows):
 
 
 def test_partition_rows_cover_every_row_once():
-    from mafrixraytracing_amd.distributed import partition_rows
+    from mafrixraytracing_amd.distributed import partition_rows, tile_row_owner
     for h in (1, 8, 12, 37, 1080):
         for world in (1, 2, 3, 8):
             allr = np.concatenate([partition_rows(h, r, world) for r in range(world)])
             assert sorted(allr.tolist()) == list(range(h))
             for r in range(world):
-                assert all((y // 8) % world == r for y in partition_rows(h, r, world))
+                assert all(tile_row_owner(y // 8, world) == r for y in partition_rows(h, r, world))
 
 
 def test_partition_covers_every_sample_once():
@@ -145,3 +145,29 @@ def test_frames_in_flight_policy():
     assert [frames_in_flight(1920, 1080, 64, n) for n in (1, 2, 4, 8)] == [1, 1, 3, 3]
     assert frames_in_flight(1920, 1080, 512, 8) == 1  # the weak job's share: 8x the paths
     assert frames_in_flight(1920, 1080, 64, 8, rows=False) == 1  # a sample partition keeps the whole film
+
+
+def test_band_rows_match_the_library(tmp_path):
+    """The kernels' band mapping (csrc/mfx_device.h band_tile_row / band_row_count, compiled here for
+    the host) is the partition distributed.py gathers by: for every band count and film height each
+    band's tile rows are exactly the rows tile_row_owner gives it, in increasing order, and the bands
+    cover every tile row once."""
+    import subprocess
+    from mafrixraytracing_amd.distributed import tile_row_owner
+    src = tmp_path / "bt.cpp"
+    src.write_text('#include "mfx_device.h"\n#include <cstdio>\nint main() {\n'
+                   '  for (int bc = 1; bc <= 9; ++bc) for (int tr = 0; tr <= 40; ++tr) for (int bi = 0; bi < bc; ++bi) {\n'
+                   '    int n = band_row_count(bi, bc, tr); printf("%d %d %d", bc, tr, bi);\n'
+                   '    for (int k = 0; k < n; ++k) printf(" %d", band_tile_row(bi, bc, k)); printf("\\n"); } }\n')
+    exe = tmp_path / "bt"
+    subprocess.run(["g++", "-std=c++17", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+                    "-I" + os.path.join(ROOT, "mafrixraytracing_amd", "csrc"), "-o", str(exe), str(src)], check=True)
+    seen = {}
+    for line in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines():
+        v = [int(x) for x in line.split()]
+        bc, tr, bi, rows = v[0], v[1], v[2], v[3:]
+        want = [t for t in range(tr) if int(tile_row_owner(t, bc)) == bi]
+        assert rows == want, (bc, tr, bi, rows, want)
+        seen.setdefault((bc, tr), []).extend(rows)
+    for (bc, tr), rows in seen.items():
+        assert sorted(rows) == list(range(tr)), (bc, tr)
