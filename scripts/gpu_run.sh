@@ -22,6 +22,7 @@
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
 #   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
 #                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
+#   sampletrace          mfx_sample under rocprofv3 kernel + memory-copy trace (scripts/sample_trace.py)
 #   py:SCRIPT[:ARGS]     scripts/SCRIPT.py ARGS (comma-separated) -> SCRIPT.json
 #   latroof:SCENE:SPP    latency roof of k_extend / k_shadow from the stamp builds build_variants/st1.so,
 #                        st2.so (scripts/latency_roof.py) -> latency_SCENE.json
@@ -127,6 +128,15 @@ for step in "$@"; do
       timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a1 --spp ${a2:-64} \
         --out $O/latency_$(basename $a1 .xml).json > $O/latroof.log 2>&1
       tail -5 $O/latroof.log ;;
+    sampletrace)
+      # mfx_sample under a kernel + memory-copy trace, banded vs unbanded (scripts/sample_trace.py)
+      D=$R/$O/sampletrace
+      mkdir -p $D
+      (cd /tmp && export TMPDIR=/tmp &&
+       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d $D/trace -o run -- \
+         python3 $R/scripts/sample_trace.py > $D/run.json 2> $D/run.err)
+      cat $D/run.json
+      python3 scripts/sample_trace.py --timeline $D/trace > $D/timeline.txt; tail -40 $D/timeline.txt ;;
     py)
       # py:SCRIPT[:ARGS] -- scripts/SCRIPT.py with comma-separated ARGS -> SCRIPT.json / SCRIPT.err
       X=(); [ -n "$a2" ] && IFS=, read -ra X <<< "$a2"
