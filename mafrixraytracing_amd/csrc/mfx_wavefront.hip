@@ -136,6 +136,8 @@ struct Scanner {
     // closed: the launch's closed-shard mask (WF_CLOSED_MASK): bit g set by the one fetch that
     // crosses shard g's end (the fetch whose start lands in [cap, cap + chunk)); a wave also skips the
     // shards its own fetches found closed, so an unset bit never makes it retry one
+    // LOAD = false (k_camera: every slot of a generation's first iteration is FREE): no state words
+    template <bool LOAD = true>
     __device__ __forceinline__ bool window(unsigned long long* heads, int chunk, int shard_size,
                                            const int32_t* __restrict__ state, const unsigned long long* qcount,
                                            unsigned long long* closed) {
@@ -149,7 +151,7 @@ struct Scanner {
             if ((int64_t)c < cap) {
                 win_next = shard * shard_size + (int)c;
                 win_end = shard * shard_size + min((int)c + chunk, cap);
-                fill(state);
+                if (LOAD) fill(state);
                 return true;
             }
 #if WF_CLOSED_MASK
@@ -681,14 +683,22 @@ __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {
     do {              \
     } while (0)
 #endif
-    while (sc.window(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr, P.ctl + WF_CTL_CLOSED_EXT)) {
-        const int j = sc.win_next + lane;
-        const int sj = sc.word();
-        sc.advance(P.state);
+    // Every slot is FREE in a generation's first iteration (wf_trace zeroes the state words), so the
+    // windows are taken without reading them, and a window is one 8x8 tile of one sample: its
+    // (sample, tile) come from one wave-uniform path_pixel (scalar arithmetic), the lanes' pixels by
+    // offset (the same x, y, sample path_pixel gives each slot; r06: the per-lane 32-bit divisions and
+    // state loads were the window scan's 12 % of k_camera's wave time, scripts/latency_roof.py)
+    while (sc.window<false>(P.ctl + WF_CTL_EXT, P.chunk, shard_size, P.state, nullptr, P.ctl + WF_CTL_CLOSED_EXT)) {
+        const int jw = __builtin_amdgcn_readfirstlane(sc.win_next);
+        sc.win_next += 64;
+        const int j = jw + lane;
         int x = 0, y = 0;
         int64_t smp = 0;
+        path_pixel(P, P.path_base + jw, x, y, smp);  // the window's first slot: its tile's corner
+        x += lane & 7;
+        y += lane >> 3;
         // edge-tile padding starts no path
-        const bool act = sj == WF_FREE && j < P.total && path_pixel(P, P.path_base + j, x, y, smp);
+        const bool act = j < P.total && x < P.width && y < P.height;
         if (!__any(act)) continue;
         CAM_MARK(t_scan);
         DV o = dv(0, 0, 0), d = dv(0, 0, 1);

@@ -37,7 +37,9 @@ print(json.dumps({"mrays": [r[0] for r in res], "ms": [r[1] for r in res], "rest
 
 
 def main():
-    libs = sorted(glob.glob(os.path.join(ROOT, "build_variants", "*.so")))
+    # MFX_AB_DIR: the directory of candidates (default build_variants/; build_ab/ keeps A/B builds apart
+    # from the diagnostic and experiment builds)
+    libs = sorted(glob.glob(os.path.join(ROOT, os.environ.get("MFX_AB_DIR", "build_variants"), "*.so")))
     scene = sys.argv[1] if len(sys.argv) > 1 else os.path.join(ROOT, "scenes", "spot.xml")
     rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 2
     spp = int(sys.argv[3]) if len(sys.argv) > 3 else 64

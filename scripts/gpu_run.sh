@@ -65,7 +65,7 @@ for step in "$@"; do
       IFS=, read -ra SC <<< "$a3"
       for sc in "${SC[@]}"; do
         echo "== $sc" >> $O/ab.txt
-        timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
+        MFX_AB_DIR=${MFX_AB_DIR:-build_ab} timeout -k 10 900 python3 scripts/ab_variants.py scenes/$sc $a1 $a2 >> $O/ab.txt 2>&1
       done
       grep -E "==|SUMMARY" $O/ab.txt ;;
     rehearse)

@@ -1,7 +1,8 @@
 """Multi-device contexts through the C ABI (mfx_options.devices).
 
 One context drives a device list from one process by an image partition: device g of G traces the
-film's 8-pixel tile rows r % G == g (every sample) on its own stream, so every per-pixel operation
+film's 8-pixel tile rows of band g of G (serpentine: one of each G consecutive tile rows; every
+sample) on its own stream, so every per-pixel operation
 runs on one device in the one-device order and every output is the one-device context's, bit for
 bit. FP64 buffers (mfx_sample's accumulator, mfx_film_mean's film) merge on devices[0]:
 - a list of distinct devices with RCCL (a communicator the library creates with ncclCommInitAll);
@@ -34,7 +35,7 @@ def test_single_device_list_is_bit_identical(gpu):
 
 @pytest.mark.parametrize("G", [2, 3])
 def test_repeated_device_list_partitions_rows_exactly(gpu, oracle, G):
-    """devices=[0]*G: device g traces tile rows g mod G; after the merge the primary's accumulator is
+    """devices=[0]*G: device g traces the tile rows of band g; after the merge the primary's accumulator is
     the one-device context's bit for bit, and so are the Sample image and the ray counters; the
     image matches the oracle. cube_cornell at 48x27: 4 tile rows, the last one partial."""
     from mafrixraytracing_amd.native import NativeContext
@@ -61,9 +62,10 @@ def test_repeated_device_list_partitions_rows_exactly(gpu, oracle, G):
 @pytest.mark.parametrize("P", [2, 3])
 def test_row_partition_ranks_merge_exactly(gpu, P):
     """MFX_F_ROW_PARTITION (the multi-process image partition): P one-device contexts, rank p traces
-    every sample of tile rows p mod P; each rank's accumulator is +0.0 outside its rows, and the sum
+    every sample of the tile rows of band p (distributed.tile_row_owner); each rank's accumulator is +0.0 outside its rows, and the sum
     over the ranks is the whole-film context's accumulator bit for bit (so is the ray total)."""
     from mafrixraytracing_amd.abi import MFX_F_ROW_PARTITION
+    from mafrixraytracing_amd.distributed import tile_row_owner
     from mafrixraytracing_amd.native import NativeContext
     w, h = 50, 29  # 4 tile rows, the last one partial; 7 tile columns, the last one partial
     a = scene("spot", w, h)
@@ -80,7 +82,7 @@ def test_row_partition_ranks_merge_exactly(gpu, P):
             c.trace_accumulate(spp, 11)
             part = c.accum_read_mean(1.0)
             rays += c.ray_counts()[:4]
-        own = np.tile(rows % P == p, w)  # x-major pixels: pixel = x * h + y
+        own = np.tile(tile_row_owner(rows, P) == p, w)  # x-major pixels: pixel = x * h + y
         assert not np.any(part[~own, :3]), p
         assert np.array_equal(part[own], want[own]), p
         total[:, :3] += part[:, :3]

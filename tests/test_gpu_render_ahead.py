@@ -133,7 +133,7 @@ def test_render_ahead_option_validated(gpu):
 @pytest.mark.parametrize("name,w,h,K", [("spot", 67, 37, 4), ("cube_cornell", 48, 27, 5)])
 def test_render_ahead_on_a_device_list(gpu, devices, name, w, h, K):
     """Scene(state, devices) — the F# binding's device-list context — serving Scene.Render from
-    batches on every device (image partition: device g traces tile rows g mod G of each batch and
+    batches on every device (image partition: device g traces the tile rows of band g of G of each batch and
     copies its rows of each frame). 14 calls with an spp = 2 call, a film read mid-batch, a reset and
     an mfx_sample call in between: every RGBA8 frame, the Sample image, the film and the rays equal
     the one-device context without render-ahead, bit for bit. (37 rows: 5 tile rows, the last one
