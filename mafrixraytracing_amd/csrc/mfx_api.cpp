@@ -212,6 +212,7 @@ struct mfx_ctx {
     int64_t dfilm_n = 0;
     unsigned long long* d_counters_aux = nullptr;  // ray counters of a film-only re-trace (not reported)
     hipEvent_t aux_ev0 = nullptr, aux_ev1 = nullptr;
+    hipStream_t sample_copy2 = nullptr;  // mfx_sample's banded readback: a second copy stream (MFX_SAMPLE_COPY_STREAMS=2)
     hipStream_t copy_stream = nullptr;  // frame copies to the host (overlap the background trace); created
                                         // at the first render-ahead call, so a batch-only context holds one
                                         // stream (one of the process's GPU_MAX_HW_QUEUES hardware queues)
@@ -288,6 +289,7 @@ static void free_ctx(mfx_ctx* c) {
         if (b) (void)hipFree(b);
     ahead_free(c);
     if (c->copy_stream) (void)hipStreamDestroy(c->copy_stream);
+    if (c->sample_copy2) (void)hipStreamDestroy(c->sample_copy2);
     if (c->h_counters) (void)hipHostFree(c->h_counters);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     for (hipEvent_t e : c->stage_ev)
@@ -1729,6 +1731,9 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     int rc = stage_events(c);
     if (rc) return rc;
     if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    int ncs = 1;  // MFX_SAMPLE_COPY_STREAMS=2: bands alternate over two copy streams (A/B knob)
+    if (const char* e = getenv("MFX_SAMPLE_COPY_STREAMS")) ncs = atoi(e) == 2 ? 2 : 1;
+    if (ncs == 2 && !c->sample_copy2) HIPCHECK(hipStreamCreateWithFlags(&c->sample_copy2, hipStreamNonBlocking));
     size_t off[kStageChunks] = {0}, len[kStageChunks] = {0};
     ResolveSplit S;
     S.nbands = nb;
@@ -1738,10 +1743,11 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
         len[k] = (size_t)(p1 - p0) * 4 * sizeof(double);
         HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, c->d_frame, c->stream, p0, p1));
         HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
-        HIPCHECK(hipStreamWaitEvent(c->copy_stream, c->band_ev[k], 0));
+        hipStream_t cs = (ncs == 2 && (k & 1)) ? c->sample_copy2 : c->copy_stream;
+        HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
         if (len[k]) HIPCHECK(hipMemcpyAsync(c->h_stage + off[k], (const uint8_t*)c->d_frame + off[k], len[k],
-                                            hipMemcpyDeviceToHost, c->copy_stream));
-        HIPCHECK(hipEventRecord(c->stage_ev[k], c->copy_stream));
+                                            hipMemcpyDeviceToHost, cs));
+        HIPCHECK(hipEventRecord(c->stage_ev[k], cs));
         return MFX_OK;
     };
     c->rep_valid = false;

@@ -23,9 +23,16 @@ def run():
     frame = np.empty((a.width * a.height, 4))
     out = {}
     with NativeContext(a, seed=DEFAULT_SEED) as ctx:
-        for mode in ("banded", "unbanded"):
-            if mode == "unbanded":
-                os.environ["MFX_SAMPLE_BANDS"] = "0"
+        modes = {"banded": {}, "unbanded": {"MFX_SAMPLE_BANDS": "0"}}
+        for b in (2, 4, 8):
+            for cs in (1, 2):
+                modes[f"bands{b}_streams{cs}"] = {"MFX_SAMPLE_BANDS": str(b), "MFX_SAMPLE_COPY_STREAMS": str(cs)}
+        if os.environ.get("SAMPLE_TRACE_SWEEP") != "1":
+            modes = {k: modes[k] for k in ("banded", "unbanded")}
+        for mode, env in modes.items():
+            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
             for _ in range(2):
                 ctx.sample(64, out=frame)
             time.sleep(0.1)
