@@ -138,7 +138,7 @@ _dp = _P(C.c_double)
 _ip = _P(C.c_int32)
 
 
-def _bind(lib):
+def _bind(lib, strict: bool = True):
     sig = {
         "mfx_create": (C.c_int, [_P(MfxSceneDesc), _P(MfxOptions), _P(C.c_void_p)]),
         "mfx_create_instanced": (C.c_int, [_P(MfxSceneDesc), _P(MfxInstance), C.c_int32, _P(MfxOptions),
@@ -179,6 +179,8 @@ def _bind(lib):
         "mfx_device_count": (C.c_int, []),
     }
     for name, (res, args) in sig.items():
+        if not strict and not hasattr(lib, name):  # (an older build under A/B: scripts only)
+            continue
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
@@ -196,15 +198,16 @@ EXPORTED_SYMBOLS = [
 _lib = None
 
 
-def load_library(path: str | None = None):
-    """Load libmafrix_rt.so (the HIP build). Raises if it is missing — no fallback exists."""
+def load_library(path: str | None = None, strict: bool = True):
+    """Load libmafrix_rt.so (the HIP build). Raises if it is missing — no fallback exists.
+    strict=False (A/B scripts timing an older build) binds only the entry points it exports."""
     global _lib
     if _lib is not None and path is None:
         return _lib
     p = path or LIB_PATH
     if not os.path.exists(p):
         raise RuntimeError(f"mafrix_rt native library not built: {p} (run __graft_entry__.build())")
-    lib = _bind(C.CDLL(p, mode=C.RTLD_GLOBAL))
+    lib = _bind(C.CDLL(p, mode=C.RTLD_GLOBAL), strict)
     if path is None:
         _lib = lib
     return lib
