@@ -1731,8 +1731,13 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     int rc = stage_events(c);
     if (rc) return rc;
     if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    int ncs = 1;  // MFX_SAMPLE_COPY_STREAMS=2: bands alternate over two copy streams (A/B knob)
+    int ncs = 2;  // MFX_SAMPLE_COPY_STREAMS=1: every band on one copy stream (A/B knob)
     if (const char* e = getenv("MFX_SAMPLE_COPY_STREAMS")) ncs = atoi(e) == 2 ? 2 : 1;
+    // MFX_SAMPLE_ZEROCOPY=1 (A/B knob): each band's mean kernel runs on a copy stream and writes the
+    // frame straight into the page-locked staging buffer across the fabric (no DMA)
+    const bool zc = getenv("MFX_SAMPLE_ZEROCOPY") && atoi(getenv("MFX_SAMPLE_ZEROCOPY")) != 0;
+    void* stage_dev = nullptr;  // the staging buffer's device address (zero-copy)
+    if (zc) HIPCHECK(hipHostGetDevicePointer(&stage_dev, c->h_stage, 0));
     if (ncs == 2 && !c->sample_copy2) HIPCHECK(hipStreamCreateWithFlags(&c->sample_copy2, hipStreamNonBlocking));
     size_t off[kStageChunks] = {0}, len[kStageChunks] = {0};
     ResolveSplit S;
@@ -1741,12 +1746,18 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
         const int64_t p0 = (int64_t)tx0 * 8 * H, p1 = (int64_t)std::min(W, (tx0 + ntx) * 8) * H;
         off[k] = (size_t)p0 * 4 * sizeof(double);
         len[k] = (size_t)(p1 - p0) * 4 * sizeof(double);
-        HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, c->d_frame, c->stream, p0, p1));
-        HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
         hipStream_t cs = (ncs == 2 && (k & 1)) ? c->sample_copy2 : c->copy_stream;
-        HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
-        if (len[k]) HIPCHECK(hipMemcpyAsync(c->h_stage + off[k], (const uint8_t*)c->d_frame + off[k], len[k],
-                                            hipMemcpyDeviceToHost, cs));
+        if (zc) {
+            HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
+            HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
+            HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, (double*)stage_dev, cs, p0, p1));
+        } else {
+            HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, c->d_frame, c->stream, p0, p1));
+            HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
+            HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
+            if (len[k]) HIPCHECK(hipMemcpyAsync(c->h_stage + off[k], (const uint8_t*)c->d_frame + off[k], len[k],
+                                                hipMemcpyDeviceToHost, cs));
+        }
         HIPCHECK(hipEventRecord(c->stage_ev[k], cs));
         return MFX_OK;
     };

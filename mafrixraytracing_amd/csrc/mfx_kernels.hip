@@ -423,10 +423,11 @@ __global__ void mean_kernel(const double* __restrict__ accum, int64_t npix, doub
                             int64_t p0, int64_t p1) {
     const int64_t q = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (q >= p1) return;
-    out[4 * q + 0] = accum[q] / n;
-    out[4 * q + 1] = accum[npix + q] / n;
-    out[4 * q + 2] = accum[2 * npix + q] / n;
-    out[4 * q + 3] = 1.0;
+    // two 16-B stores per pixel (a wave writes 2 KB in order: whole lines, also when `out` is
+    // page-locked host memory written across the fabric, mfx_sample's zero-copy readback)
+    double2* o = (double2*)out + 2 * q;
+    o[0] = make_double2(accum[q] / n, accum[npix + q] / n);
+    o[1] = make_double2(accum[2 * npix + q] / n, 1.0);
 }
 
 

@@ -24,13 +24,15 @@ def run():
     out = {}
     with NativeContext(a, seed=DEFAULT_SEED) as ctx:
         modes = {"banded": {}, "unbanded": {"MFX_SAMPLE_BANDS": "0"}}
-        for b in (2, 4, 8):
+        for b in (4, 8):
             for cs in (1, 2):
                 modes[f"bands{b}_streams{cs}"] = {"MFX_SAMPLE_BANDS": str(b), "MFX_SAMPLE_COPY_STREAMS": str(cs)}
+                modes[f"bands{b}_streams{cs}_zerocopy"] = {"MFX_SAMPLE_BANDS": str(b), "MFX_SAMPLE_COPY_STREAMS": str(cs),
+                                                           "MFX_SAMPLE_ZEROCOPY": "1"}
         if os.environ.get("SAMPLE_TRACE_SWEEP") != "1":
             modes = {k: modes[k] for k in ("banded", "unbanded")}
         for mode, env in modes.items():
-            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS"):
+            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS", "MFX_SAMPLE_ZEROCOPY"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             for _ in range(2):

@@ -19,11 +19,15 @@ def test_banded_sample_equals_unbanded_and_oracle(gpu, oracle, monkeypatch, name
     a = scene(name, w, h)
     with NativeContext(a, seed=SEED) as c:
         banded = [c.sample(spp) for _ in range(2)]
+    monkeypatch.setenv("MFX_SAMPLE_ZEROCOPY", "1")  # the means written straight into page-locked memory
+    with NativeContext(a, seed=SEED) as c:
+        zero = [c.sample(spp) for _ in range(2)]
+    monkeypatch.delenv("MFX_SAMPLE_ZEROCOPY")
     monkeypatch.setenv("MFX_SAMPLE_BANDS", "0")
     with NativeContext(a, seed=SEED) as c:
         plain = [c.sample(spp) for _ in range(2)]
-    for b, p in zip(banded, plain):
-        assert np.array_equal(b, p)
+    for b, z, p in zip(banded, zero, plain):
+        assert np.array_equal(b, p) and np.array_equal(z, p)
     o = oracle.OracleScene(a)
     assert np.array_equal(banded[1], o.sample(spp, SEED, sample_base=spp))
 
