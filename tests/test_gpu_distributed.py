@@ -289,3 +289,36 @@ def test_bench_single_process_device_list_rehearsal(gpu):
     rl = _bench(ra + ["--single-process", "--gpus", "2"] + common, env=env)
     r1 = _bench(ra + common)
     assert rl["n_gpus"] == 2 and rl["rays_per_step"] == r1["rays_per_step"] > 0
+
+
+def test_bench_two_ranks_on_two_devices_over_rccl(gpu):
+    """the default multi-GPU exchange for real — bench.py under torch.distributed.run with
+    2 ranks on 2 distinct devices, RowGather over RCCL (nccl) — merges to the 1-GPU frame bit for bit
+    (the line's own merged_equals_1gpu check) on distinct devices. Needs 2 GPUs: skipped on the
+    one-GPU box (the 2-rank gloo rehearsal above runs the same code path there)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    common = ["--steps", "2", "--warmup", "1", "--spp", "2", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    env = {k: v for k, v in os.environ.items() if k not in ("MFX_BENCH_DEVICE", "MFX_BENCH_BACKEND")}
+    line = _bench(common, env=env, torchrun=2)
+    topo = line["topology"]
+    assert topo["backend"] == "nccl" and topo["rccl_world"] == 2 and topo["distinct_devices"] is True
+    assert line["merged_equals_1gpu"] is True and line["verify"]["exact_expected"] is True
+    one = _bench(common)
+    assert line["rays_per_step"] == one["rays_per_step"] > 0
+
+
+def test_bench_single_process_two_devices(gpu):
+    """The library's own multi-device path on 2 distinct GPUs (ncclCommInitAll: 2 communicators, RCCL
+    reduce) merges to the 1-GPU frame bit for bit. Needs 2 GPUs (the [0, 0] rehearsal runs on one)."""
+    import torch
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs 2 GPUs")
+    common = ["--steps", "2", "--warmup", "1", "--spp", "4", "--no-cpu-baseline", "--no-stats", "--no-render-api"]
+    env = {k: v for k, v in os.environ.items() if k != "MFX_BENCH_DEVICE"}
+    line = _bench(common + ["--single-process", "--gpus", "2"], env=env)
+    topo = line["topology"]
+    assert topo["single_process_devices"] == [0, 1] and topo["communicators"] == 2
+    assert topo["library_context"]["merge"] == "rccl_reduce"
+    assert line["merged_equals_1gpu"] is True
