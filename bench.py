@@ -306,6 +306,8 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repea
     from mafrixraytracing_amd.native import NativeContext
     W, H = arrays.width, arrays.height
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda")
+    if os.environ.get("MFX_SHARE_TORCH_FIRST") == "1":  # (scripts/share_modes.py) torch's stream pools first
+        torch.cuda.Stream()
 
     def timed(fn, reps=20):
         fn()
