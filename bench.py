@@ -273,9 +273,13 @@ def sample_api(arrays, seed, spp, calls=5, flags=0):
 SHARE_PROCESSES = 3  # fresh processes strong_share runs in (bench.py --strong-share-child)
 
 
-def combine_shares(runs):
-    """strong_share from several fresh processes: per N the process with the median slowest rank
-    (its whole entry), plus every process's slowest rank and predictions and their spread."""
+def combine_shares(runs, value_1gpu, ms_1gpu):
+    """strong_share from several fresh processes (raw: no predictions yet): per N the process with the
+    median slowest rank (its whole entry), plus every process's slowest rank and predictions and their
+    spread, all against the N = 1 line's rate and step time."""
+    for r in runs:
+        for n, e in r["shares"].items():
+            share_efficiency(e, int(n), value_1gpu, ms_1gpu)
     out = {"shares": {}, "processes": len(runs), "partition": runs[0]["partition"],
            "note": runs[0]["note"] + f"; measured in {len(runs)} fresh processes: per N the median process's entry, "
                                      "`processes_slowest_rank_ms` / `processes_predicted_efficiency` from each and "
@@ -292,7 +296,23 @@ def combine_shares(runs):
     return out
 
 
-def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repeats=2):
+def share_efficiency(e, n, value_1gpu, ms_1gpu):
+    """The predictions of one N's share entry against the full frame's rate and time (the N = 1 line):
+    predicted_efficiency = (t_1GPU / N) / (t_slowest_rank + the exchange), the exchange not overlapped;
+    _pipelined: the exchange runs beside the next frame's trace (measured: it completes within that
+    trace and the trace keeps its time), so a step is the slowest rank's trace slowed by the measured
+    factor."""
+    t_rank, t_ex, ov = e["slowest_rank_ms"], e["exchange_ms"], e["overlap_measured"]
+    e["vs_full_step_rate"] = round(e["job_rays_per_step"] / n / (t_rank / 1e3) / 1e6 / value_1gpu, 4)
+    e["predicted_efficiency"] = round((ms_1gpu / n) / (t_rank + t_ex), 4)
+    e["predicted_efficiency_per_repeat"] = [round((ms_1gpu / n) / (t + t_ex), 4) for t in e["per_repeat_slowest_ms"]]
+    e["predicted_efficiency_pipelined"] = round(
+        (ms_1gpu / n) / (t_rank * max(1.0, ov["trace_ms_beside_it"] / ov["trace_ms_alone"]) +
+                         (0.0 if ov["exchange_completion_ms"] < t_rank else t_ex)), 4)
+    return e
+
+
+def strong_share(arrays, seed, spp, value_1gpu=None, ms_1gpu=None, steps=8, flags=0, repeats=2):
     """Every rank's share of the strong-scaled job at N = 2, 4, 8 GPUs (the line's image partition),
     measured on this GPU: rank r traces all `spp` samples of the film's tile rows of band r of N
     (MFX_F_ROW_PARTITION). Each share is timed as a rank runs it (clear + trace + sync, the frame's
@@ -393,21 +413,17 @@ def strong_share(arrays, seed, spp, value_1gpu, ms_1gpu, steps=8, flags=0, repea
                        "rank_rays_rel": [round(r / (job_rays / n), 4) for r in rank_rays],
                        "slowest_rank_ms": round(t_rank, 3), "repeats": repeats,
                        "slowest_rank_repeats_ms": [round(t, 3) for t in slow],
+                       "per_repeat_slowest_ms": [round(t, 4) for t in per_rep_slowest],
                        "spread": round((max(slow) - min(slow)) / t_rank, 4),
-                       "predicted_efficiency_per_repeat": [round((ms_1gpu / n) / (t + t_ex), 4) for t in per_rep_slowest],
                        "imbalance": round(t_rank / (sum(rank_ms) / n), 4),
                        "mrays_per_s_per_gpu": round(job_rays / n / (t_rank / 1e3) / 1e6, 2),
-                       "vs_full_step_rate": round(job_rays / n / (t_rank / 1e3) / 1e6 / value_1gpu, 4),
+                       "job_rays_per_step": job_rays,
                        "gather_ms": {"pack": round(t_pack, 4), "transfer_modeled": round(t_xfer, 4),
                                      "unpack": round(t_unpack, 4)},
-                       "predicted_efficiency": round((ms_1gpu / n) / (t_rank + t_ex), 4),
-                       "overlap_measured": ov,
-                       # the exchange runs beside the next frame's trace (measured: it completes within
-                       # that trace and the trace keeps its time), so a pipelined step is the slowest
-                       # rank's trace, slowed by the measured factor
-                       "predicted_efficiency_pipelined": round(
-                           (ms_1gpu / n) / (t_rank * max(1.0, ov["trace_ms_beside_it"] / ov["trace_ms_alone"]) +
-                                            (0.0 if ov["exchange_completion_ms"] < t_rank else t_ex)), 4)}
+                       "exchange_ms": t_ex,
+                       "overlap_measured": ov}
+        if value_1gpu:
+            share_efficiency(out[str(n)], n, value_1gpu, ms_1gpu)
     return {"shares": out, "partition": "image: serpentine tile-row band r of N per rank (MFX_F_ROW_PARTITION), "
                                         "RowGather to rank 0",
             "note": "every rank's share of --scaling strong at N GPUs, measured on one GPU one after another, in a fresh "
@@ -522,12 +538,30 @@ def main():
     if args.strong_share_child is not None:  # a fresh process, as a rank's own process runs its share
         from mafrixraytracing_amd.native import DEFAULT_SEED
         from mafrixraytracing_amd.scene_io import load_scene_file
-        share = strong_share(load_scene_file(args.scene), DEFAULT_SEED, args.spp, args.strong_share_child[0],
-                             args.strong_share_child[1], steps=args.steps, flags=CONFIG_FLAGS.get(args.config, 0))
+        share = strong_share(load_scene_file(args.scene), DEFAULT_SEED, args.spp, args.strong_share_child[0] or None,
+                             args.strong_share_child[1] or None, steps=args.steps, flags=CONFIG_FLAGS.get(args.config, 0))
         print(json.dumps(share), file=json_out, flush=True)
         return
     if args.gpus > 1 and not args.single_process and "RANK" not in os.environ:
         sys.exit(relaunch_distributed(args))
+    # strong_share: every rank's share of the N-GPU job timed on this GPU, each rank over the line's own
+    # step count (its frames-in-flight pipeline fills and drains between the barriers, as an N-GPU
+    # run's steps do), in SHARE_PROCESSES fresh processes started before this one touches the GPU, as a
+    # rank's own process runs it alone on its GPU: started later, beside this process's contexts, a
+    # third of the children ran every share 8 % slower (r06f: 4.82 / 4.46 / 4.82 ms at N = 8), started
+    # from a process with no GPU context all nine agreed within 0.4 % (r06g, scripts/share_modes.py).
+    # Never from a profiled process (the profiler initialised the GPU before this one started).
+    share_runs = []
+    if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.gpus == 1 and args.api == "batch" and not args.no_render_api
+            and not args.megakernel and not _under_profiler()):
+        cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--scene", args.scene,
+               "--steps", str(args.steps), "--strong-share-child", "0", "0"] + \
+              (["--spp", str(args.spp)] if args.spp is not None else [])
+        for _ in range(SHARE_PROCESSES):
+            pc = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+            if pc.returncode != 0:
+                raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
+            share_runs.append(json.loads(pc.stdout.strip().splitlines()[-1]))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal of the N-rank job on a one-GPU box (tests/test_gpu_distributed.py): every rank on
@@ -998,28 +1032,9 @@ def main():
             rapi["without_render_ahead"] = plain
             sapi = sample_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
             sapi["vs_batch"] = round(sapi["value"] / value, 4)
-            # each rank's share timed over the line's own step count (its frames-in-flight pipeline
-            # fills and drains between the barriers, as an N-GPU run of these steps does), in a fresh
-            # process as a rank's own process runs it: this process's earlier contexts and streams
-            # (render_api, sample_api) slowed the 1/8 share by ~8 % (profiles/r05/r05zm_*, r05zo_*)
-            # (never from a profiled process: the profiler initialised the GPU before this one started)
-            cmd = None if _under_profiler() else \
-                [sys.executable, os.path.abspath(__file__), "--config", args.config, "--spp", str(args.spp),
-                 "--scene", args.scene, "--steps", str(args.steps),
-                 "--strong-share-child", repr(float(value)), repr(float(elapsed / args.steps * 1e3))]
-            if cmd is None:
-                share = {"skipped": "under a profiler"}
-            else:
-                # SHARE_PROCESSES fresh processes: one process's shares sat 6 % apart from another's on
-                # the same box (r06b / r06d) while repeats inside one process agreed within 0.4 %, so the
-                # line carries the median process per N and the spread over processes
-                runs = []
-                for _ in range(SHARE_PROCESSES):
-                    pc = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
-                    if pc.returncode != 0:
-                        raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
-                    runs.append(json.loads(pc.stdout.strip().splitlines()[-1]))
-                share = combine_shares(runs)
+            # the shares were measured before this process touched the GPU (share_runs, main's start)
+            share = combine_shares(share_runs, value, elapsed / args.steps * 1e3) if share_runs else \
+                {"skipped": "under a profiler"}
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
