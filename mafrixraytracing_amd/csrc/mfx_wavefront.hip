@@ -1330,10 +1330,20 @@ static void launch_shadow_q(const WfParams& P, int grid, bool stats, hipStream_t
     else
         hipLaunchKernelGGL((k_shadow<false, SPILL, WAVES, SK, Q>), dim3(grid), dim3(256), lds, st, P);
 }
+// MFX_SHADOW_Q_WAVES=3 (an A/B knob, VERDICT r05 Next #7): the queue instances of a 4-wave k_shadow
+// run the 3-wave build instead (no scratch spill; 3 of the grid's 4 blocks per CU)
+static int shadow_q_waves() {
+    static const int w = getenv("MFX_SHADOW_Q_WAVES") ? atoi(getenv("MFX_SHADOW_Q_WAVES")) : 0;
+    return w;
+}
 template <bool SPILL, int WAVES, int SK>
 static void launch_shadow(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
-    if (P.qslot || P.ncount) launch_shadow_q<SPILL, WAVES, SK, true>(P, grid, stats, st, lds);
-    else launch_shadow_q<SPILL, WAVES, SK, false>(P, grid, stats, st, lds);
+    if (P.qslot || P.ncount) {
+        if (WAVES == 4 && shadow_q_waves() == 3) launch_shadow_q<SPILL, 3, SK, true>(P, grid / 4 * 3, stats, st, lds);
+        else launch_shadow_q<SPILL, WAVES, SK, true>(P, grid, stats, st, lds);
+    } else {
+        launch_shadow_q<SPILL, WAVES, SK, false>(P, grid, stats, st, lds);
+    }
 }
 template <int SK>
 static void launch_shadow_sk(const WfParams& P, int grid, bool stats, hipStream_t st, size_t lds) {
