@@ -91,7 +91,9 @@ def kernel(name, stamp, prod, waves, simds, iters):
         fi = wci / (nw * rs[key] / 1e3)
         per.append({"iteration": rs["iter"] - 1, "node_steps_per_wave": round(rs["node_iters"] / nw, 1),
                     "L_step_cycles": round(li, 1), "lat_share_stamp_build": round(rs["lat"] / wci, 4),
-                    "node_phase_share": round(rs["node"] / wci, 4), "ms_shipped": rp[key], "ms_stamp_build": rs[key],
+                    "node_phase_share": round(rs["node"] / wci, 4),
+                    "phase_shares": {k: round(rs[k] / wci, 4) for k in ("fetch", "scan", "shade", "node", "leaf", "fin")},
+                    "ms_shipped": rp[key], "ms_stamp_build": rs[key],
                     "frac": round(rs["node_iters"] / nw / (rp[key] / 1e3) / (fi / li), 4)})
     return {"bound": "latency", "achieved": round(ach / 1e6, 4), "peak": round(peak / 1e6, 4),
             "unit": "M node steps/s per resident wave", "frac": round(ach / peak, 4),
