@@ -5,7 +5,6 @@ image (the rows: bit for bit). The ranks run `native_partitioned_render` — the
 multi-process path runs — over a stand-in context whose trace is the CPU oracle (the container has
 no GPU), so the clear / trace / sync / exchange sequence tested is the bench's."""
 import os
-import socket
 import sys
 
 import numpy as np
@@ -14,14 +13,6 @@ import pytest
 from conftest import ROOT, SEED
 
 W, H, SPP = 20, 12, 5
-
-
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
 
 
 class OracleContext:
@@ -65,7 +56,7 @@ class OracleContext:
         self.calls.append("trace")
 
 
-def _worker(rank, world, port, outdir, rows):
+def _worker(rank, world, init, outdir, rows):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import torch
@@ -75,7 +66,7 @@ def _worker(rank, world, port, outdir, rows):
     from conftest import scene
     from mafrixraytracing_amd.distributed import RowGather, native_partitioned_render
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group("gloo", init_method=init, rank=rank, world_size=world)
     a = scene("spot", W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64)
     ctx = OracleContext(pyoracle.OracleScene(a), acc, rank, world, rows=rows)
@@ -96,8 +87,8 @@ def test_ranks_merge_to_the_single_rank_image(oracle, tmp_path, world, rows):
     ranks one rank owns none) — rank 0's accumulator is the single-rank image bit for bit. Else the
     sample partition with a sum-reduce, within FP64 summation order."""
     import torch.multiprocessing as mp
-    port = _free_port()
-    mp.start_processes(_worker, args=(world, port, str(tmp_path), rows), nprocs=world, join=True, start_method="spawn")
+    init = "file://" + str(tmp_path / "pg_init")  # file rendezvous: no port to race for
+    mp.start_processes(_worker, args=(world, init, str(tmp_path), rows), nprocs=world, join=True, start_method="spawn")
     from conftest import scene
     o = oracle.OracleScene(scene("spot", W, H))
     npix = W * H

@@ -29,11 +29,22 @@ W, H = 64, 36
 
 
 def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    p = s.getsockname()[1]
-    s.close()
-    return p
+    """A port free now, outside the kernel's ephemeral range (32768-60999 by default): an ephemeral
+    port released by this probe can be taken by any outgoing connection (RCCL / gloo bootstrap
+    sockets) before the rendezvous binds it (r06h: EADDRINUSE)."""
+    import random
+    rng = random.Random()
+    for _ in range(200):
+        p = rng.randrange(20000, 30000)
+        s = socket.socket()
+        try:
+            s.bind(("127.0.0.1", p))
+            return p
+        except OSError:
+            continue
+        finally:
+            s.close()
+    raise RuntimeError("no free port in 20000-30000")
 
 
 def _plain_accumulators(name, frames, part_index=0, part_count=1):
@@ -51,7 +62,7 @@ def _plain_accumulators(name, frames, part_index=0, part_count=1):
     return out
 
 
-def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False,
+def _rank_worker(rank, world, init, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False,
                  nctx=1):
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -64,7 +75,7 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
     from mafrixraytracing_amd.native import NativeContext
 
     torch.cuda.set_device(0)
-    dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    dist.init_process_group(backend, init_method=init, rank=rank, world_size=world)
     a = scene(name, W, H)
     acc = torch.zeros(3 * W * H, dtype=torch.float64, device="cuda:0")
     gather = rows and backend == "nccl"  # (gloo has no CUDA gather: rows merge by all_reduce there)
@@ -101,7 +112,9 @@ def _rank_worker(rank, world, port, backend, name, frames, outdir, all_ranks, pi
 
 def _spawn(world, backend, name, frames, outdir, all_ranks, pipelined=False, rows=False, nctx=1):
     import torch.multiprocessing as mp
-    mp.start_processes(_rank_worker, args=(world, _free_port(), backend, name, frames, str(outdir), all_ranks,
+    # file rendezvous (no port to race for)
+    init = "file://" + os.path.join(str(outdir), "pg_init")
+    mp.start_processes(_rank_worker, args=(world, init, backend, name, frames, str(outdir), all_ranks,
                                            pipelined, rows, nctx),
                        nprocs=world, join=True, start_method="spawn")
     return np.load(os.path.join(outdir, "frames.npy"))
