@@ -1,0 +1,40 @@
+#!/usr/bin/env python3
+"""mfx_sample's rate in bench.py's process state (VERDICT r05 Next #6): the line's context traces its
+timed steps, render_api runs, then bench.sample_api, per readback setting (MFX_SAMPLE_BANDS,
+MFX_SAMPLE_COPY_STREAMS read per call), interleaved over two rounds. Prints one JSON line per run."""
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    import bench
+    from mafrixraytracing_amd.native import DEFAULT_RENDER_AHEAD, DEFAULT_SEED, NativeContext
+    from mafrixraytracing_amd.scene_io import load_scene_file
+    a = load_scene_file(bench.SPOT_SCENE)
+    ctx = NativeContext(a, seed=DEFAULT_SEED)
+    for k in range(25):
+        ctx.accum_clear()
+        ctx.trace_accumulate(64, k * 64)
+    ctx.sync()
+    bench.render_api(a, DEFAULT_SEED, 2 * DEFAULT_RENDER_AHEAD, render_ahead=DEFAULT_RENDER_AHEAD)
+    settings = [("bands8_streams1", {"MFX_SAMPLE_BANDS": "8", "MFX_SAMPLE_COPY_STREAMS": "1"}),
+                ("bands8_streams2", {"MFX_SAMPLE_BANDS": "8", "MFX_SAMPLE_COPY_STREAMS": "2"}),
+                ("bands4_streams1", {"MFX_SAMPLE_BANDS": "4", "MFX_SAMPLE_COPY_STREAMS": "1"}),
+                ("unbanded", {"MFX_SAMPLE_BANDS": "0"})]
+    for rd in range(2):
+        for name, env in settings:
+            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS"):
+                os.environ.pop(k, None)
+            os.environ.update(env)
+            r = bench.sample_api(a, DEFAULT_SEED, 64)
+            print(json.dumps({"round": rd, "setting": name, "ms_per_call": r["ms_per_call"],
+                              "min": r["ms_per_call_min"], "median": r["ms_per_call_median"]}), flush=True)
+    ctx.close()
+
+
+if __name__ == "__main__":
+    main()
