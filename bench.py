@@ -255,17 +255,19 @@ def sample_api(arrays, seed, spp, calls=5, flags=0):
     with NativeContext(arrays, seed=seed, flags=flags) as ctx:
         for _ in range(2):  # warmup (pool, staging and copy streams, first touch of the frame)
             ctx.sample(spp, out=frame)
-        wall, rays = [], 0.0
+        wall, rays, dev = [], 0.0, []
         for _ in range(calls):
             t0 = time.perf_counter()
             ctx.sample(spp, out=frame)
             wall.append(time.perf_counter() - t0)
             c = ctx.ray_counts()
             rays += c[0] + c[1] + c[2]
+            dev.append(ctx.last_trace_ms())  # the call's kernels (HIP events), readback excluded
     tot = sum(wall)
     return {"value": round(rays / tot / 1e6, 2), "unit": "Mrays/s", "calls": calls, "spp": spp,
             "ms_per_call": round(tot / calls * 1e3, 3), "ms_per_call_min": round(min(wall) * 1e3, 3),
             "ms_per_call_median": round(sorted(wall)[calls // 2] * 1e3, 3),
+            "trace_device_ms_per_call": round(sum(dev) / calls, 3),
             "includes": "per call: mfx_sample(ctx, spp, frame) = trace, mean, FP64 RGBA x-major readback "
                         "to pageable host memory (banded: overlapped with the last resolve), synchronize"}
 

@@ -1721,7 +1721,10 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
 // its own thread's, and the mean is the same division. MFX_SAMPLE_BANDS=0: the unbanded path.
 // Returns 1 (nothing done) when the call is not for it (a device list, no staging memory).
 static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
-    int nb = kStageChunks;
+    // 4 bands, one copy stream: in the bench process's state (r06i, scripts/sample_in_bench_probe.py)
+    // 4 x 1 took 32.8-33.0 ms per C2 call, 8 x 1 33.0-33.2, 8 bands over two copy streams 33.7-33.9 and
+    // the unbanded path 33.7 (a lone process: 8 x 1 32.1, unbanded 32.7, r06b)
+    int nb = 4;
     if (const char* e = getenv("MFX_SAMPLE_BANDS")) nb = std::min(kStageChunks, atoi(e));
     const int W = c->host.width, H = c->host.height;
     nb = std::min(nb, (W + 7) / 8);
@@ -1731,7 +1734,7 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     int rc = stage_events(c);
     if (rc) return rc;
     if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
-    int ncs = 2;  // MFX_SAMPLE_COPY_STREAMS=1: every band on one copy stream (A/B knob)
+    int ncs = 1;  // MFX_SAMPLE_COPY_STREAMS=2: bands alternate over two copy streams (A/B knob; slower, r06i)
     if (const char* e = getenv("MFX_SAMPLE_COPY_STREAMS")) ncs = atoi(e) == 2 ? 2 : 1;
     // MFX_SAMPLE_ZEROCOPY=1 (A/B knob): each band's mean kernel runs on a copy stream and writes the
     // frame straight into the page-locked staging buffer across the fabric (no DMA)
