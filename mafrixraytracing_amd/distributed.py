@@ -198,7 +198,9 @@ def frames_in_flight(width: int, height: int, spp: int, world: int, rows: bool =
     tr = (height + 7) // 8
     rows_per_rank = -(-tr // world) if rows else tr
     paths = ((width + 7) // 8) * rows_per_rank * 64 * spp
-    return 3 if paths <= (1 << 25) else 1
+    import os
+    small = int(os.environ.get("MFX_FRAMES_IN_FLIGHT", "3"))  # (an A/B knob: scripts/share_modes.py)
+    return small if paths <= (1 << 25) else 1
 
 
 class PipelinedNativeRender:
