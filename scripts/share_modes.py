@@ -20,8 +20,8 @@ def main():
         settings = [("nif3", {"GPU_MAX_HW_QUEUES": "8"}), ("nif4", {"GPU_MAX_HW_QUEUES": "8", "MFX_FRAMES_IN_FLIGHT": "4"}),
                     ("nif2", {"GPU_MAX_HW_QUEUES": "8", "MFX_FRAMES_IN_FLIGHT": "2"})]
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--strong-share-child", "11400", "30.9"]
-    for name, env in settings:
-        for r in range(reps):
+    for r in range(reps):  # interleaved: setting after setting, round after round
+        for name, env in settings:
             p = subprocess.run(cmd, capture_output=True, text=True, timeout=600, env=dict(os.environ, **env))
             if p.returncode != 0:
                 print(name, "FAILED", p.stderr[-1500:], flush=True)
