@@ -23,6 +23,7 @@
 #   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
 #                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
 #   sampletrace          mfx_sample under rocprofv3 kernel + memory-copy trace (scripts/sample_trace.py)
+#   sharequeues:K        K strong-share children under a kernel trace: HW queue ids per rank (share_queues.py)
 #   py:SCRIPT[:ARGS]     scripts/SCRIPT.py ARGS (comma-separated) -> SCRIPT.json
 #   latroof:SCENE:SPP    latency roof of k_extend / k_shadow from the stamp builds build_variants/st1.so,
 #                        st2.so (scripts/latency_roof.py) -> latency_SCENE.json
@@ -137,6 +138,16 @@ for step in "$@"; do
          python3 $R/scripts/sample_trace.py > $D/run.json 2> $D/run.err)
       cat $D/run.json
       python3 scripts/sample_trace.py --timeline $D/trace > $D/timeline.txt; tail -40 $D/timeline.txt ;;
+    sharequeues)
+      # the strong-share child under a kernel trace, a1 times: which HW queues its contexts used
+      for i in $(seq 1 $a1); do
+        D=$R/$O/sharequeues/p$i
+        mkdir -p $D
+        (cd /tmp && export TMPDIR=/tmp &&
+         timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d $D/trace -o run -- \
+           python3 $R/bench.py --steps 20 --strong-share-child 0 0 > $D/run.json 2> $D/run.err)
+      done
+      python3 scripts/share_queues.py $O/sharequeues | tee $O/sharequeues.txt ;;
     py)
       # py:SCRIPT[:ARGS] -- scripts/SCRIPT.py with comma-separated ARGS -> SCRIPT.json / SCRIPT.err
       X=(); [ -n "$a2" ] && IFS=, read -ra X <<< "$a2"
