@@ -170,6 +170,7 @@ struct mfx_ctx {
     // (+11 % on C2 over 32 M slots). Capped at 2^28 slots (31 GB of the 288 GB) and at a quarter
     // of the free HBM.
     int64_t wf_pool_max = 1 << 28;
+    int64_t wf_pool_cap = 0;  // the generation cap a memory shortage left (0: none; wf_trace)
     unsigned long long* d_wfctl = nullptr;  // [WF_CTL_ALLOC] queue 0 counts, chunk heads, queue 1 counts
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
@@ -847,10 +848,20 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
     int64_t gen_max = 0;
     int32_t pool = 0;
     int rc = MFX_OK;
-    // the device short of memory (other contexts or processes on it): smaller generations for this
-    // call only, the same images (a generation only bounds how many paths are in flight); the next
-    // call tries the configured maximum again
-    int64_t cap = c->wf_pool_max;
+    // the device short of memory (other contexts or processes on it): smaller generations, the same
+    // images (a generation only bounds how many paths are in flight). The shrunk cap is kept, and a
+    // later call goes back to the configured maximum once the device has room for twice that pool
+    // (a one-off spike no longer shrinks a context for good; the margin keeps contexts of
+    // several processes sharing a device from growing back into each other's launches, r06j)
+    int64_t cap = c->wf_pool_cap > 0 ? c->wf_pool_cap : c->wf_pool_max;
+    if (cap < c->wf_pool_max) {
+        const int nv = c->host.max_depth + 1;
+        const double full = (double)std::min<int64_t>(total, c->wf_pool_max) *
+                            (WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4);
+        size_t mfree = 0, mtotal = 0;
+        if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && 2.0 * full < (double)(mfree + c->wf_pool_bytes))
+            cap = c->wf_pool_max;
+    }
     while (true) {
         gen_max = std::min<int64_t>(total, std::max<int64_t>(4096, cap / 4096 * 4096));
         pool = (int32_t)((gen_max + 4095) / 4096 * 4096);  // 64 shards of whole windows
@@ -859,6 +870,7 @@ static int wf_trace(mfx_ctx* c, int64_t ns, int64_t sample_base, const FrameMode
         cap = std::max<int64_t>(1 << 20, gen_max / 2);
     }
     if (rc) return rc;
+    c->wf_pool_cap = cap < c->wf_pool_max ? cap : 0;
     WfParams P = c->wf;
     fill_scene_params(c, P);
     P.ctl = c->d_wfctl - WF_CTL_Q0;
