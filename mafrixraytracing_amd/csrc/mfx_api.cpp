@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <mutex>
 #include <thread>
 #include <vector>
 #include <set>
@@ -226,6 +227,7 @@ struct mfx_ctx {
     double rep_counts[16] = {0};
     double rep_ms = 0.0;
     bool diag_iter = false;
+    bool pooled_stream = false;  // `stream` belongs to the process's pool (process_stream), not to this context
     bool iter_events = true;  // per-iteration HIP events around each launch (mfx_trace_timing's stage split)
 
     // ---- multi-device (primary context only) ----
@@ -301,7 +303,7 @@ static void free_ctx(mfx_ctx* c) {
         if (e) (void)hipEventDestroy(e);
     if (c->ev0) (void)hipEventDestroy(c->ev0);
     if (c->ev1) (void)hipEventDestroy(c->ev1);
-    if (c->stream) (void)hipStreamDestroy(c->stream);
+    if (c->stream && !c->pooled_stream) (void)hipStreamDestroy(c->stream);
     delete c;
 }
 
@@ -314,6 +316,37 @@ int mfx_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+}
+
+// MFX_STREAM_POOL=K: contexts take their stream from K streams per device that the process creates at
+// its first context and keeps, round robin, instead of creating (and at destruction releasing) one
+// each. The HIP runtime maps streams onto GPU_MAX_HW_QUEUES hardware queues as it creates them; a
+// context created after other streams came and went (torch's stream pools, earlier contexts) can land
+// on a queue another context of its frames in flight already uses, and their launches then serialize.
+// Streams created first, once, keep distinct queues for the process's life (r06k, scripts/share_queues.py).
+static int stream_pool_size() {
+    static const int k = getenv("MFX_STREAM_POOL") ? std::max(0, std::min(16, atoi(getenv("MFX_STREAM_POOL")))) : 0;
+    return k;
+}
+static hipError_t process_stream(int device, int k, hipStream_t* out) {
+    static std::mutex mu;
+    static std::vector<std::vector<hipStream_t>> pool;
+    static std::vector<unsigned> next;
+    std::lock_guard<std::mutex> lock(mu);
+    if ((int)pool.size() <= device) {
+        pool.resize(device + 1);
+        next.resize(device + 1, 0);
+    }
+    if (pool[device].empty()) {
+        for (int i = 0; i < k; ++i) {
+            hipStream_t s = nullptr;
+            const hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+            if (e != hipSuccess) return e;
+            pool[device].push_back(s);
+        }
+    }
+    *out = pool[device][next[device]++ % pool[device].size()];
+    return hipSuccess;
 }
 
 // Device resources of a context whose host scene, device, seed, flags and partition are set:
@@ -332,7 +365,12 @@ static int ctx_setup(mfx_ctx* c) {
         }                                                                                      \
     } while (0)
     CK(hipSetDevice(c->device));
-    CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    if (const int k = stream_pool_size()) {  // MFX_STREAM_POOL (see process_stream)
+        CK(process_stream(c->device, k, &c->stream));
+        c->pooled_stream = true;
+    } else {
+        CK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    }
     CK(hipHostMalloc((void**)&c->h_counters, WF_NCTR * WF_SHARDS * sizeof(unsigned long long), hipHostMallocDefault));
     CK(hipEventCreate(&c->ev0));
     CK(hipEventCreate(&c->ev1));
