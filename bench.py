@@ -275,6 +275,16 @@ def sample_api(arrays, seed, spp, calls=5, flags=0):
 SHARE_PROCESSES = 3  # fresh processes strong_share runs in (bench.py --strong-share-child)
 
 
+def _hip_stream():
+    """A non-blocking HIP stream on the current device, created through the HIP runtime directly."""
+    import ctypes as C
+    hip = C.CDLL("libamdhip64.so")
+    s = C.c_void_p()
+    if hip.hipStreamCreateWithFlags(C.byref(s), 1) != 0:  # hipStreamNonBlocking
+        raise RuntimeError("hipStreamCreateWithFlags failed")
+    return s.value
+
+
 def combine_shares(runs, value_1gpu, ms_1gpu):
     """strong_share from several fresh processes (raw: no predictions yet): per N the process with the
     median slowest rank (its whole entry), plus every process's slowest rank and predictions and their
@@ -349,7 +359,11 @@ def strong_share(arrays, seed, spp, value_1gpu=None, ms_1gpu=None, steps=8, flag
         """The exchange's pack + unpack enqueued on a second stream 1 ms into this rank's trace (the
         bench's pipelined frames): its completion time from its own start, and the trace's time
         beside it against alone (scripts/overlap_probe.py measures the same for other operations)."""
-        side = torch.cuda.Stream()
+        # a HIP stream of its own, not torch's: torch.cuda.Stream() creates torch's stream pools (dozens of
+        # streams), after which the HIP runtime maps the next contexts' streams onto shared hardware
+        # queues and a rank's frames in flight serialize (r06k, scripts/share_queues.py: two queues for
+        # three contexts, the 1/8 share 8 % slower)
+        side = torch.cuda.ExternalStream(_hip_stream())
         lat, tr, al = [], [], []
         for k in range(reps):
             ctx.trace_accumulate(spp, (k + 20) * spp)
