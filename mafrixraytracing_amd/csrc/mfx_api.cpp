@@ -8,10 +8,14 @@
 // the device list) sums the FP64 accumulators into the primary's, where film and post run. No
 // call falls back to a CPU path.
 #include <dlfcn.h>
+#include <sched.h>
+#include <sys/syscall.h>
+#include <unistd.h>
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <functional>
 #include <cstdlib>
@@ -172,6 +176,7 @@ struct mfx_ctx {
     // of the free HBM.
     int64_t wf_pool_max = 1 << 28;
     int64_t wf_pool_cap = 0;  // the generation cap a memory shortage left (0: none; wf_trace)
+    bool pool_fail_once = false;  // MFX_POOL_FAIL_ONCE=1 (tests): the first pool allocation is refused by hipMalloc
     unsigned long long* d_wfctl = nullptr;  // [WF_CTL_ALLOC] queue 0 counts, chunk heads, queue 1 counts
     std::vector<hipEvent_t> it_ev;          // per iteration: start, extend|shadow boundary, end
     int it_recorded = 0;                    // iterations of the last trace with events in it_ev
@@ -409,6 +414,7 @@ static int ctx_setup(mfx_ctx* c) {
         }
     }
     // (at most 2^28 slots: k_extend's pending entries keep a slot index in 28 bits)
+    c->pool_fail_once = getenv("MFX_POOL_FAIL_ONCE") && atoi(getenv("MFX_POOL_FAIL_ONCE")) != 0;
     if (const char* pm = getenv("MFX_POOL")) c->wf_pool_max = std::max<int64_t>(2048, std::min<int64_t>(1 << 28, atoll(pm)));
     c->diag_iter = getenv("MFX_DIAG_ITER") != nullptr;
     if (const char* e = getenv("MFX_ITER_EVENTS")) c->iter_events = atoi(e) != 0 || c->diag_iter;
@@ -754,14 +760,18 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     const int nv = c->host.max_depth + 1;  // vertices per path
     const size_t per_slot = WF_DOUBLES_PER_SLOT(nv) * 8 + WF_WORDS_PER_SLOT(nv) * 4 - (queues ? 0 : WF_QUEUE_BYTES_PER_SLOT);
     const size_t bytes = P * per_slot + 64 * 256;
-    // leave the runtime its headroom (kernel scratch is allocated at launch): a pool that would take
-    // the device's last min(512 MiB, a quarter of what is free) counts as out of memory, and wf_trace
+    // leave the runtime its headroom (kernel scratch is allocated at launch, and the runtime gives
+    // an idle queue's scratch back, so a later launch allocates it again): a pool that would take
+    // the device's last min(2 GiB, a quarter of what is free) counts as out of memory, and wf_trace
     // retries with smaller generations. The check runs before the current pool is freed (its bytes
     // count as free), so a refused growth keeps it: a smaller generation may fit in it.
-    size_t mfree = 0, mtotal = 0;
+    // It runs again after the allocation: processes sharing the device (the one-GPU rehearsal of an
+    // N-rank job) that checked at the same time must not take the headroom together (r06n: eight
+    // ranks' pools left no room for a launch's scratch).
+    size_t mfree = 0, mtotal = 0, headroom = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
         const size_t avail = mfree + (c->wf_mem ? c->wf_pool_bytes : 0);
-        const size_t headroom = std::min<size_t>((size_t)512 << 20, avail / 4);
+        headroom = std::min<size_t>((size_t)2 << 30, avail / 4);
         if (bytes + headroom > avail)
             return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB with " +
                                          std::to_string(avail >> 20) + " MiB free");
@@ -770,9 +780,25 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     c->wf_mem = nullptr;
     c->wf_pool = 0;
     c->wf_pool_bytes = 0;
-    hipError_t e = hipMalloc(&c->wf_mem, bytes);
-    if (e != hipSuccess) return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
-                                     std::string("wavefront pool: ") + hipGetErrorString(e));
+    // (MFX_POOL_FAIL_ONCE: the first request is one the device cannot hold, as another process's
+    // allocation between the check above and this one would make it)
+    hipError_t e = hipMalloc(&c->wf_mem, c->pool_fail_once ? ((size_t)1 << 50) : bytes);
+    c->pool_fail_once = false;
+    if (e != hipSuccess) {
+        // wf_trace recovers with smaller generations: clear the failure from the thread's last
+        // error, or the next launch's hipGetLastError reports it as the launch's own (r06p: eight
+        // ranks on one GPU failed "mfx_wf_iteration: out of memory" after a refused pool)
+        (void)hipGetLastError();
+        c->wf_mem = nullptr;
+        return fail(e == hipErrorOutOfMemory ? MFX_E_NOMEM : MFX_E_DEVICE,
+                    std::string("wavefront pool: ") + hipGetErrorString(e));
+    }
+    if (headroom > 0 && hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree < headroom) {
+        (void)hipFree(c->wf_mem);
+        c->wf_mem = nullptr;
+        return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB left " +
+                                     std::to_string(mfree >> 20) + " MiB free");
+    }
     char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
     double** dbl[6] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz};
@@ -1315,17 +1341,51 @@ static bool ensure_stage(mfx_ctx* c, size_t bytes) {
 // Pieces [off[i], off[i] + len[i]) of h_stage, each complete once stage_ev[i] has fired, copied to
 // dst at the same offsets by nt host threads (MFX_READBACK_THREADS; thread t takes slice t of every
 // piece, in piece order). Returns when every piece is in dst.
+static double host_ms() {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// MFX_SAMPLE_TIMING=1 (diagnostics): the host's clock at each piece's arrival and copy, on stderr
+static bool sample_timing() {
+    static const bool on = getenv("MFX_SAMPLE_TIMING") && atoi(getenv("MFX_SAMPLE_TIMING")) != 0;
+    return on;
+}
+
+// NUMA node of the page holding `p` (-1: unknown), by get_mempolicy(MPOL_F_NODE | MPOL_F_ADDR)
+static int page_node(const void* p) {
+    int node = -1;
+    if (syscall(SYS_get_mempolicy, &node, nullptr, 0UL, p, 3UL) != 0) return -1;
+    return node;
+}
+// the device's NUMA node from sysfs (-1: unknown)
+static int device_node(int device) {
+    char bus[64] = {0};
+    if (hipDeviceGetPCIBusId(bus, sizeof(bus), device) != hipSuccess) return -1;
+    for (char* q = bus; *q; ++q) *q = (char)tolower(*q);
+    const std::string path = std::string("/sys/bus/pci/devices/") + bus + "/numa_node";
+    FILE* f = fopen(path.c_str(), "r");
+    if (!f) return -1;
+    int n = -1;
+    if (fscanf(f, "%d", &n) != 1) n = -1;
+    fclose(f);
+    return n;
+}
+
 static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* len, int npiece) {
     int nt = 8;
     if (const char* e = getenv("MFX_READBACK_THREADS")) nt = std::max(1, std::min(32, atoi(e)));
+    const bool tm = sample_timing();
+    double t_ready[kStageChunks] = {0}, t_copied[kStageChunks] = {0};
+    const double t0 = tm ? host_ms() : 0.0;
     auto work = [&](int t) -> hipError_t {
         for (int i = 0; i < npiece; ++i) {
             const hipError_t e = hipEventSynchronize(c->stage_ev[i]);
             if (e != hipSuccess) return e;
+            if (tm && t == 0) t_ready[i] = host_ms();
             const size_t part = (len[i] / nt + 4095) & ~(size_t)4095;
             if (part * t >= len[i]) continue;
             const size_t o = off[i] + part * t;
             std::memcpy((uint8_t*)dst + o, c->h_stage + o, std::min(part, len[i] - part * t));
+            if (tm && t == 0) t_copied[i] = host_ms();
         }
         return hipSuccess;
     };
@@ -1334,6 +1394,13 @@ static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* l
     for (int t = 1; t < nt; ++t) th.emplace_back([&, t] { err[t] = work(t); });
     err[0] = work(0);
     for (auto& t : th) t.join();
+    if (tm) {
+        fprintf(stderr, "copy_staged: %d pieces, from the call's wait (ms): ready/copied", npiece);
+        for (int i = 0; i < npiece; ++i) fprintf(stderr, " %.3f/%.3f", t_ready[i] - t0, t_copied[i] - t0);
+        fprintf(stderr, "; joined %.3f; nodes: staging %d..%d, frame %d..%d, device %d, this cpu %d\n", host_ms() - t0,
+                page_node(c->h_stage), page_node(c->h_stage + off[npiece - 1] + len[npiece - 1] - 1), page_node(dst),
+                page_node((uint8_t*)dst + off[npiece - 1] + len[npiece - 1] - 1), device_node(c->device), sched_getcpu());
+    }
     for (hipError_t e : err)
         if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("readback: ") + hipGetErrorString(e));
     return MFX_OK;
@@ -1816,6 +1883,7 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     };
     c->rep_valid = false;
     c->accum_merged = false;
+    const double t0 = sample_timing() ? host_ms() : 0.0;
     rc = dev_trace_accumulate(c, spp, c->next_sample, &S);
     if (rc) return rc;
     rc = settle_queue_auto(c);
@@ -1825,8 +1893,12 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
         rc = mfx_accum_read_mean(c, (double)spp, frame);
         return rc ? rc : mfx_sync(c);
     }
+    if (sample_timing()) fprintf(stderr, "sample_banded: enqueued in %.3f ms\n", host_ms() - t0);
     rc = copy_staged(c, frame, off, len, nb);
-    return rc ? rc : mfx_sync(c);
+    if (rc) return rc;
+    rc = mfx_sync(c);
+    if (sample_timing()) fprintf(stderr, "sample_banded: call %.3f ms\n", host_ms() - t0);
+    return rc;
 }
 
 int mfx_sample(mfx_ctx* c, int32_t spp, double* frame) {

@@ -861,33 +861,84 @@ __device__ __forceinline__ void cswap3(float& da, int& ca, uint64_t& ma, float& 
     cb = s ? u : cb;
     mb = s ? w : mb;
 }
+// the same network over (integer key, child, lane mask) held in scalar registers
+__device__ __forceinline__ void cswap3u(uint32_t& da, int& ca, uint64_t& ma, uint32_t& db, int& cb, uint64_t& mb) {
+    const bool s = db < da;
+    const uint32_t t = da;
+    const int u = ca;
+    const uint64_t w = ma;
+    da = s ? db : da;
+    ca = s ? cb : ca;
+    ma = s ? mb : ma;
+    db = s ? t : db;
+    cb = s ? u : cb;
+    mb = s ? w : mb;
+}
+#ifndef MFX_PACKET_SORT
+#define MFX_PACKET_SORT 0  // the packet step's child sort: 0 float keys (vector compares), 1 integer keys (scalar), 2 packed index keys
+#endif
+// The node columns (MfxNode: lo x, hi x, lo y, hi y, lo z, hi z as float4 over the four children)
+// of the near and far planes per axis, for a packet whose active lanes' directions share their signs
+// on every axis (the camera rays of almost every tile): a child's near plane on an axis is its lo
+// plane where the direction is positive and its hi plane where it is negative. Because fmaf rounds
+// monotonically and a child's lo <= hi (outward-rounded boxes; an empty child is lo = hi = FLT_MAX),
+// fmaf(near, 1/d, -o/d) is exactly min(fmaf(lo, ...), fmaf(hi, ...)): the slab test keeps its
+// bits without the per-axis min / max pairs (VALU issue is the packet step's bound).
+struct PacketPlanes {
+    int nx, fx, ny, fy, nz, fz;
+};
+
 // One node of the packet walk. `mask`, kept beside every stack entry, names the lanes whose own
 // test hit the node: only they test its children, so a leaf is tested by the lanes whose ray hits
 // its box (child boxes lie inside their parent's, so a lane that missed a node misses its subtree).
 // The stack is wave-uniform: stk[] nodes and stm[] masks in LDS.
+// (The sort on the scalar unit instead — integer keys, the ballots and'ed with the node's mask —
+// halves the step's vector instructions but doubles its scalar ones, and the scalar unit issues
+// for one SIMD per cycle, as the vector unit: k_camera 4.40 -> 4.61 ms, r06o. The step balances
+// the two as it is: ~90 vector, ~80 scalar instructions.)
+template <bool UNI>
 __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ nodes, int node, uint64_t& mask,
-                                                const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp, int rep) {
+                                                const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp, int rep,
+                                                const PacketPlanes& pp) {
     mfx_cf4* q = (mfx_cf4*)(nodes + node);
-    const mfx_f4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
     const mfx_i4 ch = ((mfx_ci4*)q)[6];
-    const bool live = (mask >> __lane_id()) & 1;
-    float d[4];
+    float n[4], f[4];
+    if (UNI) {
+        const mfx_f4 NX = q[pp.nx], FX = q[pp.fx], NY = q[pp.ny], FY = q[pp.fy], NZ = q[pp.nz], FZ = q[pp.fz];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float ax = fmaf(NX[k], r.ix, -r.oix), bx = fmaf(FX[k], r.ix, -r.oix);
+            const float ay = fmaf(NY[k], r.iy, -r.oiy), by = fmaf(FY[k], r.iy, -r.oiy);
+            const float az = fmaf(NZ[k], r.iz, -r.oiz), bz = fmaf(FZ[k], r.iz, -r.oiz);
+            n[k] = fmaxf(fmaxf(ax, ay), fmaxf(az, 0.0f));
+            f[k] = fminf(fminf(bx, by), fminf(bz, tlim));
+        }
+    } else {
+        const mfx_f4 lx = q[0], hx = q[1], ly = q[2], hy = q[3], lz = q[4], hz = q[5];
+        Slab4 SL;
+        slab4(float4{lx.x, lx.y, lx.z, lx.w}, float4{hx.x, hx.y, hx.z, hx.w}, float4{ly.x, ly.y, ly.z, ly.w},
+              float4{hy.x, hy.y, hy.z, hy.w}, float4{lz.x, lz.y, lz.z, lz.w}, float4{hz.x, hz.y, hz.z, hz.w}, r, SL);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];
+            n[k] = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+            f[k] = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+        }
+    }
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     uint64_t m[4];
     int nh = 0;
-    Slab4 SL;
-    slab4(float4{lx.x, lx.y, lx.z, lx.w}, float4{hx.x, hx.y, hx.z, hx.w}, float4{ly.x, ly.y, ly.z, ly.w},
-          float4{hy.x, hy.y, hy.z, hy.w}, float4{lz.x, lz.y, lz.z, lz.w}, float4{hz.x, hz.y, hz.z, hz.w}, r, SL);
+#if MFX_PACKET_SORT == 0
+    float d[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-        const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];
-        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
-        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
-        const bool h = live && n <= f;
-        m[k] = __ballot(h);
+        // the lanes of the node's mask whose test hits: the compare's lane mask and'ed with it (no
+        // per-lane copy of the node's mask), back to a lane predicate for the select below
+        m[k] = __builtin_amdgcn_ballot_w64(n[k] <= f[k]) & mask;
+        const bool h = __builtin_amdgcn_inverse_ballot_w64(m[k]);
         // the representative lane's entry distance, read across lanes into a scalar register
         // (v_readlane: rep is wave-uniform; a __shfl is an LDS permute on the step's chain)
-        const float kd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h ? n : 3.0e38f), rep));
+        const float kd = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h ? n[k] : 3.0e38f), rep));
         d[k] = m[k] ? kd : __builtin_inff();
         nh += m[k] ? 1 : 0;
     }
@@ -897,6 +948,50 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
     cswap3(d[1], c[1], m[1], d[3], c[3], m[3]);
     cswap3(d[1], c[1], m[1], d[2], c[2], m[2]);
     nh = __builtin_amdgcn_readfirstlane(nh);
+#else
+    // integer keys on the scalar unit: entry distances are >= 0, where IEEE order is the bits' order
+    // (the sign bit cleared: a -0 sorts as the 0 it compares equal to)
+    uint32_t d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        m[k] = __builtin_amdgcn_ballot_w64(n[k] <= f[k]) & mask;
+        const bool h = __builtin_amdgcn_inverse_ballot_w64(m[k]);
+        const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(h ? n[k] : 3.0e38f), rep) & 0x7fffffffu;
+        d[k] = m[k] ? kd : 0x7f800000u;
+        nh += m[k] ? 1 : 0;
+    }
+#if MFX_PACKET_SORT == 1
+    cswap3u(d[0], c[0], m[0], d[1], c[1], m[1]);
+    cswap3u(d[2], c[2], m[2], d[3], c[3], m[3]);
+    cswap3u(d[0], c[0], m[0], d[2], c[2], m[2]);
+    cswap3u(d[1], c[1], m[1], d[3], c[3], m[3]);
+    cswap3u(d[1], c[1], m[1], d[2], c[2], m[2]);
+#else
+    // the child's index in the key's two low bits (ties within 4 ulps break by index: the visit
+    // order only steers the walk, every order gives the same hits), sorted by min / max alone
+#pragma unroll
+    for (int k = 0; k < 4; ++k) d[k] = (d[k] & ~3u) | (uint32_t)k;
+    const int c0[4] = {c[0], c[1], c[2], c[3]};
+    const uint64_t m0[4] = {m[0], m[1], m[2], m[3]};
+#define MFX_KSWAP(a, b)                          \
+    do {                                         \
+        const uint32_t _lo = min(d[a], d[b]);    \
+        d[b] = max(d[a], d[b]);                  \
+        d[a] = _lo;                              \
+    } while (0)
+    MFX_KSWAP(0, 1);
+    MFX_KSWAP(2, 3);
+    MFX_KSWAP(0, 2);
+    MFX_KSWAP(1, 3);
+    MFX_KSWAP(1, 2);
+#undef MFX_KSWAP
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        c[k] = c0[d[k] & 3];
+        m[k] = m0[d[k] & 3];
+    }
+#endif
+#endif
     if (__lane_id() == 0) {  // the pushes are wave-uniform: one lane writes them
         if (nh >= 2) {
             stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);
@@ -933,14 +1028,12 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
 // 128-B node each) and leaf slots (an 80-B test prefix each), counted on every lane alike.
 // PH (diagnostic builds, -DMFX_DIAG_STAMPS=3): ph[0] += the wave's cycles in node steps, ph[1] += in
 // leaf tests, ph[2] += node steps, ph[3] += leaf visits
-template <bool STATS, bool PH = false>
-__device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
-                                               int* stk, uint64_t* stm, Stats& st, uint32_t& pk_nodes,
-                                               uint32_t& pk_slots, uint64_t* ph = nullptr) {
-    B = Best{tMax, -1, -1, false};
-    const RayF rf = make_rayf(o, d);
+template <bool STATS, bool PH, bool UNI>
+__device__ __forceinline__ void packet_walk(const SceneView& S, DV o, DV d, const RayF& rf, uint64_t mask, Best& B,
+                                            int* stk, uint64_t* stm, Stats& st, uint32_t& pk_nodes,
+                                            uint32_t& pk_slots, uint64_t* ph, const PacketPlanes& pp) {
+    const double tMax = B.t;
     float tlim = f_tlim(tMax);
-    uint64_t mask = __ballot(act);
     const int rep = __builtin_ctzll(mask);
     int sp = 0, node = 0;
     uint64_t t0 = 0;
@@ -950,7 +1043,7 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
             if (STATS && ((mask >> __lane_id()) & 1)) st.nodes++;
             if (STATS) pk_nodes++;
             if (PH) ph[2]++;
-            node = packet_node_step(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep);
+            node = packet_node_step<UNI>(S.nodes, node, mask, rf, tlim, stk, stm, sp, rep, pp);
         }
         if (PH) {
             const uint64_t t1 = diag_clock();
@@ -976,6 +1069,28 @@ __device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV 
         } else {
             return;
         }
+    }
+}
+// the walk specialised on the packet's direction signs: one walk with the near / far columns of the
+// tile's octant when its active lanes agree on every axis, the general slab test otherwise
+template <bool STATS, bool PH = false>
+__device__ __forceinline__ void packet_closest(const SceneView& S, bool act, DV o, DV d, double tMax, Best& B,
+                                               int* stk, uint64_t* stm, Stats& st, uint32_t& pk_nodes,
+                                               uint32_t& pk_slots, uint64_t* ph = nullptr) {
+    B = Best{tMax, -1, -1, false};
+    const RayF rf = make_rayf(o, d);
+    const uint64_t mask = __ballot(act);
+    if (mask == 0) return;
+    const uint64_t nx = __ballot(act && rf.ix < 0.0f), ny = __ballot(act && rf.iy < 0.0f),
+                   nz = __ballot(act && rf.iz < 0.0f);
+    const bool uni = (nx == 0 || nx == mask) && (ny == 0 || ny == mask) && (nz == 0 || nz == mask);
+    if (uni) {
+        const int sx = nx ? 1 : 0, sy = ny ? 1 : 0, sz = nz ? 1 : 0;
+        const PacketPlanes pp{sx, 1 - sx, 2 + sy, 3 - sy, 4 + sz, 5 - sz};
+        packet_walk<STATS, PH, true>(S, o, d, rf, mask, B, stk, stm, st, pk_nodes, pk_slots, ph, pp);
+    } else {
+        const PacketPlanes pp{0, 1, 2, 3, 4, 5};
+        packet_walk<STATS, PH, false>(S, o, d, rf, mask, B, stk, stm, st, pk_nodes, pk_slots, ph, pp);
     }
 }
 

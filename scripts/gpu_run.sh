@@ -22,6 +22,7 @@
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
 #   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
 #                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
+#   sampletime           mfx_sample's host timeline per band, bench state vs a lone process
 #   sampletrace          mfx_sample under rocprofv3 kernel + memory-copy trace (scripts/sample_trace.py)
 #   sharequeues:K        K strong-share children under a kernel trace: HW queue ids per rank (share_queues.py)
 #   py:SCRIPT[:ARGS]     scripts/SCRIPT.py ARGS (comma-separated) -> SCRIPT.json
@@ -129,6 +130,15 @@ for step in "$@"; do
       timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a1 --spp ${a2:-64} \
         --out $O/latency_$(basename $a1 .xml).json > $O/latroof.log 2>&1
       tail -5 $O/latroof.log ;;
+    sampletime)
+      # mfx_sample's host timeline (MFX_SAMPLE_TIMING=1: each band's arrival and copy) in bench.py's
+      # process state and in a process that only samples (scripts/sample_in_bench_probe.py)
+      SAMPLE_PROBE_SETTINGS=bands4_streams1,unbanded MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
+        python3 scripts/sample_in_bench_probe.py > $O/sampletime_bench.json 2> $O/sampletime_bench.err
+      SAMPLE_PROBE_SETTINGS=bands4_streams1,unbanded MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
+        python3 scripts/sample_in_bench_probe.py --lone > $O/sampletime_lone.json 2> $O/sampletime_lone.err
+      (lscpu | grep -i numa; grep Cpus_allowed_list /proc/self/status) > $O/sampletime_numa.txt || true
+      cat $O/sampletime_bench.json $O/sampletime_lone.json $O/sampletime_numa.txt ;;
     sampletrace)
       # mfx_sample under a kernel + memory-copy trace, banded vs unbanded (scripts/sample_trace.py)
       D=$R/$O/sampletrace

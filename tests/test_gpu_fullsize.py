@@ -157,3 +157,21 @@ def test_pool_shrinks_when_the_device_is_short_of_memory(gpu):
     assert np.array_equal(counts, want_counts)
     assert gens_short > 1 and gens_after == 1
     assert np.array_equal(again, want)
+
+
+def test_trace_after_a_refused_pool_allocation(gpu, monkeypatch):
+    """The pool's hipMalloc itself refused (another process took the memory between the headroom check
+    and the allocation; MFX_POOL_FAIL_ONCE=1 asks for a size no device holds): wf_trace retries, and the
+    refusal must not surface as the next launch's error (HIP's last error, which the launches return:
+    r06p, eight ranks on one GPU failed "mfx_wf_iteration: out of memory"). The frame equals a plain
+    context's bit for bit."""
+    from mafrixraytracing_amd.native import NativeContext
+    a = scene("cube_cornell", 64, 36)
+    with NativeContext(a, seed=SEED) as c:
+        c.trace_accumulate(4, 0)
+        want = c.accum_read_mean(4.0)
+    monkeypatch.setenv("MFX_POOL_FAIL_ONCE", "1")
+    with NativeContext(a, seed=SEED) as c:
+        c.trace_accumulate(4, 0)
+        got = c.accum_read_mean(4.0)
+    assert np.array_equal(got, want)
