@@ -1370,7 +1370,9 @@ static int device_node(int device) {
     return n;
 }
 
-static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* len, int npiece) {
+// rgb: the staging buffer holds interleaved RGB (24 B a pixel; off / len in its bytes, whole pixels)
+// and dst RGBA (32 B a pixel): each pixel is widened with alpha 1.0 as it is copied (mfx_sample)
+static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* len, int npiece, bool rgb = false) {
     int nt = 8;
     if (const char* e = getenv("MFX_READBACK_THREADS")) nt = std::max(1, std::min(32, atoi(e)));
     const bool tm = sample_timing();
@@ -1381,6 +1383,22 @@ static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* l
             const hipError_t e = hipEventSynchronize(c->stage_ev[i]);
             if (e != hipSuccess) return e;
             if (tm && t == 0) t_ready[i] = host_ms();
+            if (rgb) {
+                const size_t npx = len[i] / 24, p0 = off[i] / 24;
+                const size_t part = (npx / nt + 63) & ~(size_t)63;  // whole pixels, 64 at a time
+                if (part * t >= npx) continue;
+                const double* src = (const double*)c->h_stage + 3 * (p0 + part * t);
+                double* out = (double*)dst + 4 * (p0 + part * t);
+                const size_t n = std::min(part, npx - part * t);
+                for (size_t k = 0; k < n; ++k) {
+                    out[4 * k] = src[3 * k];
+                    out[4 * k + 1] = src[3 * k + 1];
+                    out[4 * k + 2] = src[3 * k + 2];
+                    out[4 * k + 3] = 1.0;
+                }
+                if (tm && t == 0) t_copied[i] = host_ms();
+                continue;
+            }
             const size_t part = (len[i] / nt + 4095) & ~(size_t)4095;
             if (part * t >= len[i]) continue;
             const size_t o = off[i] + part * t;
@@ -1399,7 +1417,7 @@ static int copy_staged(mfx_ctx* c, void* dst, const size_t* off, const size_t* l
         for (int i = 0; i < npiece; ++i) fprintf(stderr, " %.3f/%.3f", t_ready[i] - t0, t_copied[i] - t0);
         fprintf(stderr, "; joined %.3f; nodes: staging %d..%d, frame %d..%d, device %d, this cpu %d\n", host_ms() - t0,
                 page_node(c->h_stage), page_node(c->h_stage + off[npiece - 1] + len[npiece - 1] - 1), page_node(dst),
-                page_node((uint8_t*)dst + off[npiece - 1] + len[npiece - 1] - 1), device_node(c->device), sched_getcpu());
+                page_node((uint8_t*)dst + (off[npiece - 1] + len[npiece - 1]) / (rgb ? 24 : 1) * (rgb ? 32 : 1) - 1), device_node(c->device), sched_getcpu());
     }
     for (hipError_t e : err)
         if (e != hipSuccess) return fail(MFX_E_DEVICE, std::string("readback: ") + hipGetErrorString(e));
@@ -1837,6 +1855,61 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
 // range of the x-major frame (pixel = x * h + y). The bits are the unbanded path's: a pixel's sum is
 // its own thread's, and the mean is the same division. MFX_SAMPLE_BANDS=0: the unbanded path.
 // Returns 1 (nothing done) when the call is not for it (a device list, no staging memory).
+// mfx_sample's copy stream, chosen by measurement: a stream's device-to-host copies keep the DMA
+// engine their first copy took, and a context's readback ran at ~53 GB/s on some streams and at
+// ~26-31 GB/s on others, stream for stream (r06q-r06s: the same process, call after call; the
+// staging pages and the device on the same NUMA node). So MFX_COPY_PROBE (default 4) candidate
+// streams each copy `bytes` (up to 16 MB) of the frame twice, the second copy timed, and the fastest
+// is kept. Once per context, at its first Sample call.
+static int pick_copy_stream(mfx_ctx* c, size_t bytes) {
+    int n = 4;
+    if (const char* e = getenv("MFX_COPY_PROBE")) n = std::max(1, std::min(8, atoi(e)));
+    if (n == 1) {
+        HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+        return MFX_OK;
+    }
+    const size_t pb = std::min(bytes, (size_t)16 << 20);
+    std::vector<hipStream_t> cand(n, nullptr);
+    std::vector<float> ms(n, 1e30f);
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    HIPCHECK(hipEventCreate(&e0));
+    HIPCHECK(hipEventCreate(&e1));
+    for (int i = 0; i < n; ++i) {
+        HIPCHECK(hipStreamCreateWithFlags(&cand[i], hipStreamNonBlocking));
+        HIPCHECK(hipMemcpyAsync(c->h_stage, c->d_frame, pb, hipMemcpyDeviceToHost, cand[i]));
+        HIPCHECK(hipEventRecord(e0, cand[i]));
+        HIPCHECK(hipMemcpyAsync(c->h_stage, c->d_frame, pb, hipMemcpyDeviceToHost, cand[i]));
+        HIPCHECK(hipEventRecord(e1, cand[i]));
+        HIPCHECK(hipEventSynchronize(e1));
+        HIPCHECK(hipEventElapsedTime(&ms[i], e0, e1));
+    }
+    const int best = (int)(std::min_element(ms.begin(), ms.end()) - ms.begin());
+    if (sample_timing()) {  // (diagnostics: the candidates' copies at once, k = 2 and all n)
+        for (int k : {2, n}) {
+            HIPCHECK(hipDeviceSynchronize());
+            const double t0 = host_ms();
+            for (int i = 0; i < k; ++i)
+                HIPCHECK(hipMemcpyAsync(c->h_stage + (size_t)i * (pb / n), (const uint8_t*)c->d_frame, pb / n * (n / k),
+                                        hipMemcpyDeviceToHost, cand[i]));
+            for (int i = 0; i < k; ++i) HIPCHECK(hipStreamSynchronize(cand[i]));
+            const double dt = host_ms() - t0;
+            fprintf(stderr, "pick_copy_stream: %d streams at once, %zu B each: %.1f GB/s together\n", k, pb / n * (n / k),
+                    (double)(pb / n * (n / k)) * k / (dt * 1e6));
+        }
+    }
+    c->copy_stream = cand[best];
+    for (int i = 0; i < n; ++i)
+        if (i != best) HIPCHECK(hipStreamDestroy(cand[i]));
+    HIPCHECK(hipEventDestroy(e0));
+    HIPCHECK(hipEventDestroy(e1));
+    if (sample_timing()) {
+        fprintf(stderr, "pick_copy_stream: %zu B per probe, GB/s:", pb);
+        for (int i = 0; i < n; ++i) fprintf(stderr, " %.1f", pb / (ms[i] * 1e6));
+        fprintf(stderr, "; kept %d\n", best);
+    }
+    return MFX_OK;
+}
+
 static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     // 4 bands, one copy stream: in the bench process's state (r06i, scripts/sample_in_bench_probe.py)
     // 4 x 1 took 32.8-33.0 ms per C2 call, 8 x 1 33.0-33.2, 8 bands over two copy streams 33.7-33.9 and
@@ -1845,12 +1918,19 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     if (const char* e = getenv("MFX_SAMPLE_BANDS")) nb = std::min(kStageChunks, atoi(e));
     const int W = c->host.width, H = c->host.height;
     nb = std::min(nb, (W + 7) / 8);
-    const size_t bytes = 4 * sizeof(double) * (size_t)c->npix;
+    // the means staged as interleaved RGB (MFX_SAMPLE_RGBA=1: the whole RGBA frame, A/B knob): the
+    // host writes alpha while it copies, so the DMA carries 49.8 MB of C2's 66 MB frame
+    const bool rgb = !(getenv("MFX_SAMPLE_RGBA") && atoi(getenv("MFX_SAMPLE_RGBA")) != 0);
+    const size_t pxb = (rgb ? 3 : 4) * sizeof(double);
+    const size_t bytes = pxb * (size_t)c->npix;
     if (nb < 1 || !c->peers.empty() || !c->comms.empty() || !ensure_stage(c, bytes)) return 1;
     HIPCHECK(hipSetDevice(c->device));
     int rc = stage_events(c);
     if (rc) return rc;
-    if (!c->copy_stream) HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));
+    if (!c->copy_stream) {
+        rc = pick_copy_stream(c, bytes);
+        if (rc) return rc;
+    }
     int ncs = 1;  // MFX_SAMPLE_COPY_STREAMS=2: bands alternate over two copy streams (A/B knob; slower, r06i)
     if (const char* e = getenv("MFX_SAMPLE_COPY_STREAMS")) ncs = atoi(e) == 2 ? 2 : 1;
     // MFX_SAMPLE_ZEROCOPY=1 (A/B knob): each band's mean kernel runs on a copy stream and writes the
@@ -1864,15 +1944,19 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
     S.nbands = nb;
     S.after = [&](int k, int tx0, int ntx) -> int {
         const int64_t p0 = (int64_t)tx0 * 8 * H, p1 = (int64_t)std::min(W, (tx0 + ntx) * 8) * H;
-        off[k] = (size_t)p0 * 4 * sizeof(double);
-        len[k] = (size_t)(p1 - p0) * 4 * sizeof(double);
+        off[k] = (size_t)p0 * pxb;
+        len[k] = (size_t)(p1 - p0) * pxb;
         hipStream_t cs = (ncs == 2 && (k & 1)) ? c->sample_copy2 : c->copy_stream;
+        auto mean = [&](double* out, hipStream_t st) {
+            return rgb ? mfx_launch_mean_rgb(c->d_accum, c->npix, (double)spp, out, st, p0, p1)
+                       : mfx_launch_mean(c->d_accum, c->npix, (double)spp, out, st, p0, p1);
+        };
         if (zc) {
             HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
             HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
-            HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, (double*)stage_dev, cs, p0, p1));
+            HIPCHECK(mean((double*)stage_dev, cs));
         } else {
-            HIPCHECK(mfx_launch_mean(c->d_accum, c->npix, (double)spp, c->d_frame, c->stream, p0, p1));
+            HIPCHECK(mean(c->d_frame, c->stream));
             HIPCHECK(hipEventRecord(c->band_ev[k], c->stream));
             HIPCHECK(hipStreamWaitEvent(cs, c->band_ev[k], 0));
             if (len[k]) HIPCHECK(hipMemcpyAsync(c->h_stage + off[k], (const uint8_t*)c->d_frame + off[k], len[k],
@@ -1894,7 +1978,7 @@ static int sample_banded(mfx_ctx* c, int32_t spp, double* frame) {
         return rc ? rc : mfx_sync(c);
     }
     if (sample_timing()) fprintf(stderr, "sample_banded: enqueued in %.3f ms\n", host_ms() - t0);
-    rc = copy_staged(c, frame, off, len, nb);
+    rc = copy_staged(c, frame, off, len, nb, rgb);
     if (rc) return rc;
     rc = mfx_sync(c);
     if (sample_timing()) fprintf(stderr, "sample_banded: call %.3f ms\n", host_ms() - t0);

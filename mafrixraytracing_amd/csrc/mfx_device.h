@@ -65,6 +65,9 @@ hipError_t mfx_trace_occupancy(int stack_size, int* blocks_per_cu, bool inst = f
 hipError_t mfx_launch_query(const QueryParams& Q, bool shadow, hipStream_t st);
 hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* out, hipStream_t st, int64_t p0 = 0,
                            int64_t p1 = -1);
+// pixels [p0, p1) of the mean as interleaved RGB (3 doubles a pixel): mfx_sample's staged readback
+hipError_t mfx_launch_mean_rgb(const double* accum, int64_t npix, double n, double* out, hipStream_t st, int64_t p0,
+                               int64_t p1);
 hipError_t mfx_launch_film_post(const double* accum, double* film, int w, int h, double spp, double frame_count,
                                 int add, uint8_t* rgba, hipStream_t st);
 hipError_t mfx_launch_film_mean(const double* film, int64_t npix, double frame_count, double* out, hipStream_t st);

@@ -430,6 +430,17 @@ __global__ void mean_kernel(const double* __restrict__ accum, int64_t npix, doub
     o[1] = make_double2(accum[2 * npix + q] / n, 1.0);
 }
 
+// the same means as interleaved RGB: the alpha channel (1.0) is the host's to write, so the readback
+// carries three quarters of the bytes
+__global__ void mean_rgb_kernel(const double* __restrict__ accum, int64_t npix, double n, double* __restrict__ out,
+                                int64_t p0, int64_t p1) {
+    const int64_t q = p0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (q >= p1) return;
+    double* o = out + 3 * q;
+    o[0] = accum[q] / n;
+    o[1] = accum[npix + q] / n;
+    o[2] = accum[2 * npix + q] / n;
+}
 
 // Film.AddSample (Film.fs:18-23) with frame = accum / spp, then PostProcessAndToScreenBuffer
 // (Scene.fs:315-330) on target = film / frameCount.
@@ -563,6 +574,13 @@ hipError_t mfx_launch_mean(const double* accum, int64_t npix, double n, double* 
     if (p1 < 0) p1 = npix;
     if (p1 <= p0) return hipSuccess;
     hipLaunchKernelGGL(mean_kernel, dim3(grid_for(p1 - p0, 256)), dim3(256), 0, st, accum, npix, n, out, p0, p1);
+    return hipGetLastError();
+}
+
+hipError_t mfx_launch_mean_rgb(const double* accum, int64_t npix, double n, double* out, hipStream_t st, int64_t p0,
+                               int64_t p1) {
+    if (p1 <= p0) return hipSuccess;
+    hipLaunchKernelGGL(mean_rgb_kernel, dim3(grid_for(p1 - p0, 256)), dim3(256), 0, st, accum, npix, n, out, p0, p1);
     return hipGetLastError();
 }
 

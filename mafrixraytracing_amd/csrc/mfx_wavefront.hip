@@ -644,7 +644,11 @@ __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
 // or MISS | FRESH. Flat scenes only (two-level scenes take k_extend).
 // ------------------------------------------------------------------------------------------------
 #ifndef MFX_CAM_WAVES
-#define MFX_CAM_WAVES 4  // k_camera's register budget: waves per SIMD (a packet walk is one chain of scalar loads per wave)
+// k_camera's register budget: waves per SIMD (a packet walk is one chain of scalar loads per wave).
+// Five (96 VGPRs, 56 B of spill) beat four (112 VGPRs, none): 4.30 -> 4.12 ms per C2 launch, Renault
+// 6.46 -> 6.19 (interleaved A/B, profiles/r06/r06r_ab_camera_five_waves.txt): the walk waits on its
+// loads more than it issues, and the fifth wave fills those waits
+#define MFX_CAM_WAVES 5
 #endif
 template <bool STATS>
 __global__ void __launch_bounds__(256, MFX_CAM_WAVES) k_camera(WfParams P) {

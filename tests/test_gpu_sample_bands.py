@@ -3,7 +3,8 @@ runs in column bands of tiles, each band's mean and readback enqueued behind it 
 Every Sample frame must be the unbanded path's (MFX_SAMPLE_BANDS=0) and the oracle's bit for bit:
 films whose width is not a multiple of 8 (a partial last tile column), fewer tile columns than bands,
 several generations (MFX_POOL: only the last one is banded), one sample per pixel (the megakernel,
-no bands) and back-to-back calls that reuse the staging buffer."""
+no bands) and back-to-back calls that reuse the staging buffer. The bands' means are staged as RGB and
+widened to RGBA by the host (alpha 1.0); MFX_SAMPLE_RGBA=1 stages the RGBA frame itself."""
 import numpy as np
 import pytest
 
@@ -23,11 +24,15 @@ def test_banded_sample_equals_unbanded_and_oracle(gpu, oracle, monkeypatch, name
     with NativeContext(a, seed=SEED) as c:
         zero = [c.sample(spp) for _ in range(2)]
     monkeypatch.delenv("MFX_SAMPLE_ZEROCOPY")
+    monkeypatch.setenv("MFX_SAMPLE_RGBA", "1")  # the whole RGBA frame staged (no host-written alpha)
+    with NativeContext(a, seed=SEED) as c:
+        rgba = [c.sample(spp) for _ in range(2)]
+    monkeypatch.delenv("MFX_SAMPLE_RGBA")
     monkeypatch.setenv("MFX_SAMPLE_BANDS", "0")
     with NativeContext(a, seed=SEED) as c:
         plain = [c.sample(spp) for _ in range(2)]
-    for b, z, p in zip(banded, zero, plain):
-        assert np.array_equal(b, p) and np.array_equal(z, p)
+    for b, z, r, p in zip(banded, zero, rgba, plain):
+        assert np.array_equal(b, p) and np.array_equal(z, p) and np.array_equal(r, p)
     o = oracle.OracleScene(a)
     assert np.array_equal(banded[1], o.sample(spp, SEED, sample_base=spp))
 
