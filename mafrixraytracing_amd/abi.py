@@ -30,7 +30,8 @@ MFX_MAX_DEVICES = 64
 MFX_ABI_VERSION = 6
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmafrix_rt.so")
+# MFX_LIB_PATH: another build of the same library (scripts' A/B and roof passes on a variant)
+LIB_PATH = os.environ.get("MFX_LIB_PATH") or os.path.join(_HERE, "libmafrix_rt.so")
 
 
 class MfxPrim(C.Structure):

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <functional>
 #include <cstdlib>
@@ -75,6 +76,44 @@ const Rccl* rccl() {
     return ok ? &r : nullptr;
 }
 
+// IEEE binary16 bits of the half nearest x in the direction `up` (true: the least half >= x, false:
+// the greatest half <= x); beyond the half range: +-inf on the outward side, +-65504 on the inward
+uint16_t half_dir(float x, bool up) {
+    if (std::isinf(x)) return x > 0 ? 0x7c00 : 0xfc00;
+    if (x < 0) return (uint16_t)(0x8000 | half_dir(-x, !up));
+    if (x == 0) return up ? 0 : 0;
+    if (x > 65504.f) return up ? 0x7c00 : 0x7bff;
+    int e = 0;
+    (void)std::frexp((double)x, &e);  // x = m * 2^e, m in [0.5, 1)
+    const int ex = std::max(e - 1, -14);  // the half's exponent (subnormals: -14)
+    const double ulp = std::ldexp(1.0, ex - 10);
+    const double m = (double)x / ulp;  // exact (a power-of-two scaling)
+    const double k = up ? std::ceil(m) : std::floor(m);
+    const double v = k * ulp;  // representable (k <= 2048)
+    if (v > 65504.0) return 0x7c00;
+    if (v < std::ldexp(1.0, -14)) return (uint16_t)(v / std::ldexp(1.0, -24));  // subnormal
+    int ve = 0;
+    const double vm = std::frexp(v, &ve);  // v = vm * 2^ve
+    const int E = ve - 1;
+    const int mant = (int)((vm * 2.0 - 1.0) * 1024.0);
+    return (uint16_t)(((E + 15) << 10) | mant);
+}
+// the per-lane kernels' FP16 node: each child's box rounded outward, empty children all +inf
+MfxNodeH node_to_half(const MfxNode& n) {
+    MfxNodeH h;
+    for (int k = 0; k < 4; ++k) {
+        const bool empty = n.child[k] == MFX_CHILD_EMPTY;
+        h.lox[k] = empty ? 0x7c00 : half_dir(n.lox[k], false);
+        h.hix[k] = empty ? 0x7c00 : half_dir(n.hix[k], true);
+        h.loy[k] = empty ? 0x7c00 : half_dir(n.loy[k], false);
+        h.hiy[k] = empty ? 0x7c00 : half_dir(n.hiy[k], true);
+        h.loz[k] = empty ? 0x7c00 : half_dir(n.loz[k], false);
+        h.hiz[k] = empty ? 0x7c00 : half_dir(n.hiz[k], true);
+        h.child[k] = n.child[k];
+    }
+    return h;
+}
+
 template <typename T>
 hipError_t upload(T** dptr, const std::vector<T>& v) {
     size_t bytes = std::max<size_t>(sizeof(T), v.size() * sizeof(T));
@@ -126,6 +165,7 @@ struct mfx_ctx {
     MfxHostScene host;
     MfxNode* d_nodes = nullptr;
     MfxSlot* d_slots = nullptr;
+    MfxNodeH* d_nodes_h = nullptr;  // MFX_NODE_F16 builds: the FP16 copy of d_nodes (per-lane kernels)
     int32_t* d_slot_ref = nullptr;
     uint8_t* d_ref_blob = nullptr;
     MfxShade* d_shade = nullptr;
@@ -278,6 +318,65 @@ static void ahead_free(mfx_ctx* c) {
     c->ab_cur = -1;
 }
 
+// MFX_POOL_CACHE=1: the path-slot pool of a destroyed context is kept for the next context on its
+// device (one block per device; default: freed at once). A context's trace ran 8 % slower in about one
+// context of six created after others had come and gone in the process (r06y/r06z: mfx_sample's
+// trace 32.8-33.5 against 30.5 ms, the same kernels), and a fresh block of tens of GB after the
+// frees is where that churn shows; taking the block a finished context used avoids it and the
+// allocation itself. A request the block does not fit (smaller, or more than twice its size)
+// frees it first, so the cache never stands between a context and the memory it needs.
+namespace {
+struct CachedPool {
+    int device;
+    void* ptr;
+    size_t bytes;
+};
+std::mutex g_pool_mu;
+std::vector<CachedPool> g_pool_cache;
+bool pool_cache_on() { return getenv("MFX_POOL_CACHE") && atoi(getenv("MFX_POOL_CACHE")) != 0; }
+// the device's cached block when it holds `bytes` without doubling them (its size in *got), else
+// nullptr after freeing it
+void* pool_cache_take(int device, size_t bytes, size_t* got) {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if (g_pool_cache.empty()) return nullptr;
+    const bool on = pool_cache_on();
+    void* r = nullptr;
+    for (size_t i = 0; i < g_pool_cache.size(); ++i) {
+        CachedPool& b = g_pool_cache[i];
+        if (b.device != device) continue;
+        if (on && !r && b.bytes >= bytes && b.bytes <= 2 * bytes) {
+            r = b.ptr;
+            *got = b.bytes;
+        } else {
+            (void)hipFree(b.ptr);
+        }
+        g_pool_cache.erase(g_pool_cache.begin() + (long)i);
+        --i;
+    }
+    return r;
+}
+// keep a finished context's pool (the larger of it and the device's cached block)
+void pool_cache_put(int device, void* ptr, size_t bytes) {
+    if (!pool_cache_on()) {
+        (void)hipFree(ptr);
+        return;
+    }
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (CachedPool& b : g_pool_cache) {
+        if (b.device != device) continue;
+        if (b.bytes >= bytes) {
+            (void)hipFree(ptr);
+        } else {
+            (void)hipFree(b.ptr);
+            b.ptr = ptr;
+            b.bytes = bytes;
+        }
+        return;
+    }
+    g_pool_cache.push_back(CachedPool{device, ptr, bytes});
+}
+}  // namespace
+
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
     for (ncclComm_t cm : c->comms)
@@ -291,8 +390,10 @@ static void free_ctx(mfx_ctx* c) {
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     if (c->d_merge) (void)hipFree(c->d_merge);
+    if (c->wf_mem) pool_cache_put(c->device, c->wf_mem, c->wf_pool_bytes);  // for the device's next context
+    c->wf_mem = nullptr;
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
-                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_light, c->d_cam, (void*)c->d_refs};
+                    c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_light, c->d_cam, (void*)c->d_refs, c->d_nodes_h};
     for (void* b : bufs)
         if (b) (void)hipFree(b);
     ahead_free(c);
@@ -381,6 +482,11 @@ static int ctx_setup(mfx_ctx* c) {
     CK(hipEventCreate(&c->ev1));
     CK(upload(&c->d_nodes, c->host.nodes));
     CK(upload(&c->d_slots, c->host.slots));
+    if (MFX_NODE_F16 && !getenv("MFX_NODE_F32")) {  // (MFX_NODE_F32=1: the F16 build on FP32 nodes)
+        std::vector<MfxNodeH> nh(c->host.nodes.size());
+        for (size_t i = 0; i < nh.size(); ++i) nh[i] = node_to_half(c->host.nodes[i]);
+        CK(upload(&c->d_nodes_h, nh));
+    }
     CK(upload(&c->d_slot_ref, c->host.slot_ref));
     CK(upload(&c->d_ref_blob, c->host.ref_blob));
     CK(upload(&c->d_shade, c->host.shade));
@@ -768,6 +874,12 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     // It runs again after the allocation: processes sharing the device (the one-GPU rehearsal of an
     // N-rank job) that checked at the same time must not take the headroom together (r06n: eight
     // ranks' pools left no room for a launch's scratch).
+    size_t cached = 0;
+    if (void* cp = pool_cache_take(c->device, bytes, &cached)) {  // a finished context's pool
+        if (c->wf_mem) (void)hipFree(c->wf_mem);
+        c->wf_mem = cp;
+        c->wf_pool_bytes = cached;
+    } else {
     size_t mfree = 0, mtotal = 0, headroom = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
         const size_t avail = mfree + (c->wf_mem ? c->wf_pool_bytes : 0);
@@ -798,6 +910,8 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
         c->wf_mem = nullptr;
         return fail(MFX_E_NOMEM, "wavefront pool: " + std::to_string(bytes >> 20) + " MiB left " +
                                      std::to_string(mfree >> 20) + " MiB free");
+    }
+    c->wf_pool_bytes = bytes;
     }
     char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
@@ -833,7 +947,6 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
 #endif
     c->wf_pool = pool;
     c->wf_pool_q = queues;
-    c->wf_pool_bytes = bytes;
     return MFX_OK;
 }
 
@@ -867,6 +980,9 @@ static void wf_queue_views(mfx_ctx* c, WfParams& P, int d) {
 
 static void fill_scene_params(mfx_ctx* c, WfParams& P) {
     P.nodes = c->d_nodes;
+#if MFX_NODE_F16
+    P.nodes_h = c->d_nodes_h;
+#endif
     P.slots = c->d_slots;
     P.slot_ref = c->d_slot_ref;
     P.ref_blob = c->d_ref_blob;

@@ -42,6 +42,19 @@ struct alignas(16) MfxNode {  // BVH4 node: four child boxes, 128 B (one cache l
 };
 #define MFX_CHILD_EMPTY (-0x7fffffff - 1)
 
+// The per-lane kernels' (k_extend, k_shadow) BVH4 nodes with the FP32 planes rounded outward to FP16
+// (IEEE binary16 bits), 64 B a node: four 16-B loads instead of seven, two nodes a cache line; an
+// empty child's planes are all +inf. k_camera's packets and the megakernel keep the FP32 nodes.
+// Round 6 A/B (profiles/r06/r06v_ab_fp16_nodes.txt): C2 +1.4 %, Renault +2.6 %; -DMFX_NODE_F16=0 builds
+// the FP32-only library.
+#ifndef MFX_NODE_F16
+#define MFX_NODE_F16 1
+#endif
+struct alignas(16) MfxNodeH {
+    uint16_t lox[4], hix[4], loy[4], hiy[4], loz[4], hiz[4];
+    int32_t child[4];
+};
+
 // nodes[0 .. MFX_TOP_NODES) are the BVH's top levels in breadth-first order (the trace kernels
 // keep a prefix of them in LDS); the rest follow in preorder
 #ifndef MFX_TOP_NODES

@@ -36,7 +36,6 @@ __device__ __forceinline__ DV vnormalize(DV v) {
     if (l == 0.0) return dv(0, 0, 0);
     return dv(v.x / l, v.y / l, v.z / l);
 }
-
 // ----------------------------------------------------------------------------------------------
 // Counter-based RNG — identical to oracle/mfx_oracle.c rng_*
 // ----------------------------------------------------------------------------------------------
@@ -725,6 +724,9 @@ __device__ __forceinline__ void cswap(float& da, int& ca, float& db, int& cb) {
 struct TopNodes {
     const float4* lds;
     int ntop;
+#if MFX_NODE_F16
+    const MfxNodeH* nodes_h = nullptr;  // the per-lane kernels' FP16 nodes (the LDS copy alike)
+#endif
 };
 __device__ __forceinline__ int top_col(int n, int c) { return n * 8 + (c ^ ((n >> 1) & 7)); }
 // block-wide copy at kernel start (all threads; ends with a barrier); a node is eight 16-B columns
@@ -734,6 +736,20 @@ __device__ __forceinline__ void load_top_nodes(float4* lds, const void* __restri
     for (int i = threadIdx.x; i < ntop * 8; i += blockDim.x) lds[top_col(i >> 3, i & 7)] = g[i];
     __syncthreads();
 }
+#if MFX_NODE_F16
+// an FP16 node's four 16-B columns at float4 n * 8 + (c ^ ((n >> 1) & 3))
+__device__ __forceinline__ void load_top_nodes_h(float4* lds, const MfxNodeH* __restrict__ nodes, int ntop) {
+    const float4* __restrict__ g = (const float4*)nodes;
+    for (int i = threadIdx.x; i < ntop * 4; i += blockDim.x) lds[(i >> 2) * 8 + ((i & 3) ^ ((i >> 3) & 3))] = g[i];
+    __syncthreads();
+}
+typedef _Float16 mfx_h2 __attribute__((ext_vector_type(2)));
+// four FP16 planes (two dwords) as floats
+__device__ __forceinline__ float4 h4f(uint32_t a, uint32_t b) {
+    const mfx_h2 x = __builtin_bit_cast(mfx_h2, a), y = __builtin_bit_cast(mfx_h2, b);
+    return make_float4((float)x.x, (float)x.y, (float)y.x, (float)y.y);
+}
+#endif
 
 // Two-level frame bookkeeping after a step or a pop. A lane in an instance remembers the stack
 // depth at which it entered (inst_sp): entries below it belong to the world frame, so a pop below
@@ -784,10 +800,66 @@ __device__ __forceinline__ uint64_t diag_clock() {
     __builtin_amdgcn_sched_barrier(0);
     return t;
 }
+#if MFX_NODE_F16
+// node_step on the FP16 node (VERDICT r05 Next #4b): four 16-B loads instead of seven, the planes
+// widened exactly (v_cvt_f32_f16), then the same FP32 slab test, order and pushes. The boxes are the
+// FP32 ones rounded outward, so a lane visits a superset of its FP32 walk's nodes; the leaf tests
+// decide the hits (§3), and the images are the same bits
+template <bool TOP, bool FAR, typename ST>
+__device__ __forceinline__ int node_step_h(int node, const RayF& r, float tlim, const ST& stack, int& sp, TopNodes tn,
+                                           uint64_t* lat) {
+    const bool dp = stack.deep(sp + 3);
+    const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
+    const uint64_t t_issue = lat ? diag_clock() : 0;
+    uint4 A, B, C;
+    int4 ch;
+    if (TOP && node < tn.ntop) {
+        const int sw = (node >> 1) & 3;
+        const uint4* t = (const uint4*)tn.lds + node * 8;
+        A = t[0 ^ sw]; B = t[1 ^ sw]; C = t[2 ^ sw];
+        const uint4 c4 = t[3 ^ sw];
+        ch = make_int4((int)c4.x, (int)c4.y, (int)c4.z, (int)c4.w);
+    } else {
+        const uint4* __restrict__ q = (const uint4*)(tn.nodes_h + node);
+        A = q[0]; B = q[1]; C = q[2];
+        ch = *(const int4*)(q + 3);
+    }
+    Slab4 SL;
+    slab4(h4f(A.x, A.y), h4f(A.z, A.w), h4f(B.x, B.y), h4f(B.z, B.w), h4f(C.x, C.y), h4f(C.z, C.w), r, SL);
+    if (lat) *lat += diag_clock() - t_issue;
+    float d[4];
+    int c[4] = {ch.x, ch.y, ch.z, ch.w};
+    int nh = 0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float a0 = SL.a0[k], a1 = SL.a1[k], b0 = SL.b0[k], b1 = SL.b1[k], c0 = SL.c0[k], c1 = SL.c1[k];
+        const float n = fmaxf(fmaxf(fminf(a0, a1), fminf(b0, b1)), fmaxf(fminf(c0, c1), 0.0f));
+        const float f = fminf(fminf(fmaxf(a0, a1), fmaxf(b0, b1)), fminf(fmaxf(c0, c1), tlim));
+        const bool h = n <= f;
+        d[k] = h ? (FAR ? -f : n) : __builtin_inff();
+        nh += h ? 1 : 0;
+    }
+    cswap(d[0], c[0], d[1], c[1]);
+    cswap(d[2], c[2], d[3], c[3]);
+    cswap(d[0], c[0], d[2], c[2]);
+    cswap(d[1], c[1], d[3], c[3]);
+    cswap(d[1], c[1], d[2], c[2]);
+    if (nh >= 2) stack.put(sp, nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]), dp);
+    if (nh >= 3) stack.put(sp + 1, nh == 4 ? c[2] : c[1], dp);
+    if (nh >= 4) stack.put(sp + 2, c[1], dp);
+    const bool pop = nh == 0 && sp > 0;
+    const int next = nh > 0 ? c[0] : (pop ? top : MFX_TRAV_EXIT);
+    sp += nh > 0 ? nh - 1 : (pop ? -1 : 0);
+    return next;
+}
+#endif
 template <bool TOP = false, bool FAR = false, typename ST>
 __device__ __forceinline__ int node_step(const MfxNode* __restrict__ nodes, int node, const RayF& r, float tlim,
                                          const ST& stack, int& sp, TopNodes tn = TopNodes{nullptr, 0},
                                          uint64_t* lat = nullptr) {
+#if MFX_NODE_F16
+    if (tn.nodes_h) return node_step_h<TOP, FAR>(node, r, tlim, stack, sp, tn, lat);
+#endif
     const bool dp = stack.deep(sp + 3);  // this step reads sp - 1 and may write sp .. sp + 2
     const int top = stack.get(sp > 0 ? sp - 1 : 0, dp);
     const uint64_t t_issue = lat ? diag_clock() : 0;
@@ -861,22 +933,6 @@ __device__ __forceinline__ void cswap3(float& da, int& ca, uint64_t& ma, float& 
     cb = s ? u : cb;
     mb = s ? w : mb;
 }
-// the same network over (integer key, child, lane mask) held in scalar registers
-__device__ __forceinline__ void cswap3u(uint32_t& da, int& ca, uint64_t& ma, uint32_t& db, int& cb, uint64_t& mb) {
-    const bool s = db < da;
-    const uint32_t t = da;
-    const int u = ca;
-    const uint64_t w = ma;
-    da = s ? db : da;
-    ca = s ? cb : ca;
-    ma = s ? mb : ma;
-    db = s ? t : db;
-    cb = s ? u : cb;
-    mb = s ? w : mb;
-}
-#ifndef MFX_PACKET_SORT
-#define MFX_PACKET_SORT 0  // the packet step's child sort: 0 float keys (vector compares), 1 integer keys (scalar), 2 packed index keys
-#endif
 // The node columns (MfxNode: lo x, hi x, lo y, hi y, lo z, hi z as float4 over the four children)
 // of the near and far planes per axis, for a packet whose active lanes' directions share their signs
 // on every axis (the camera rays of almost every tile): a child's near plane on an axis is its lo
@@ -901,8 +957,8 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
                                                 const RayF& r, float tlim, int* stk, uint64_t* stm, int& sp, int rep,
                                                 const PacketPlanes& pp) {
     mfx_cf4* q = (mfx_cf4*)(nodes + node);
-    const mfx_i4 ch = ((mfx_ci4*)q)[6];
     float n[4], f[4];
+    const mfx_i4 ch = ((mfx_ci4*)q)[6];
     if (UNI) {
         const mfx_f4 NX = q[pp.nx], FX = q[pp.fx], NY = q[pp.ny], FY = q[pp.fy], NZ = q[pp.nz], FZ = q[pp.fz];
 #pragma unroll
@@ -928,7 +984,6 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
     int c[4] = {ch.x, ch.y, ch.z, ch.w};
     uint64_t m[4];
     int nh = 0;
-#if MFX_PACKET_SORT == 0
     float d[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -948,50 +1003,6 @@ __device__ __forceinline__ int packet_node_step(const MfxNode* __restrict__ node
     cswap3(d[1], c[1], m[1], d[3], c[3], m[3]);
     cswap3(d[1], c[1], m[1], d[2], c[2], m[2]);
     nh = __builtin_amdgcn_readfirstlane(nh);
-#else
-    // integer keys on the scalar unit: entry distances are >= 0, where IEEE order is the bits' order
-    // (the sign bit cleared: a -0 sorts as the 0 it compares equal to)
-    uint32_t d[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        m[k] = __builtin_amdgcn_ballot_w64(n[k] <= f[k]) & mask;
-        const bool h = __builtin_amdgcn_inverse_ballot_w64(m[k]);
-        const uint32_t kd = (uint32_t)__builtin_amdgcn_readlane(__float_as_int(h ? n[k] : 3.0e38f), rep) & 0x7fffffffu;
-        d[k] = m[k] ? kd : 0x7f800000u;
-        nh += m[k] ? 1 : 0;
-    }
-#if MFX_PACKET_SORT == 1
-    cswap3u(d[0], c[0], m[0], d[1], c[1], m[1]);
-    cswap3u(d[2], c[2], m[2], d[3], c[3], m[3]);
-    cswap3u(d[0], c[0], m[0], d[2], c[2], m[2]);
-    cswap3u(d[1], c[1], m[1], d[3], c[3], m[3]);
-    cswap3u(d[1], c[1], m[1], d[2], c[2], m[2]);
-#else
-    // the child's index in the key's two low bits (ties within 4 ulps break by index: the visit
-    // order only steers the walk, every order gives the same hits), sorted by min / max alone
-#pragma unroll
-    for (int k = 0; k < 4; ++k) d[k] = (d[k] & ~3u) | (uint32_t)k;
-    const int c0[4] = {c[0], c[1], c[2], c[3]};
-    const uint64_t m0[4] = {m[0], m[1], m[2], m[3]};
-#define MFX_KSWAP(a, b)                          \
-    do {                                         \
-        const uint32_t _lo = min(d[a], d[b]);    \
-        d[b] = max(d[a], d[b]);                  \
-        d[a] = _lo;                              \
-    } while (0)
-    MFX_KSWAP(0, 1);
-    MFX_KSWAP(2, 3);
-    MFX_KSWAP(0, 2);
-    MFX_KSWAP(1, 3);
-    MFX_KSWAP(1, 2);
-#undef MFX_KSWAP
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        c[k] = c0[d[k] & 3];
-        m[k] = m0[d[k] & 3];
-    }
-#endif
-#endif
     if (__lane_id() == 0) {  // the pushes are wave-uniform: one lane writes them
         if (nh >= 2) {
             stk[sp] = nh == 4 ? c[3] : (nh == 3 ? c[2] : c[1]);

@@ -98,6 +98,9 @@ struct WfParams {
     const MfxInstance* inst;  // two-level scenes: instances (null for a flat scene)
     MfxLight light;  // by value: kernel arguments are scalar-loaded, never per-lane gathers (k_resolve)
     const MfxCamera* cam_dev;   // the camera in device memory: k_camera copies it into LDS
+#if MFX_NODE_F16
+    const MfxNodeH* nodes_h;    // MFX_NODE_F16 builds: the per-lane kernels' FP16 nodes (else null)
+#endif
     const MfxLight* light_dev;
     const void* const* refs_dev;  // {slot_ref, ref_blob} in device memory (k_shadow copies them into LDS)  // the same in device memory: k_shadow copies it into LDS, so its 52
                                 // dwords are not held in scalar registers through the kernel's loops

@@ -469,8 +469,16 @@ template <bool STATS, bool SPILL, int SK, bool Q, bool START = false>
 __global__ void __launch_bounds__(256, MFX_TRAV_WAVES) k_extend(WfParams P) {
     constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
+#if MFX_NODE_F16
+    const TopNodes tn{(const float4*)lds_all, P.ntop_ext, P.nodes_h};
+#else
     const TopNodes tn{(const float4*)lds_all, P.ntop_ext};
-    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
+#endif
+#if MFX_NODE_F16
+    if (P.nodes_h) load_top_nodes_h((float4*)lds_all, P.nodes_h, P.ntop_ext);
+    else
+#endif
+        load_top_nodes((float4*)lds_all, P.nodes, P.ntop_ext);
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_ext * 32);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
@@ -796,7 +804,11 @@ template <bool STATS, bool SPILL, int WAVES, int SK, bool Q>
 __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
     constexpr bool INST = SK == WF_SK_INST, SLDS = SK == WF_SK_SLDS;
     extern __shared__ int lds_all[];
+#if MFX_NODE_F16
+    const TopNodes tn{(const float4*)lds_all, P.ntop_shd, P.nodes_h};
+#else
     const TopNodes tn{(const float4*)lds_all, P.ntop_shd};
+#endif
     MfxInstance* inst_lds = (MfxInstance*)(lds_all + P.ntop_shd * 32);
     int4* slot_lds = (int4*)(inst_lds + (INST ? P.ninst_lds : 0));
     const int nslot = SLDS ? P.nslot_shd : 0;
@@ -819,7 +831,11 @@ __global__ void __launch_bounds__(256, WAVES) k_shadow(WfParams P) {
         *(PixParams*)((ShdPtrs*)(light_lds + 1) + 1) =
             PixParams{P.path_base, P.base_q, P.base_smp, P.sample_base, P.seed, P.width, P.height, P.band_index,
                       P.band_count, P.band_rows, P.part_index, P.part_count, 0};
-    load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
+#if MFX_NODE_F16
+    if (P.nodes_h) load_top_nodes_h((float4*)lds_all, P.nodes_h, P.ntop_shd);
+    else
+#endif
+        load_top_nodes((float4*)lds_all, P.nodes, P.ntop_shd);
     if (INST) load_inst_lds(inst_lds, P.inst, P.ninst_lds);
     if (SLDS) load_slots_lds(slot_lds, P.slots, nslot);
     const MfxLight& LT = *light_lds;

@@ -22,6 +22,10 @@
 #   iterstats:SCENE:SPP  per-bounce node / leaf / primitive visits per ray (scripts/iter_stats.py)
 #   sharetrace:PARTS:NIF rocprofv3 kernel trace of one rank's 1/PARTS share over NIF contexts (comma list)
 #                        (scripts/share_trace.py) and its timeline (scripts/share_timeline.py)
+#   latroofvar:NAME:SCENE[:SPP]  latency roof of build_ab/NAME.so with its stamp builds NAME_st1/_st2
+#   tdvar:NAME:CFG       TD roof of build_ab/NAME.so
+#   vparityab            scripts/variant_parity.py on every build_ab/*.so
+#   churn                trace time of contexts created after others were destroyed (pool cache on / off)
 #   sampletime           mfx_sample's host timeline per band, bench state vs a lone process
 #   sampletrace          mfx_sample under rocprofv3 kernel + memory-copy trace (scripts/sample_trace.py)
 #   sharequeues:K        K strong-share children under a kernel trace: HW queue ids per rank (share_queues.py)
@@ -130,12 +134,30 @@ for step in "$@"; do
       timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a1 --spp ${a2:-64} \
         --out $O/latency_$(basename $a1 .xml).json > $O/latroof.log 2>&1
       tail -5 $O/latroof.log ;;
+    latroofvar)
+      # a variant's latency roof: build_ab/NAME.so with its stamp builds build_ab_st/NAME_st1.so, _st2.so
+      timeout -k 10 900 python3 scripts/latency_roof.py --scene scenes/$a2 --spp ${a3:-64} --lib build_ab/$a1.so \
+        --st1 build_ab_st/${a1}_st1.so --st2 build_ab_st/${a1}_st2.so --st3 none \
+        --out $O/latency_${a1}_$(basename $a2 .xml).json > $O/latroof_$a1.log 2>&1
+      tail -5 $O/latroof_$a1.log ;;
+    tdvar)
+      # the TD roof of build_ab/NAME.so (MFX_LIB_PATH) on config CFG
+      make -s -C scripts/ubench td_gather sload > /dev/null 2>&1 || true
+      MFX_LIB_PATH=$R/build_ab/$a1.so bash scripts/pmc_td_roof.sh ${TAG}_${a1}_$(echo $a2 | tr A-Z a-z) --config $a2 \
+        > $O/td_${a1}_$a2.log 2>&1 ;;
+    vparityab)
+      timeout -k 10 600 python3 scripts/variant_parity.py build_ab/*.so > $O/vparityab.txt 2>&1
+      cat $O/vparityab.txt ;;
+    churn)
+      # a context's trace time after others came and went, pools kept or freed (scripts/context_churn_probe.py)
+      timeout -k 10 600 python3 scripts/context_churn_probe.py > $O/churn.json 2> $O/churn.err
+      cat $O/churn.json ;;
     sampletime)
       # mfx_sample's host timeline (MFX_SAMPLE_TIMING=1: each band's arrival and copy) in bench.py's
       # process state and in a process that only samples (scripts/sample_in_bench_probe.py)
-      SAMPLE_PROBE_SETTINGS=bands4_streams1,unbanded MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
+      SAMPLE_PROBE_SETTINGS=${SAMPLE_PROBE_SETTINGS:-bands4_streams1,unbanded} MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
         python3 scripts/sample_in_bench_probe.py > $O/sampletime_bench.json 2> $O/sampletime_bench.err
-      SAMPLE_PROBE_SETTINGS=bands4_streams1,unbanded MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
+      SAMPLE_PROBE_SETTINGS=${SAMPLE_PROBE_SETTINGS:-bands4_streams1,unbanded} MFX_SAMPLE_TIMING=1 timeout -k 10 300 \
         python3 scripts/sample_in_bench_probe.py --lone > $O/sampletime_lone.json 2> $O/sampletime_lone.err
       (lscpu | grep -i numa; grep Cpus_allowed_list /proc/self/status) > $O/sampletime_numa.txt || true
       cat $O/sampletime_bench.json $O/sampletime_lone.json $O/sampletime_numa.txt ;;

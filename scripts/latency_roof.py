@@ -111,15 +111,19 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--out", default=None)
     ap.add_argument("--simds", type=int, default=1024, help="256 CUs x 4 SIMDs (MI355X)")
+    # a variant's roof (VERDICT r05 Next #4): its library and its own stamp builds
+    ap.add_argument("--lib", default=os.path.join(ROOT, "mafrixraytracing_amd", "libmafrix_rt.so"))
+    ap.add_argument("--st1", default=os.path.join(ROOT, "build_variants", "st1.so"))
+    ap.add_argument("--st2", default=os.path.join(ROOT, "build_variants", "st2.so"))
+    ap.add_argument("--st3", default=os.path.join(ROOT, "build_variants", "st3.so"))
     a = ap.parse_args()
-    lib = os.path.join(ROOT, "mafrixraytracing_amd", "libmafrix_rt.so")
-    prod, shape = parse(run(lib, a.scene, a.spp))
-    st1, _ = parse(run(os.path.join(ROOT, "build_variants", "st1.so"), a.scene, a.spp))
-    st2, _ = parse(run(os.path.join(ROOT, "build_variants", "st2.so"), a.scene, a.spp))
+    prod, shape = parse(run(a.lib, a.scene, a.spp))
+    st1, _ = parse(run(a.st1, a.scene, a.spp))
+    st2, _ = parse(run(a.st2, a.scene, a.spp))
     ebpc, sbpc, _ = shape  # 256-lane blocks per CU = waves per SIMD
     nit = max(r["iter"] for r in prod)
     cam = None
-    st3p = os.path.join(ROOT, "build_variants", "st3.so")
+    st3p = a.st3
     if os.path.exists(st3p):  # k_camera's phases (-DMFX_DIAG_STAMPS=3), VERDICT r05 Next #5
         st3, _ = parse(run(st3p, a.scene, a.spp))
         r = [x for x in st3 if x["iter"] == 1][0]

@@ -29,13 +29,15 @@ def main():
     settings = [("bands8_streams1", {"MFX_SAMPLE_BANDS": "8", "MFX_SAMPLE_COPY_STREAMS": "1"}),
                 ("bands8_streams2", {"MFX_SAMPLE_BANDS": "8", "MFX_SAMPLE_COPY_STREAMS": "2"}),
                 ("bands4_streams1", {"MFX_SAMPLE_BANDS": "4", "MFX_SAMPLE_COPY_STREAMS": "1"}),
-                ("unbanded", {"MFX_SAMPLE_BANDS": "0"})]
+                ("unbanded", {"MFX_SAMPLE_BANDS": "0"}),
+                ("bands4_noprobe", {"MFX_SAMPLE_BANDS": "4", "MFX_COPY_PROBE": "1"}),
+                ("bands4_fp32nodes", {"MFX_SAMPLE_BANDS": "4", "MFX_NODE_F32": "1"})]
     if os.environ.get("SAMPLE_PROBE_SETTINGS"):
         keep = os.environ["SAMPLE_PROBE_SETTINGS"].split(",")
         settings = [x for x in settings if x[0] in keep]
     for rd in range(2):
         for name, env in settings:
-            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS"):
+            for k in ("MFX_SAMPLE_BANDS", "MFX_SAMPLE_COPY_STREAMS", "MFX_COPY_PROBE", "MFX_NODE_F32"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             r = bench.sample_api(a, DEFAULT_SEED, 64)

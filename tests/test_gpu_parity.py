@@ -234,15 +234,21 @@ def test_megakernel_and_wavefront_counters_agree(gpu, monkeypatch):
     from mafrixraytracing_amd.native import NativeContext
     monkeypatch.setenv("MFX_CAMERA_PACKETS", "0")
     a = scene("spot", 96, 54)
+    with NativeContext(a, seed=SEED, flags=MFX_F_COUNT_STATS) as w:  # the per-lane kernels on FP16 nodes
+        w.sample(2)
+        c16 = w.ray_counts()
+    monkeypatch.setenv("MFX_NODE_F32", "1")  # the per-lane kernels on the FP32 nodes the megakernel walks
     with NativeContext(a, seed=SEED, flags=MFX_F_COUNT_STATS) as w:
         w.sample(2)
         cw = w.ray_counts()
     with NativeContext(a, seed=SEED, flags=MFX_F_COUNT_STATS | MFX_F_MEGAKERNEL) as m:
         m.sample(2)
         cm = m.ray_counts()
-    assert np.array_equal(cw[:4], cm[:4])
+    assert np.array_equal(cw[:4], cm[:4]) and np.array_equal(c16[:4], cm[:4])
     # identical traversal algorithm per ray -> identical visit counts
     assert np.array_equal(cw[4:10], cm[4:10])
+    # FP16 boxes contain the FP32 ones: a superset of the visits, the same rays
+    assert np.all(c16[4:10] >= cw[4:10])
 
 
 @pytest.mark.gpu
