@@ -275,6 +275,11 @@ def sample_api(arrays, seed, spp, calls=5, flags=0):
 SHARE_PROCESSES = 3  # fresh processes strong_share runs in (bench.py --strong-share-child)
 
 
+def progress(what):
+    """A line on stderr per phase (the JSON line alone goes to stdout): a long run shows it is alive."""
+    print(f"bench.py: {what} ({time.strftime('%H:%M:%S')})", file=sys.stderr, flush=True)
+
+
 def _hip_stream():
     """A non-blocking HIP stream on the current device, created through the HIP runtime directly."""
     import ctypes as C
@@ -568,8 +573,9 @@ def main():
     # from a process with no GPU context all nine agreed within 0.4 % (r06g, scripts/share_modes.py).
     # Never from a profiled process (the profiler initialised the GPU before this one started).
     share_runs = []
+    # (the metric's configuration only: C3's 1024 spp in three fresh processes would take minutes)
     if (int(os.environ.get("WORLD_SIZE", "1")) == 1 and args.gpus == 1 and args.api == "batch" and not args.no_render_api
-            and not args.megakernel and not _under_profiler()):
+            and not args.megakernel and not _under_profiler() and args.config == "C2"):
         cmd = [sys.executable, os.path.abspath(__file__), "--config", args.config, "--scene", args.scene,
                "--steps", str(args.steps), "--strong-share-child", "0", "0"] + \
               (["--spp", str(args.spp)] if args.spp is not None else [])
@@ -578,6 +584,7 @@ def main():
             if pc.returncode != 0:
                 raise RuntimeError("strong_share child failed: " + pc.stderr[-2000:])
             share_runs.append(json.loads(pc.stdout.strip().splitlines()[-1]))
+            progress(f"strong_share process {len(share_runs)} of {SHARE_PROCESSES} done")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # Rehearsal of the N-rank job on a one-GPU box (tests/test_gpu_distributed.py): every rank on
@@ -684,6 +691,7 @@ def main():
             if devices:
                 ctx.accum_reduce()
 
+    progress(f"{args.warmup} warmup + {args.steps} timed steps")
     for k in range(args.warmup):
         step(k)
     barrier()
@@ -1039,6 +1047,7 @@ def main():
             # the shipped binding's default (fsharp/Native.fs DefaultRenderAhead, native.Scene): Scene.Render
             # served from batches of DEFAULT_RENDER_AHEAD samples
             cf = CONFIG_FLAGS.get(args.config, 0)
+            progress("render_api")
             rapi = render_api(arrays, DEFAULT_SEED, 2 * DEFAULT_RENDER_AHEAD, render_ahead=DEFAULT_RENDER_AHEAD, flags=cf)
             rapi["vs_batch"] = round(rapi["value"] / value, 4)
             rapi["binding_default"] = True
@@ -1046,13 +1055,15 @@ def main():
             plain = render_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
             plain["vs_batch"] = round(plain["value"] / value, 4)
             rapi["without_render_ahead"] = plain
+            progress("sample_api")
             sapi = sample_api(arrays, DEFAULT_SEED, args.spp, flags=cf)
             sapi["vs_batch"] = round(sapi["value"] / value, 4)
             # the shares were measured before this process touched the GPU (share_runs, main's start)
             share = combine_shares(share_runs, value, elapsed / args.steps * 1e3) if share_runs else \
-                {"skipped": "under a profiler"}
+                {"skipped": "under a profiler" if _under_profiler() else "measured on the metric's configuration (C2)"}
         cpu = None
         if ngpu == 1 and not args.no_cpu_baseline:
+            progress("cpu_baseline")
             cpu = cpu_baseline(arrays, args.spp, DEFAULT_SEED, args.cpu_seconds)
         if ngpu == 1 and use_dist:
             par = ("one GPU through the one-process-per-GPU path (process group, attached accumulators, reduce "
