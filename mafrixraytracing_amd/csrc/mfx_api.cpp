@@ -318,64 +318,6 @@ static void ahead_free(mfx_ctx* c) {
     c->ab_cur = -1;
 }
 
-// MFX_POOL_CACHE=1: the path-slot pool of a destroyed context is kept for the next context on its
-// device (one block per device; default: freed at once). A context's trace ran 8 % slower in about one
-// context of six created after others had come and gone in the process (r06y/r06z: mfx_sample's
-// trace 32.8-33.5 against 30.5 ms, the same kernels), and a fresh block of tens of GB after the
-// frees is where that churn shows; taking the block a finished context used avoids it and the
-// allocation itself. A request the block does not fit (smaller, or more than twice its size)
-// frees it first, so the cache never stands between a context and the memory it needs.
-namespace {
-struct CachedPool {
-    int device;
-    void* ptr;
-    size_t bytes;
-};
-std::mutex g_pool_mu;
-std::vector<CachedPool> g_pool_cache;
-bool pool_cache_on() { return getenv("MFX_POOL_CACHE") && atoi(getenv("MFX_POOL_CACHE")) != 0; }
-// the device's cached block when it holds `bytes` without doubling them (its size in *got), else
-// nullptr after freeing it
-void* pool_cache_take(int device, size_t bytes, size_t* got) {
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    if (g_pool_cache.empty()) return nullptr;
-    const bool on = pool_cache_on();
-    void* r = nullptr;
-    for (size_t i = 0; i < g_pool_cache.size(); ++i) {
-        CachedPool& b = g_pool_cache[i];
-        if (b.device != device) continue;
-        if (on && !r && b.bytes >= bytes && b.bytes <= 2 * bytes) {
-            r = b.ptr;
-            *got = b.bytes;
-        } else {
-            (void)hipFree(b.ptr);
-        }
-        g_pool_cache.erase(g_pool_cache.begin() + (long)i);
-        --i;
-    }
-    return r;
-}
-// keep a finished context's pool (the larger of it and the device's cached block)
-void pool_cache_put(int device, void* ptr, size_t bytes) {
-    if (!pool_cache_on()) {
-        (void)hipFree(ptr);
-        return;
-    }
-    std::lock_guard<std::mutex> lk(g_pool_mu);
-    for (CachedPool& b : g_pool_cache) {
-        if (b.device != device) continue;
-        if (b.bytes >= bytes) {
-            (void)hipFree(ptr);
-        } else {
-            (void)hipFree(b.ptr);
-            b.ptr = ptr;
-            b.bytes = bytes;
-        }
-        return;
-    }
-    g_pool_cache.push_back(CachedPool{device, ptr, bytes});
-}
-}  // namespace
 
 static void free_ctx(mfx_ctx* c) {
     if (!c) return;
@@ -390,8 +332,6 @@ static void free_ctx(mfx_ctx* c) {
     if (c->reduce_done) (void)hipEventDestroy(c->reduce_done);
     if (c->d_reduce_stage) (void)hipFree(c->d_reduce_stage);
     if (c->d_merge) (void)hipFree(c->d_merge);
-    if (c->wf_mem) pool_cache_put(c->device, c->wf_mem, c->wf_pool_bytes);  // for the device's next context
-    c->wf_mem = nullptr;
     void* bufs[] = {c->d_nodes, c->d_slots, c->d_slot_ref, c->d_ref_blob, c->d_shade, c->d_inst, c->d_accum_own,
                     c->d_film, c->d_frame, c->d_rgba, c->d_work, c->d_counters, c->d_counters_total, c->wf_mem, c->d_wfctl, c->d_spill, c->d_vscratch, c->d_albedo, c->d_light, c->d_cam, (void*)c->d_refs, c->d_nodes_h};
     for (void* b : bufs)
@@ -874,12 +814,6 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
     // It runs again after the allocation: processes sharing the device (the one-GPU rehearsal of an
     // N-rank job) that checked at the same time must not take the headroom together (r06n: eight
     // ranks' pools left no room for a launch's scratch).
-    size_t cached = 0;
-    if (void* cp = pool_cache_take(c->device, bytes, &cached)) {  // a finished context's pool
-        if (c->wf_mem) (void)hipFree(c->wf_mem);
-        c->wf_mem = cp;
-        c->wf_pool_bytes = cached;
-    } else {
     size_t mfree = 0, mtotal = 0, headroom = 0;
     if (hipMemGetInfo(&mfree, &mtotal) == hipSuccess && mfree > 0) {
         const size_t avail = mfree + (c->wf_mem ? c->wf_pool_bytes : 0);
@@ -912,7 +846,6 @@ static int wf_ensure_pool(mfx_ctx* c, int32_t pool, bool queues) {
                                      std::to_string(mfree >> 20) + " MiB free");
     }
     c->wf_pool_bytes = bytes;
-    }
     char* p = (char*)c->wf_mem;
     auto take = [&](size_t n) { char* r = p; p += (n + 255) & ~(size_t)255; return r; };
     double** dbl[6] = {&c->wf.ox, &c->wf.oy, &c->wf.oz, &c->wf.dx, &c->wf.dy, &c->wf.dz};
@@ -1971,14 +1904,15 @@ static int ahead_render(mfx_ctx* c, uint8_t* rgba) {
 // range of the x-major frame (pixel = x * h + y). The bits are the unbanded path's: a pixel's sum is
 // its own thread's, and the mean is the same division. MFX_SAMPLE_BANDS=0: the unbanded path.
 // Returns 1 (nothing done) when the call is not for it (a device list, no staging memory).
-// mfx_sample's copy stream, chosen by measurement: a stream's device-to-host copies keep the DMA
-// engine their first copy took, and a context's readback ran at ~53 GB/s on some streams and at
-// ~26-31 GB/s on others, stream for stream (r06q-r06s: the same process, call after call; the
-// staging pages and the device on the same NUMA node). So MFX_COPY_PROBE (default 4) candidate
-// streams each copy `bytes` (up to 16 MB) of the frame twice, the second copy timed, and the fastest
-// is kept. Once per context, at its first Sample call.
+// mfx_sample's copy stream. MFX_COPY_PROBE=K (K > 1; an A/B knob, off by default) chooses it by
+// measurement: K candidate streams each copy `bytes` (up to 16 MB) of the frame twice, the second copy
+// timed, and the fastest is kept, once per context. The readback had run at ~53 GB/s in some contexts
+// and ~26-31 GB/s in others; the probe found every candidate of a box alike (29.7 GB/s on one box,
+// r06t: the rate is the box's, not the stream's), and contexts that probed traced 8 % slower in two
+// cases of six (the streams it creates and destroys move the context's hardware queues; r06y, r06z),
+// never without it. One stream, created at the first Sample call, is the default.
 static int pick_copy_stream(mfx_ctx* c, size_t bytes) {
-    int n = 4;
+    int n = 1;
     if (const char* e = getenv("MFX_COPY_PROBE")) n = std::max(1, std::min(8, atoi(e)));
     if (n == 1) {
         HIPCHECK(hipStreamCreateWithFlags(&c->copy_stream, hipStreamNonBlocking));

@@ -1,9 +1,9 @@
 #!/usr/bin/env python3
 """A context's trace time after other contexts came and went in the process (round 6: mfx_sample's
-context traced C2 in 32.8-33.5 ms in about one context of six, 30.5 ms in the others). With a
-long-lived context beside them, as bench.py's line context: six contexts one after another, each
-2 warm + 3 timed 64-spp traces (HIP-event device time), with the finished contexts' pools kept for
-the next one (MFX_POOL_CACHE=1) and freed (=0, the default), interleaved. One JSON line per context."""
+context traced C2 in 32.8-33.5 ms in two contexts of six, 30.5 ms in the others). With a long-lived
+context beside them, as bench.py's line context: twelve contexts one after another, each 2 warm + 3
+timed 64-spp traces (HIP-event device time). (Round 6 ran it with a finished context's pool kept for
+the next one and freed, interleaved: all twelve 30.0-30.2 ms, r06final2.) One JSON line per context."""
 import json
 import os
 import sys
@@ -19,18 +19,16 @@ def main():
     line = NativeContext(a, seed=DEFAULT_SEED)
     line.trace_accumulate(64, 0)
     line.sync()
-    for i in range(6):
-        for cache in ("0", "1"):
-            os.environ["MFX_POOL_CACHE"] = cache
-            with NativeContext(a, seed=DEFAULT_SEED) as c:
-                ms = []
-                for k in range(5):
-                    c.accum_clear()
-                    c.trace_accumulate(64, k * 64)
-                    c.sync()
-                    if k >= 2:
-                        ms.append(round(c.last_trace_ms(), 3))
-            print(json.dumps({"context": i, "pool_cache": cache, "trace_ms": ms}), flush=True)
+    for i in range(12):
+        with NativeContext(a, seed=DEFAULT_SEED) as c:
+            ms = []
+            for k in range(5):
+                c.accum_clear()
+                c.trace_accumulate(64, k * 64)
+                c.sync()
+                if k >= 2:
+                    ms.append(round(c.last_trace_ms(), 3))
+        print(json.dumps({"context": i, "trace_ms": ms}), flush=True)
     line.close()
 
 

@@ -25,7 +25,7 @@
 #   latroofvar:NAME:SCENE[:SPP]  latency roof of build_ab/NAME.so with its stamp builds NAME_st1/_st2
 #   tdvar:NAME:CFG       TD roof of build_ab/NAME.so
 #   vparityab            scripts/variant_parity.py on every build_ab/*.so
-#   churn                trace time of contexts created after others were destroyed (pool cache on / off)
+#   churn                trace time of contexts created after others were destroyed
 #   sampletime           mfx_sample's host timeline per band, bench state vs a lone process
 #   sampletrace          mfx_sample under rocprofv3 kernel + memory-copy trace (scripts/sample_trace.py)
 #   sharequeues:K        K strong-share children under a kernel trace: HW queue ids per rank (share_queues.py)
@@ -149,7 +149,7 @@ for step in "$@"; do
       timeout -k 10 600 python3 scripts/variant_parity.py build_ab/*.so > $O/vparityab.txt 2>&1
       cat $O/vparityab.txt ;;
     churn)
-      # a context's trace time after others came and went, pools kept or freed (scripts/context_churn_probe.py)
+      # a context's trace time after others came and went (scripts/context_churn_probe.py)
       timeout -k 10 600 python3 scripts/context_churn_probe.py > $O/churn.json 2> $O/churn.err
       cat $O/churn.json ;;
     sampletime)

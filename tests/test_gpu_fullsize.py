@@ -120,7 +120,7 @@ def test_full_size_render_ahead_device_list(gpu):
         assert np.array_equal(c1.film_mean(), c2.film_mean())
 
 
-def test_pool_shrinks_when_the_device_is_short_of_memory(gpu, monkeypatch):
+def test_pool_shrinks_when_the_device_is_short_of_memory(gpu):
     """A context created while the device had room, traced after other allocations left it short:
     the wavefront pool's allocation fails, the trace retries with half-size generations until it
     fits (wf_trace), and the accumulator and ray counts equal an unconstrained context's bit for bit.
@@ -128,8 +128,6 @@ def test_pool_shrinks_when_the_device_is_short_of_memory(gpu, monkeypatch):
     at a quarter of the generation, with room for the runtime's own allocations)."""
     import torch
     from mafrixraytracing_amd.native import NativeContext
-    # no pool kept from a finished context (the reference's would serve the short context)
-    monkeypatch.setenv("MFX_POOL_CACHE", "0")
     a = scene("spot")  # 1920 x 1080
     with NativeContext(a, seed=SEED) as ref_ctx:
         ref_ctx.trace_accumulate(64, 0)
@@ -173,25 +171,8 @@ def test_trace_after_a_refused_pool_allocation(gpu, monkeypatch):
         c.trace_accumulate(4, 0)
         want = c.accum_read_mean(4.0)
     monkeypatch.setenv("MFX_POOL_FAIL_ONCE", "1")
-    monkeypatch.setenv("MFX_POOL_CACHE", "0")  # an allocation, not the finished context's kept pool
     with NativeContext(a, seed=SEED) as c:
         c.trace_accumulate(4, 0)
         got = c.accum_read_mean(4.0)
     assert np.array_equal(got, want)
 
-
-def test_a_finished_contexts_pool_serves_the_next_context(gpu, monkeypatch):
-    """MFX_POOL_CACHE=1: mfx_destroy keeps the path-slot pool for the device's next context (one
-    block per device): the next context of the same size traces in it, with the same frame as a
-    context that allocated its own; MFX_POOL_CACHE=0 frees it at once."""
-    from mafrixraytracing_amd.native import NativeContext
-    a = scene("spot", 96, 54)
-    with NativeContext(a, seed=SEED) as c:
-        want = c.sample(3)
-    got = []
-    for cache in ("1", "0", "1"):
-        monkeypatch.setenv("MFX_POOL_CACHE", cache)
-        with NativeContext(a, seed=SEED) as c:
-            got.append(c.sample(3))
-    for g in got:
-        assert np.array_equal(g, want)
