@@ -2,8 +2,9 @@
 """How reproducible one GPU's strong-scaling shares are across fresh processes: runs bench.py's
 strong_share child (bench.py --strong-share-child) REPS times under each environment setting and
 prints every process's slowest-rank ms per N. Settings: GPU_MAX_HW_QUEUES 8 and 16, and
-MFX_SHARE_TORCH_FIRST=1 (torch's stream pools created before the ranks' contexts).
-Usage: share_modes.py [REPS] [inflight]"""
+MFX_SHARE_TORCH_FIRST=1 (torch's stream pools created before the ranks' contexts); `inflight`: 2, 3
+or 4 frames in flight; `pool`: each context's stream from a pool the process creates once
+(MFX_STREAM_POOL=3) against a stream per context. Usage: share_modes.py [REPS] [inflight|pool]"""
 import json
 import os
 import subprocess
@@ -16,6 +17,9 @@ def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     settings = [("hwq8", {"GPU_MAX_HW_QUEUES": "8"}), ("hwq16", {"GPU_MAX_HW_QUEUES": "16"}),
                 ("hwq8_torch_first", {"GPU_MAX_HW_QUEUES": "8", "MFX_SHARE_TORCH_FIRST": "1"})]
+    if len(sys.argv) > 2 and sys.argv[2] == "pool":  # each rank's contexts on streams created once (MFX_STREAM_POOL)
+        settings = [("fresh_streams", {"GPU_MAX_HW_QUEUES": "8"}),
+                    ("stream_pool3", {"GPU_MAX_HW_QUEUES": "8", "MFX_STREAM_POOL": "3"})]
     if len(sys.argv) > 2 and sys.argv[2] == "inflight":  # frames in flight per small share: 3 (default) vs 4
         settings = [("nif3", {"GPU_MAX_HW_QUEUES": "8"}), ("nif4", {"GPU_MAX_HW_QUEUES": "8", "MFX_FRAMES_IN_FLIGHT": "4"}),
                     ("nif2", {"GPU_MAX_HW_QUEUES": "8", "MFX_FRAMES_IN_FLIGHT": "2"})]
